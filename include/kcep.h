@@ -1,0 +1,173 @@
+/*
+ * kcep.h — C-ABI of libkcep.so, the MI355X-native replacement for the
+ * kafkastreams-cep NFA evaluation path.
+ *
+ * The reference evaluates one record at a time inside
+ *   CEPProcessor.process(K,V)            core/.../cep/processor/CEPProcessor.java:134-150
+ *     -> NFA.matchPattern(Event)         core/.../cep/nfa/NFA.java:134-149
+ * with the pattern compiled once by
+ *   new StagesFactory().make(pattern)    core/.../cep/pattern/StagesFactory.java:49-70
+ * This library takes the same pattern (as the byte IR produced by the host DSL,
+ * kcep/pattern.py) and whole batches of records laid out struct-of-arrays in
+ * HBM, grouped by record key in arrival order, and returns the emitted
+ * sequences as a CSR.  A JNI / FFM binding for a Java GpuCEPProcessor is shown
+ * in INTEGRATION.md.
+ *
+ * Threading: a session is used by one thread at a time (the reference's
+ * CEPProcessor is driven single-threaded by its stream task).  Sessions are
+ * independent.  Errors are int status codes; cep_last_error() returns a
+ * thread-local message.  Codes mirror the reference exceptions.
+ */
+#ifndef KCEP_H
+#define KCEP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the reference throws; we return) */
+#define CEP_OK 0
+#define CEP_E_INVALID_PATTERN 1   /* StagesFactory.InvalidPatternException  StagesFactory.java:182-191 */
+#define CEP_E_UNKNOWN_AGGREGATE 2 /* States.UnknownAggregateException        States.java:80-89 */
+#define CEP_E_ILLEGAL_STATE 3     /* missing buffer predecessor  SharedVersionedBufferStoreImpl.java:113-115 */
+#define CEP_E_NPE 4               /* NullPointerException (null strategy, null previous stage, ...) */
+#define CEP_E_ARITHMETIC 5        /* integer "/ by zero" inside a matcher or aggregator */
+#define CEP_E_CLASS_CAST 6        /* state read with another boxed type than it was folded with */
+#define CEP_E_INDEX 7             /* DeweyVersion.addRun out of bounds  DeweyVersion.java:62-67 */
+#define CEP_E_BAD_IR 8            /* malformed pattern IR */
+#define CEP_E_RUN_CAPACITY 9      /* a key exceeded the device run/buffer capacity even after regrowth */
+#define CEP_E_HIP 10              /* HIP runtime error */
+#define CEP_E_ARG 11              /* invalid argument */
+#define CEP_E_UNSUPPORTED 12      /* pattern feature not lowered to the device */
+
+/* evaluation modes */
+#define CEP_MODE_NFA 0            /* in-memory NFA per key (NFATest.java:842-866 semantics) */
+#define CEP_MODE_PROCESSOR 1      /* CEPProcessor semantics: null filter, per-topic high-water mark,
+                                     run queue round-trips ComputationStageSerde (isIgnored dropped) */
+
+/* column types of the value schema */
+#define CEP_T_I32 1
+#define CEP_T_I64 2
+#define CEP_T_F64 3
+
+/* execution path chosen by cep_session_open */
+#define CEP_PATH_STENCIL 1        /* strict single-cardinality patterns: k-event stencil */
+#define CEP_PATH_GENERAL 2        /* full NFA: runs, Dewey versions, shared versioned buffer */
+
+typedef struct cep_pattern cep_pattern;
+typedef struct cep_session cep_session;
+
+typedef struct {
+  int32_t n_stages;        /* compiled stages incl. $final (Stages.getAllStages().size()) */
+  int32_t n_names;         /* distinct stage names; name 0 is "$final" */
+  int32_t n_patterns;      /* user stages (select() calls) */
+  int32_t n_cols;
+  int32_t stencil_ok;      /* 1 if the strict stencil path applies */
+  int32_t stencil_k;       /* number of events per stencil match */
+} cep_pattern_info;
+
+typedef struct {
+  int32_t device;          /* HIP device ordinal */
+  int32_t mode;            /* CEP_MODE_* */
+  int32_t force_path;      /* 0 = auto, else CEP_PATH_* */
+  int32_t reserved;
+  int64_t max_events;      /* capacity of one batch */
+  int64_t max_keys;        /* capacity of distinct keys per batch (0 = max_events) */
+  double arena_scale;      /* general path: per-key workspace multiplier (0 = default 1.0) */
+} cep_opts;
+
+#define CEP_MEM_HOST 0
+#define CEP_MEM_DEVICE 1
+
+/* Batch flags */
+#define CEP_BATCH_OFFSETS_MONOTONE 1  /* per key and topic, offsets strictly increase (no re-delivery) */
+
+/* One batch of records, struct-of-arrays, grouped by key (each key's records
+ * contiguous and in arrival order).  Replaces a sequence of
+ * CEPProcessor.process(key, value) calls; the per-record Event fields of
+ * Event.java:27-123 map to key_id/topic/partition/offset/ts, the value's typed
+ * fields to cols.  Optional arrays may be NULL: valid -> all records valid,
+ * topic/partition -> 0, offset -> record index, ts -> record index. */
+typedef struct {
+  int64_t n;
+  const int32_t* key_id;
+  const uint8_t* valid;       /* 0 = null key or value (CEPProcessor.java:136-138) */
+  const int32_t* topic;
+  const int32_t* partition;
+  const int64_t* offset;
+  const int64_t* ts;
+  int32_t n_cols;
+  int32_t mem;                /* CEP_MEM_HOST or CEP_MEM_DEVICE */
+  const void* const* cols;    /* n_cols typed column pointers (host array of pointers) */
+  uint32_t flags;
+  uint32_t reserved;
+} cep_batch;
+
+/* Emitted sequences of one batch, library-owned, valid until the next
+ * push/collect/close on the session.  Match m was emitted while processing
+ * record match_record[m] (context.forward order of CEPProcessor.java:148),
+ * for key match_key[m].  Its traversal of the shared buffer, final stage
+ * first (SharedVersionedBufferStoreImpl.peek :176-201), is
+ *   entries [ent_off[m], ent_off[m+1]) : (ent_name[i], ent_record[i])
+ * i.e. stage-name id and batch record index.  Sequence.Builder.build(true)
+ * (Sequence.java:504-517) groups these by name in reverse order; helpers in
+ * kcep/sequence.py do it.  Matches are ordered by key (batch order), and per
+ * key in emission order, which is the reference's per-key forward order. */
+typedef struct {
+  int64_t n_matches;
+  int64_t n_entries;
+  const int64_t* match_record;
+  const int32_t* match_key;
+  const int64_t* ent_off;     /* n_matches + 1 */
+  const int32_t* ent_name;
+  const int64_t* ent_record;
+  int32_t path;               /* CEP_PATH_* that produced it */
+  int32_t err;                /* first error (reference exception) of the batch, CEP_OK if none */
+  int64_t err_record;         /* record that raised it (-1 if none) */
+} cep_matches;
+
+/* --- pattern: replaces StagesFactory.make (StagesFactory.java:49-70) --- */
+int cep_compile(const uint8_t* ir, size_t len, cep_pattern** out);
+void cep_pattern_free(cep_pattern* p);
+int cep_pattern_get_info(const cep_pattern* p, cep_pattern_info* out);
+const char* cep_pattern_name(const cep_pattern* p, int32_t name_id);
+/* Compiled stage `sid` (Stages.getAllStages().get(sid), Stage.java:40-252):
+ * name id, StateType (0 BEGIN, 1 NORMAL, 2 FINAL), window, and up to `cap`
+ * edges as (EdgeOperation 0 BEGIN 1 TAKE 2 PROCEED 3 SKIP_PROCEED 4 IGNORE,
+ * target stage id or -1).  Returns the edge count, or -1 for a bad id. */
+int32_t cep_pattern_stage(const cep_pattern* p, int32_t sid, int32_t* name_id, int32_t* type, int64_t* window_ms,
+                          int32_t* ops, int32_t* targets, int32_t cap);
+
+/* --- session: one per stream task (CEPProcessor.init :88-108) --- */
+int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** out);
+void cep_session_close(cep_session* s);
+int cep_session_path(const cep_session* s);
+
+/* --- batch evaluation: replaces NFA.matchPattern per record (NFA.java:134-149) ---
+ * Enqueues the match phase on `stream` (a hipStream_t, NULL = default stream)
+ * and returns without waiting.  Device-resident batches are read in place. */
+int cep_push_batch(cep_session* s, const cep_batch* b, void* stream);
+
+/* Number of matches of the last pushed batch, device-resident (int64 on the
+ * device) so that a caller can chain work without a host sync. */
+const int64_t* cep_device_match_count(const cep_session* s);
+
+/* Waits for the last batch and materialises the host CSR. */
+int cep_collect(cep_session* s, cep_matches* out);
+
+/* Order-independent 64-bit checksum of the last batch's matches, computed on
+ * the device (matches the oracle's orc_baseline checksum); waits. */
+int cep_checksum(cep_session* s, uint64_t* sum, int64_t* n_matches);
+
+/* Kernel timing of the last batch's dominant kernel (HIP events on the launch stream). */
+int cep_last_kernel_ms(cep_session* s, float* ms);
+
+const char* cep_last_error(void);
+const char* cep_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,449 @@
+// compile.cpp — pattern IR -> stage graph (+ device programs).
+//
+// The stage graph follows the reference compiler StagesFactory.make /
+// buildStages (core/.../cep/pattern/StagesFactory.java:49-180): stage ids are
+// assigned $final = 0, then the stages of the LAST pattern first; a pattern
+// gets a main stage (BEGIN or TAKE edge, IGNORE per strategy, PROCEED for
+// TAKE), internal stages for oneOrMore / times(n), and a SKIP_PROCEED edge on
+// its entry stage when optional.  Invalid shapes raise the reference's
+// InvalidPatternException as CEP_E_INVALID_PATTERN.
+//
+// The stencil lowering implements SURVEY Q9: a pattern whose stages are all
+// strict-contiguity, cardinality ONE, not optional, without folds, with
+// pairwise-distinct names and side-effect-free predicates emits, per key, a
+// match at record j iff the k consecutive records j-k+1..j satisfy P1..Pk.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <limits>
+
+#include "kcep_internal.h"
+#include "../../include/kcep.h"
+
+namespace kcep {
+namespace {
+
+struct Reader {
+  const uint8_t* p;
+  size_t n, i = 0;
+  bool bad = false;
+  bool need(size_t k) {
+    if (i + k > n) bad = true;
+    return !bad;
+  }
+  template <class T>
+  T get() {
+    T v{};
+    if (need(sizeof(T))) { memcpy(&v, p + i, sizeof(T)); i += sizeof(T); }
+    return v;
+  }
+  bool str(std::string& s, bool& is_null) {
+    uint16_t len = get<uint16_t>();
+    is_null = len == 0xFFFF;
+    if (is_null || bad) return !bad;
+    if (!need(len)) return false;
+    s.assign(reinterpret_cast<const char*>(p + i), len);
+    i += len;
+    return true;
+  }
+};
+
+int intern(std::vector<std::string>& v, const std::string& s) {
+  auto it = std::find(v.begin(), v.end(), s);
+  if (it != v.end()) return int(it - v.begin());
+  v.push_back(s);
+  return int(v.size() - 1);
+}
+
+ExprP parse_expr(Reader& r, Program& P, int depth) {
+  if (depth > 256 || r.bad) { r.bad = true; return nullptr; }
+  auto e = std::make_shared<Expr>();
+  e->op = r.get<uint8_t>();
+  auto num = [](const ExprP& x) { return x && x->t != T_BOOL; };
+  auto boo = [](const ExprP& x) { return x && x->t == T_BOOL; };
+  switch (e->op) {
+    case OP_TRUE: case OP_FALSE: e->t = T_BOOL; break;
+    case OP_CONST_I32: e->t = T_I32; e->i32 = r.get<int32_t>(); break;
+    case OP_CONST_I64: e->t = T_I64; e->i64 = r.get<int64_t>(); break;
+    case OP_CONST_F64: e->t = T_F64; e->f64 = r.get<double>(); break;
+    case OP_FIELD:
+      e->col = r.get<uint16_t>();
+      if (e->col >= int(P.coltypes.size())) { r.bad = true; return nullptr; }
+      e->t = P.coltypes[e->col];
+      break;
+    case OP_EV_KEY: case OP_EV_PARTITION: e->t = T_I32; break;
+    case OP_EV_TS: case OP_EV_OFFSET: e->t = T_I64; break;
+    case OP_EV_TOPIC_EQ: e->t = T_BOOL; e->i32 = r.get<int32_t>(); break;
+    case OP_STATE_GET: case OP_STATE_GET_OR_ELSE: {
+      e->ct = e->t = r.get<uint8_t>();
+      std::string s; bool isnull;
+      if (!r.str(s, isnull) || isnull) { r.bad = true; return nullptr; }
+      e->name = intern(P.states, s);
+      if (e->op == OP_STATE_GET_OR_ELSE) {
+        e->a = parse_expr(r, P, depth + 1);
+        if (!num(e->a) || e->a->t != e->ct) { r.bad = true; return nullptr; }
+      }
+      if (e->ct < T_I32 || e->ct > T_F64) { r.bad = true; return nullptr; }
+      break;
+    }
+    case OP_FOLD_CURR:
+      e->ct = e->t = r.get<uint8_t>();
+      if (e->ct < T_I32 || e->ct > T_F64) { r.bad = true; return nullptr; }
+      break;
+    case OP_SEQ_AVG:
+      e->col = r.get<uint16_t>();
+      e->t = T_F64;
+      if (e->col >= int(P.coltypes.size())) { r.bad = true; return nullptr; }
+      break;
+    case OP_NOT:
+      e->a = parse_expr(r, P, depth + 1);
+      if (!boo(e->a)) { r.bad = true; return nullptr; }
+      e->t = T_BOOL;
+      break;
+    case OP_AND: case OP_OR:
+      e->a = parse_expr(r, P, depth + 1);
+      e->b = parse_expr(r, P, depth + 1);
+      if (!boo(e->a) || !boo(e->b)) { r.bad = true; return nullptr; }
+      e->t = T_BOOL;
+      break;
+    case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_REM:
+      e->a = parse_expr(r, P, depth + 1);
+      e->b = parse_expr(r, P, depth + 1);
+      if (!num(e->a) || !num(e->b)) { r.bad = true; return nullptr; }
+      e->t = std::max(e->a->t, e->b->t);
+      break;
+    case OP_NEG:
+      e->a = parse_expr(r, P, depth + 1);
+      if (!num(e->a)) { r.bad = true; return nullptr; }
+      e->t = e->a->t;
+      break;
+    case OP_EQ: case OP_NE: case OP_LT: case OP_LE: case OP_GT: case OP_GE:
+      e->a = parse_expr(r, P, depth + 1);
+      e->b = parse_expr(r, P, depth + 1);
+      if (!e->a || !e->b || (e->a->t == T_BOOL) != (e->b->t == T_BOOL)) { r.bad = true; return nullptr; }
+      if (e->a->t == T_BOOL && e->op != OP_EQ && e->op != OP_NE) { r.bad = true; return nullptr; }
+      e->t = T_BOOL;
+      break;
+    case OP_CAST:
+      e->ct = r.get<uint8_t>();
+      e->a = parse_expr(r, P, depth + 1);
+      if (!num(e->a) || e->ct < T_I32 || e->ct > T_F64) { r.bad = true; return nullptr; }
+      e->t = e->ct;
+      break;
+    default: r.bad = true; return nullptr;
+  }
+  return r.bad ? nullptr : e;
+}
+
+ExprP mk(uint8_t op, ExprP a = nullptr, ExprP b = nullptr) {
+  auto e = std::make_shared<Expr>();
+  e->op = op; e->t = T_BOOL; e->a = a; e->b = b;
+  return e;
+}
+ExprP mk_topic(int32_t topic) { auto e = mk(OP_EV_TOPIC_EQ); e->i32 = topic; return e; }
+
+struct BuildErr { int code; std::string msg; };
+
+// StagesFactory.buildStages (StagesFactory.java:77-172)
+std::vector<StageDef> build_stages(Program& P, uint8_t type, int pi, int succ_stage, int succ_pat,
+                                   const std::vector<StageDef>& built, int& next_id) {
+  const PatternDef& pat = P.pats[pi];
+  const bool many = pat.one_or_more;
+  StageDef main{next_id++, pat.name_id, uint8_t(many ? ST_NORMAL : type), -1, pi, {}};
+  int64_t w = pat.window_ms;
+  if (w == -1 && succ_pat >= 0) w = P.pats[succ_pat].window_ms;
+  main.window_ms = w;
+  if (!pat.pred) throw BuildErr{CEP_E_NPE, "pattern '" + pat.name + "' has no predicate"};
+  ExprP pred = pat.topic >= 0 ? mk(OP_AND, mk_topic(pat.topic), pat.pred) : pat.pred;
+  const uint8_t first_op = many ? E_TAKE : E_BEGIN;
+  main.edges.push_back({first_op, pred, succ_stage});
+  if (pat.strategy == S_NULL) throw BuildErr{CEP_E_NPE, "selected strategy is null for '" + pat.name + "'"};
+  ExprP ignore;
+  if (pat.strategy == S_ANY) {
+    ignore = mk(OP_TRUE);
+    main.edges.push_back({E_IGNORE, ignore, -1});
+  } else if (pat.strategy == S_NEXT) {
+    ignore = mk(OP_NOT, pred);
+    main.edges.push_back({E_IGNORE, ignore, -1});
+  }
+  const bool succ_final = built[succ_stage].type == ST_FINAL;
+  if (first_op == E_TAKE) {
+    if (succ_pat < 0 && succ_final)
+      throw BuildErr{CEP_E_INVALID_PATTERN, "Cannot define a pattern with a final stage expecting multiple matching events"};
+    const PatternDef& sp = P.pats[succ_pat];
+    ExprP succ = sp.topic >= 0 ? mk(OP_AND, mk_topic(sp.topic), sp.pred) : sp.pred;
+    ExprP proceed = pat.strategy == S_STRICT
+                        ? mk(OP_OR, succ, mk(OP_NOT, pred))
+                        : mk(OP_OR, succ, mk(OP_AND, mk(OP_NOT, pred), mk(OP_NOT, ignore)));
+    main.edges.push_back({E_PROCEED, proceed, succ_stage});
+  }
+  std::vector<StageDef> out{main};
+  int times = pat.times;
+  if (many || times > 1) {
+    do {
+      StageDef in{next_id++, pat.name_id, type, w, pi, {}};
+      in.edges.push_back({E_BEGIN, pred, out.back().id});
+      if (ignore) in.edges.push_back({E_IGNORE, ignore, -1});
+      out.push_back(in);
+    } while (--times > 1);
+  }
+  if (pat.optional) {
+    if (succ_pat < 0 && succ_final)
+      throw BuildErr{CEP_E_INVALID_PATTERN, "Cannot define a pattern with an optional final stage"};
+    // the successor predicate without its topic filter (StagesFactory.java:165)
+    out.back().edges.push_back({E_SKIP_PROCEED, mk(OP_AND, P.pats[succ_pat].pred, mk(OP_NOT, pred)), succ_stage});
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------- stencil DNF
+struct Range { int64_t lo, hi; double dlo, dhi; };
+struct Term { bool has_v = false, has_t = false; Range v{}, t{}; };
+using DNF = std::vector<Term>;
+
+constexpr int64_t IMIN = std::numeric_limits<int64_t>::min();
+constexpr int64_t IMAX = std::numeric_limits<int64_t>::max();
+
+struct Lowering {
+  int col = -1;
+  uint8_t coltype = 0;
+  bool ok = true;
+  std::string why;
+
+  void fail(const std::string& w) { if (ok) { ok = false; why = w; } }
+
+  static bool empty(const Range& r, bool isf) { return isf ? !(r.dlo <= r.dhi) : r.lo > r.hi; }
+
+  bool intersect(Term& a, const Term& b) {
+    bool isf = coltype == T_F64;
+    if (b.has_v) {
+      if (!a.has_v) { a.has_v = true; a.v = b.v; }
+      else {
+        a.v.lo = std::max(a.v.lo, b.v.lo); a.v.hi = std::min(a.v.hi, b.v.hi);
+        a.v.dlo = std::max(a.v.dlo, b.v.dlo); a.v.dhi = std::min(a.v.dhi, b.v.dhi);
+      }
+      if (empty(a.v, isf)) return false;
+    }
+    if (b.has_t) {
+      if (!a.has_t) { a.has_t = true; a.t = b.t; }
+      else { a.t.lo = std::max(a.t.lo, b.t.lo); a.t.hi = std::min(a.t.hi, b.t.hi); }
+      if (a.t.lo > a.t.hi) return false;
+    }
+    return true;
+  }
+
+  DNF conj(const DNF& x, const DNF& y) {
+    DNF out;
+    for (auto& a : x)
+      for (auto& b : y) {
+        Term t = a;
+        if (intersect(t, b)) out.push_back(t);
+      }
+    if (out.size() > STENCIL_MAX_TERMS) fail("predicate needs too many terms");
+    return out;
+  }
+
+  static DNF int_cmp(uint8_t op, int64_t k, bool topic) {
+    auto mkT = [&](int64_t lo, int64_t hi) {
+      Term t;
+      if (topic) { t.has_t = true; t.t.lo = lo; t.t.hi = hi; }
+      else { t.has_v = true; t.v.lo = lo; t.v.hi = hi; }
+      return t;
+    };
+    DNF d;
+    switch (op) {
+      case OP_EQ: d.push_back(mkT(k, k)); break;
+      case OP_NE:
+        if (k != IMIN) d.push_back(mkT(IMIN, k - 1));
+        if (k != IMAX) d.push_back(mkT(k + 1, IMAX));
+        break;
+      case OP_LT: if (k != IMIN) d.push_back(mkT(IMIN, k - 1)); break;
+      case OP_LE: d.push_back(mkT(IMIN, k)); break;
+      case OP_GT: if (k != IMAX) d.push_back(mkT(k + 1, IMAX)); break;
+      case OP_GE: d.push_back(mkT(k, IMAX)); break;
+    }
+    return d;
+  }
+
+  static uint8_t flip(uint8_t op) {
+    switch (op) { case OP_LT: return OP_GT; case OP_LE: return OP_GE; case OP_GT: return OP_LT; case OP_GE: return OP_LE; }
+    return op;
+  }
+  static uint8_t negate(uint8_t op) {
+    switch (op) {
+      case OP_EQ: return OP_NE; case OP_NE: return OP_EQ; case OP_LT: return OP_GE;
+      case OP_GE: return OP_LT; case OP_LE: return OP_GT; case OP_GT: return OP_LE;
+    }
+    return op;
+  }
+
+  DNF lower(const ExprP& e, bool neg) {
+    if (!ok) return {};
+    switch (e->op) {
+      case OP_TRUE: case OP_FALSE: {
+        bool v = (e->op == OP_TRUE) != neg;
+        return v ? DNF{Term{}} : DNF{};
+      }
+      case OP_NOT: return lower(e->a, !neg);
+      case OP_AND: case OP_OR: {
+        bool is_and = (e->op == OP_AND) != neg;
+        DNF x = lower(e->a, neg), y = lower(e->b, neg);
+        if (is_and) return conj(x, y);
+        x.insert(x.end(), y.begin(), y.end());
+        if (x.size() > STENCIL_MAX_TERMS) fail("predicate needs too many terms");
+        return x;
+      }
+      case OP_EV_TOPIC_EQ: return int_cmp(neg ? OP_NE : OP_EQ, e->i32, true);
+      case OP_EQ: case OP_NE: case OP_LT: case OP_LE: case OP_GT: case OP_GE: {
+        ExprP f = e->a, c = e->b;
+        uint8_t op = e->op;
+        if (f->op != OP_FIELD) { std::swap(f, c); op = flip(op); }
+        if (f->op != OP_FIELD || !(c->op == OP_CONST_I32 || c->op == OP_CONST_I64 || c->op == OP_CONST_F64)) {
+          fail("predicate is not a column/constant comparison");
+          return {};
+        }
+        if (col >= 0 && f->col != col) { fail("predicates read more than one column"); return {}; }
+        col = f->col;
+        coltype = f->t;
+        if (neg) op = negate(op);
+        if (f->t == T_F64) {
+          if (op == OP_NE || neg) { fail("negated comparison on a double column (NaN)"); return {}; }
+          double k = c->op == OP_CONST_F64 ? c->f64 : c->op == OP_CONST_I32 ? double(c->i32) : double(c->i64);
+          Term t; t.has_v = true;
+          t.v.dlo = -INFINITY; t.v.dhi = INFINITY;
+          switch (op) {
+            case OP_EQ: t.v.dlo = t.v.dhi = k; break;
+            case OP_LT: t.v.dhi = nextafter(k, -INFINITY); break;
+            case OP_LE: t.v.dhi = k; break;
+            case OP_GT: t.v.dlo = nextafter(k, INFINITY); break;
+            case OP_GE: t.v.dlo = k; break;
+          }
+          if (isnan(k)) return {};
+          return DNF{t};
+        }
+        if (c->op == OP_CONST_F64) { fail("integer column compared with a double constant"); return {}; }
+        int64_t k = c->op == OP_CONST_I32 ? int64_t(c->i32) : c->i64;
+        return int_cmp(op, k, false);
+      }
+      default:
+        fail("predicate uses state, sequence, arithmetic or event metadata");
+        return {};
+    }
+  }
+};
+
+void analyse_stencil(Program& P) {
+  auto no = [&](const std::string& w) { P.stencil_ok = false; P.stencil_why = w; };
+  const int k = int(P.pats.size());
+  if (k > STENCIL_MAX_K) return no("more than 8 stages");
+  for (int i = 0; i < k; i++) {
+    const auto& p = P.pats[i];
+    if (p.strategy != S_STRICT) return no("non-strict selection strategy");
+    if (p.one_or_more || p.times > 1 || p.optional) return no("quantifier");
+    if (!p.folds.empty()) return no("fold");
+    for (int j = 0; j < i; j++)
+      if (P.pats[j].name_id == p.name_id) return no("duplicate stage names");
+  }
+  Lowering L;
+  StencilProgram& S = P.stencil;
+  memset(&S, 0, sizeof S);
+  S.k = k;
+  for (int i = 0; i < k && L.ok; i++) {
+    const auto& p = P.pats[i];
+    ExprP pred = p.topic >= 0 ? mk(OP_AND, mk_topic(p.topic), p.pred) : p.pred;
+    DNF d = L.lower(pred, false);
+    if (!L.ok) break;
+    if (d.size() > STENCIL_MAX_TERMS) { L.fail("too many terms"); break; }
+    S.nterms[i] = int(d.size());
+    S.name[i] = p.name_id;
+    for (size_t t = 0; t < d.size(); t++) {
+      const Term& tm = d[t];
+      S.vi[i][t] = tm.has_v ? StencilAtomI{tm.v.lo, tm.v.hi} : StencilAtomI{IMIN, IMAX};
+      S.vf[i][t] = tm.has_v ? StencilAtomF{tm.v.dlo, tm.v.dhi} : StencilAtomF{-INFINITY, INFINITY};
+      S.tp[i][t] = tm.has_t ? StencilAtomI{tm.t.lo, tm.t.hi} : StencilAtomI{IMIN, IMAX};
+      S.hasv[i][t] = tm.has_v ? 1 : 0;
+      if (tm.has_t) S.use_topic = 1;
+    }
+  }
+  if (!L.ok) return no(L.why);
+  if (L.col < 0) { L.col = 0; L.coltype = P.coltypes.empty() ? T_I32 : P.coltypes[0]; }
+  S.col = L.col;
+  S.coltype = L.coltype;
+  P.stencil_ok = true;
+  P.stencil_why.clear();
+}
+
+}  // namespace
+
+int compile_ir(const uint8_t* ir, size_t len, Program& P, std::string& err) {
+  Reader r{ir, len};
+  if (len < 8 || memcmp(ir, "KCEP", 4) != 0) { err = "bad magic"; return CEP_E_BAD_IR; }
+  r.i = 4;
+  if (r.get<uint32_t>() != 1) { err = "unsupported IR version"; return CEP_E_BAD_IR; }
+  uint16_t ncols = r.get<uint16_t>();
+  for (int i = 0; i < ncols; i++) {
+    uint8_t t = r.get<uint8_t>();
+    if (t < T_I32 || t > T_F64) r.bad = true;
+    P.coltypes.push_back(t);
+  }
+  P.names.push_back("$final");
+  uint16_t npat = r.get<uint16_t>();
+  if (npat == 0) r.bad = true;
+  for (int i = 0; i < npat && !r.bad; i++) {
+    PatternDef pd;
+    bool isnull = false;
+    r.str(pd.name, isnull);
+    pd.level = r.get<int32_t>();
+    if (isnull) pd.name = std::to_string(pd.level);            // Pattern.getName (Pattern.java:181-183)
+    pd.name_id = intern(P.names, pd.name);
+    pd.strategy = r.get<uint8_t>();
+    pd.topic = r.get<int32_t>();
+    pd.one_or_more = r.get<uint8_t>();
+    pd.optional = r.get<uint8_t>();
+    pd.times = r.get<int32_t>();
+    pd.window_ms = r.get<int64_t>();
+    if (r.get<uint8_t>()) pd.pred = parse_expr(r, P, 0);
+    uint16_t nf = r.get<uint16_t>();
+    for (int f = 0; f < nf && !r.bad; f++) {
+      std::string s;
+      if (!r.str(s, isnull) || isnull) { r.bad = true; break; }
+      Fold fd;
+      fd.state = intern(P.states, s);
+      fd.type = r.get<uint8_t>();
+      fd.expr = parse_expr(r, P, 0);
+      if (!fd.expr || fd.expr->t == T_BOOL || fd.type < T_I32 || fd.type > T_F64) r.bad = true;
+      pd.folds.push_back(fd);
+    }
+    P.pats.push_back(std::move(pd));
+  }
+  if (r.bad || r.i != len) { err = "malformed pattern IR"; return CEP_E_BAD_IR; }
+
+  // StagesFactory.make (StagesFactory.java:49-70)
+  try {
+    int next_id = 0;
+    P.stages.push_back(StageDef{next_id++, 0, ST_FINAL, -1, -1, {}});
+    int succ_stage = 0, succ_pat = -1;
+    for (int cur = int(P.pats.size()) - 1; cur >= 0; cur--) {
+      auto st = build_stages(P, cur > 0 ? ST_NORMAL : ST_BEGIN, cur, succ_stage, succ_pat, P.stages, next_id);
+      for (auto& s : st) P.stages.push_back(std::move(s));
+      succ_stage = int(P.stages.size()) - 1;
+      succ_pat = cur;
+    }
+  } catch (const BuildErr& e) {
+    err = e.msg;
+    return e.code;
+  }
+  for (auto& s : P.stages)                                       // Stages.getBeginingStage (Stages.java:49-51)
+    if (s.type == ST_BEGIN) { P.begin = s.id; break; }
+  for (auto& s : P.stages) {                                     // Stages.getDefinedStates (Stages.java:62-67)
+    if (s.pattern < 0) continue;
+    for (auto& f : P.pats[s.pattern].folds)
+      if (std::find(P.defined_states.begin(), P.defined_states.end(), f.state) == P.defined_states.end())
+        P.defined_states.push_back(f.state);
+  }
+  analyse_stencil(P);
+  return CEP_OK;
+}
+
+}  // namespace kcep

@@ -1,0 +1,209 @@
+"""ctypes binding of libkcep.so (include/kcep.h).
+
+This is the only way the Python host reaches the matcher: there is no Python
+or CPU evaluation path behind it.  If the shared library is missing the
+import of the binding fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libkcep.so")
+
+CEP_OK = 0
+ERRORS = {
+    1: "InvalidPatternException", 2: "UnknownAggregateException", 3: "IllegalStateException",
+    4: "NullPointerException", 5: "ArithmeticException", 6: "ClassCastException",
+    7: "ArrayIndexOutOfBoundsException", 8: "BadIR", 9: "RunCapacity", 10: "HipError", 11: "BadArgument",
+    12: "Unsupported",
+}
+MODE_NFA, MODE_PROCESSOR = 0, 1
+PATH_STENCIL, PATH_GENERAL = 1, 2
+MEM_HOST, MEM_DEVICE = 0, 1
+BATCH_OFFSETS_MONOTONE = 1
+
+
+class CepError(RuntimeError):
+    def __init__(self, code: int, msg: str, record: int = -1):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}" + (f" (record {record})" if record >= 0 else ""))
+        self.code = code
+        self.record = record
+
+
+class PatternInfo(C.Structure):
+    _fields_ = [("n_stages", C.c_int32), ("n_names", C.c_int32), ("n_patterns", C.c_int32),
+                ("n_cols", C.c_int32), ("stencil_ok", C.c_int32), ("stencil_k", C.c_int32)]
+
+
+class Opts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("mode", C.c_int32), ("force_path", C.c_int32), ("reserved", C.c_int32),
+                ("max_events", C.c_int64), ("max_keys", C.c_int64), ("arena_scale", C.c_double)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n", C.c_int64), ("key_id", C.c_void_p), ("valid", C.c_void_p), ("topic", C.c_void_p),
+                ("partition", C.c_void_p), ("offset", C.c_void_p), ("ts", C.c_void_p), ("n_cols", C.c_int32),
+                ("mem", C.c_int32), ("cols", C.POINTER(C.c_void_p)), ("flags", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class Matches(C.Structure):
+    _fields_ = [("n_matches", C.c_int64), ("n_entries", C.c_int64), ("match_record", C.POINTER(C.c_int64)),
+                ("match_key", C.POINTER(C.c_int32)), ("ent_off", C.POINTER(C.c_int64)),
+                ("ent_name", C.POINTER(C.c_int32)), ("ent_record", C.POINTER(C.c_int64)),
+                ("path", C.c_int32), ("err", C.c_int32), ("err_record", C.c_int64)]
+
+
+SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_pattern_name", "cep_pattern_stage",
+           "cep_session_open",
+           "cep_session_close", "cep_session_path", "cep_push_batch", "cep_device_match_count", "cep_collect",
+           "cep_checksum", "cep_last_kernel_ms", "cep_last_error", "cep_version"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C kafkastreams-cep_amd` "
+                          "(there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    L.cep_compile.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(P)]
+    L.cep_pattern_free.argtypes = [P]
+    L.cep_pattern_free.restype = None
+    L.cep_pattern_get_info.argtypes = [P, C.POINTER(PatternInfo)]
+    L.cep_pattern_name.argtypes = [P, C.c_int32]
+    L.cep_pattern_name.restype = C.c_char_p
+    L.cep_pattern_stage.argtypes = [P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
+    L.cep_pattern_stage.restype = C.c_int32
+    L.cep_session_open.argtypes = [P, C.POINTER(Opts), C.POINTER(P)]
+    L.cep_session_close.argtypes = [P]
+    L.cep_session_close.restype = None
+    L.cep_session_path.argtypes = [P]
+    L.cep_push_batch.argtypes = [P, C.POINTER(Batch), P]
+    L.cep_device_match_count.argtypes = [P]
+    L.cep_device_match_count.restype = C.c_void_p
+    L.cep_collect.argtypes = [P, C.POINTER(Matches)]
+    L.cep_checksum.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]
+    L.cep_last_kernel_ms.argtypes = [P, C.POINTER(C.c_float)]
+    L.cep_last_error.restype = C.c_char_p
+    L.cep_version.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != CEP_OK:
+        raise CepError(rc, lib().cep_last_error().decode())
+
+
+class CompiledPattern:
+    """``cep_compile`` handle: the device-side equivalent of ``Stages``."""
+
+    def __init__(self, ir: bytes):
+        L = lib()
+        self.h = C.c_void_p()
+        check(L.cep_compile(ir, len(ir), C.byref(self.h)))
+        info = PatternInfo()
+        check(L.cep_pattern_get_info(self.h, C.byref(info)))
+        self.info = info
+        self.names = [L.cep_pattern_name(self.h, i).decode() for i in range(info.n_names)]
+
+    def stages(self):
+        """[(name, type, window, [(op, target)])] in Stages list order."""
+        L = lib()
+        out = []
+        nm, ty = C.c_int32(), C.c_int32()
+        w = C.c_int64()
+        ops = (C.c_int32 * 16)()
+        tg = (C.c_int32 * 16)()
+        for s in range(self.info.n_stages):
+            ne = L.cep_pattern_stage(self.h, s, C.byref(nm), C.byref(ty), C.byref(w), ops, tg, 16)
+            out.append((self.names[nm.value], ty.value, w.value, [(ops[i], tg[i]) for i in range(ne)]))
+        return out
+
+    def close(self):
+        if self.h:
+            lib().cep_pattern_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Session:
+    """One ``cep_session`` (one stream task's processor on one GPU)."""
+
+    def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0):
+        self.pattern = pattern
+        self.h = C.c_void_p()
+        o = Opts(device, mode, force_path, 0, max_events, 0, 0.0)
+        check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
+        self.path = lib().cep_session_path(self.h)
+        self._keep = None
+
+    def close(self):
+        if self.h:
+            lib().cep_session_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, n, key, cols, valid=None, topic=None, partition=None, offset=None, ts=None, mem=MEM_HOST,
+             flags=0, stream=None):
+        """Arrays are numpy arrays (mem=MEM_HOST) or integer device pointers (mem=MEM_DEVICE)."""
+        def ptr(a):
+            if a is None:
+                return None
+            if isinstance(a, int):
+                return a
+            return a.ctypes.data
+
+        colptrs = (C.c_void_p * max(1, len(cols)))(*[ptr(c) for c in cols])
+        b = Batch(int(n), ptr(key), ptr(valid), ptr(topic), ptr(partition), ptr(offset), ptr(ts), len(cols), mem,
+                  colptrs, flags, 0)
+        self._keep = (key, cols, valid, topic, partition, offset, ts, colptrs, b)
+        check(lib().cep_push_batch(self.h, C.byref(b), C.c_void_p(stream) if stream else None))
+
+    def collect(self):
+        m = Matches()
+        check(lib().cep_collect(self.h, C.byref(m)))
+        nm, ne = m.n_matches, m.n_entries
+
+        def arr(p, n, dt):
+            if n == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+        out = dict(match_record=arr(m.match_record, nm, np.int64), match_key=arr(m.match_key, nm, np.int32),
+                   ent_off=arr(m.ent_off, nm + 1, np.int64), ent_name=arr(m.ent_name, ne, np.int32),
+                   ent_record=arr(m.ent_record, ne, np.int64), path=m.path)
+        if m.err:
+            raise CepError(m.err, lib().cep_last_error().decode(), m.err_record)
+        return out
+
+    def checksum(self):
+        s = C.c_uint64()
+        n = C.c_int64()
+        check(lib().cep_checksum(self.h, C.byref(s), C.byref(n)))
+        return n.value, s.value
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        check(lib().cep_last_kernel_ms(self.h, C.byref(ms)))
+        return ms.value

@@ -1,0 +1,80 @@
+"""CPU-side checks of libkcep.so: it loads, exports every symbol of
+include/kcep.h, and its pattern compiler (csrc/compile.cpp, an independent
+restatement of StagesFactory) produces the same stage tables as the oracle.
+No HIP compute call is made here."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from kcep import native as N
+from kcep import synth, Schema, QueryBuilder, Event, Selected
+import oracle as O
+from golden_util import scenarios, load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "kcep.h")).read()
+    return sorted(set(re.findall(r"\b(cep_[a-z_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    L = N.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), f"libkcep.so does not export {s}"
+    assert set(N.SYMBOLS) <= set(syms)
+    assert b"gfx950" in L.cep_version()
+
+
+ALL_IR = [(f["name"], f["ir"]) for f in scenarios()] + [(f["name"], f["ir"]) for f in load("stages_factory.json")]
+
+
+@pytest.mark.parametrize("name,ir", ALL_IR, ids=[n for n, _ in ALL_IR])
+def test_compiler_matches_oracle(name, ir):
+    ir = bytes.fromhex(ir)
+    try:
+        want = O.OraclePattern(ir)
+    except O.OracleError as e:
+        with pytest.raises(N.CepError) as ei:
+            N.CompiledPattern(ir)
+        assert ei.value.code == e.code
+        return
+    got = N.CompiledPattern(ir)
+    assert got.names == want.names
+    assert got.stages() == want.stages()
+
+
+def test_stencil_eligibility():
+    sch = Schema([("value", "i32")])
+    p = N.CompiledPattern(synth.c2_pattern().to_ir(sch))
+    assert p.info.stencil_ok == 1 and p.info.stencil_k == 3
+    for fx in scenarios():
+        cp = N.CompiledPattern(bytes.fromhex(fx["ir"]))
+        eligible = fx["name"] in ("nfa_strict3", "readme_letters", "proc_high_water_mark", "proc_null_key_value")
+        assert bool(cp.info.stencil_ok) == eligible, fx["name"]
+
+
+def test_bad_ir_rejected():
+    sch = Schema([("value", "i32")])
+    ir = synth.c2_pattern().to_ir(sch)
+    for bad in (b"", b"XXXX" + ir[4:], ir[:-1], ir + b"\x00"):
+        with pytest.raises(N.CepError) as ei:
+            N.CompiledPattern(bad)
+        assert ei.value.code == 8
+
+
+def test_null_strategy_is_npe():
+    sch = Schema([("value", "i32")], topics=["t"])
+    p = (QueryBuilder().select("a").where(Event.value() == 0).then()
+         .select("b", Selected.fromTopic("t")).where(Event.value() == 1).build())
+    with pytest.raises(N.CepError) as ei:
+        N.CompiledPattern(p.to_ir(sch))
+    assert ei.value.code == 4
+    with pytest.raises(O.OracleError) as eo:
+        O.OraclePattern(p.to_ir(sch))
+    assert eo.value.code == 4
