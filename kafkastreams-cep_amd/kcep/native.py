@@ -73,6 +73,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C kafkastreams-cep_amd` "
                           "(there is no CPU fallback)")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.  Load
+    # it first so that libkcep.so binds to the same runtime (same SONAME) and
+    # torch tensors, streams and our sessions share one device context.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P = C.c_void_p
     L.cep_compile.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(P)]
