@@ -333,6 +333,70 @@ struct Lowering {
   }
 };
 
+// exact membership of (value, topic) in stage s of the lowered program
+bool stage_accepts(const StencilProgram& S, int s, bool isf, int64_t vi, double vf, int64_t topic) {
+  for (int t = 0; t < S.nterms[s]; t++) {
+    bool ok = true;
+    if (S.hasv[s][t]) ok = isf ? (S.vf[s][t].lo <= vf && vf <= S.vf[s][t].hi) : (S.vi[s][t].lo <= vi && vi <= S.vi[s][t].hi);
+    ok = ok && S.tp[s][t].lo <= topic && topic <= S.tp[s][t].hi;
+    if (ok) return true;
+  }
+  return false;
+}
+
+bool build_table(StencilProgram& S) {
+  const bool isf = S.coltype == T_F64;
+  std::vector<int64_t> bi;
+  std::vector<double> bf;
+  std::vector<int64_t> tb;
+  for (int s = 0; s < S.k; s++)
+    for (int t = 0; t < S.nterms[s]; t++) {
+      if (S.hasv[s][t]) {
+        if (isf) {
+          if (S.vf[s][t].lo > -INFINITY) bf.push_back(S.vf[s][t].lo);
+          if (S.vf[s][t].hi < INFINITY) bf.push_back(nextafter(S.vf[s][t].hi, INFINITY));
+        } else {
+          if (S.vi[s][t].lo > IMIN) bi.push_back(S.vi[s][t].lo);
+          if (S.vi[s][t].hi < IMAX) bi.push_back(S.vi[s][t].hi + 1);
+        }
+      }
+      if (S.tp[s][t].lo > IMIN) tb.push_back(S.tp[s][t].lo);
+      if (S.tp[s][t].hi < IMAX) tb.push_back(S.tp[s][t].hi + 1);
+    }
+  auto uniq = [](auto& v) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); };
+  if (S.coltype == T_I32) {                       // the column is int32: clamp the cut points
+    for (auto& b : bi) b = std::max<int64_t>(b, INT32_MIN);
+    bi.erase(std::remove_if(bi.begin(), bi.end(), [](int64_t b) { return b > INT32_MAX; }), bi.end());
+  }
+  for (auto& b : tb) b = std::max<int64_t>(b, INT32_MIN);   // topic ids are int32
+  tb.erase(std::remove_if(tb.begin(), tb.end(), [](int64_t b) { return b > INT32_MAX; }), tb.end());
+  uniq(bi); uniq(bf); uniq(tb);
+  const int nb = int(isf ? bf.size() : bi.size());
+  if (nb > 15 || tb.size() > 3) return false;
+  S.nbp = nb;
+  S.ntbp = int(tb.size());
+  for (int i = 0; i < nb; i++) { if (isf) S.bpf[i] = bf[i]; else S.bpi[i] = bi[i]; }
+  for (size_t i = 0; i < tb.size(); i++) S.tbp[i] = int32_t(tb[i]);
+  memset(S.table, 0, sizeof S.table);
+  memset(S.nan_mask, 0, sizeof S.nan_mask);
+  for (int it = 0; it <= S.ntbp; it++) {
+    const int64_t trep = it == 0 ? (S.ntbp ? int64_t(S.tbp[0]) - 1 : 0) : int64_t(S.tbp[it - 1]);
+    for (int iv = 0; iv <= nb; iv++) {
+      int64_t vi = 0;
+      double vf = 0;
+      if (isf) vf = iv == 0 ? -INFINITY : bf[iv - 1];
+      else vi = iv == 0 ? (nb ? bi[0] - (bi[0] > IMIN ? 1 : 0) : 0) : bi[iv - 1];
+      uint8_t m = 0;
+      for (int s = 0; s < S.k; s++) m |= uint8_t(stage_accepts(S, s, isf, vi, vf, trep)) << s;
+      S.table[it * 16 + iv] = m;
+    }
+    uint8_t m = 0;
+    for (int s = 0; s < S.k; s++) m |= uint8_t(stage_accepts(S, s, isf, 0, NAN, trep)) << s;
+    S.nan_mask[it] = m;
+  }
+  return true;
+}
+
 void analyse_stencil(Program& P) {
   auto no = [&](const std::string& w) { P.stencil_ok = false; P.stencil_why = w; };
   const int k = int(P.pats.size());
@@ -370,11 +434,149 @@ void analyse_stencil(Program& P) {
   if (L.col < 0) { L.col = 0; L.coltype = P.coltypes.empty() ? T_I32 : P.coltypes[0]; }
   S.col = L.col;
   S.coltype = L.coltype;
+  if (!build_table(S)) return no("predicates cut the value axis into more than 16 intervals");
   P.stencil_ok = true;
   P.stencil_why.clear();
 }
 
+// ---------------------------------------------------------------- bytecode
+struct CodeGen {
+  std::vector<int32_t> code;
+  bool ok = true;
+  std::string why;
+
+  void op(uint8_t o, int a = 0, int b = 0) { code.push_back(int32_t(o) | (a << 8) | (b << 16)); }
+  void push64(int64_t v) {
+    op(BC_PUSH);
+    code.push_back(int32_t(uint32_t(uint64_t(v))));
+    code.push_back(int32_t(uint32_t(uint64_t(v) >> 32)));
+  }
+  int jump(uint8_t o) {
+    op(o);
+    code.push_back(0);
+    return int(code.size()) - 1;
+  }
+  void patch(int at) { code[at] = int32_t(code.size()) - (at + 1); }
+  void cvt(uint8_t from, uint8_t to) {
+    if (from == to || (from == T_I32 && to == T_I64)) return;     // ints are kept sign-extended
+    if (to == T_F64) op(BC_I_TO_F64);
+    else if (from == T_F64) op(to == T_I32 ? BC_F64_TO_I32 : BC_F64_TO_I64);
+    else op(BC_I64_TO_I32);
+  }
+  void arith(uint8_t eop, uint8_t t) {
+    static const uint8_t base[3] = {BC_ADD_I32, BC_ADD_I64, BC_ADD_F64};
+    const int k = t == T_I32 ? 0 : t == T_I64 ? 1 : 2;
+    const int off = eop == OP_ADD ? 0 : eop == OP_SUB ? 1 : eop == OP_MUL ? 2 : eop == OP_DIV ? 3 : eop == OP_REM ? 4 : 5;
+    op(uint8_t(base[k] + off));
+  }
+  void gen(const ExprP& e) {
+    if (!ok) return;
+    switch (e->op) {
+      case OP_TRUE: push64(1); break;
+      case OP_FALSE: push64(0); break;
+      case OP_CONST_I32: push64(e->i32); break;
+      case OP_CONST_I64: push64(e->i64); break;
+      case OP_CONST_F64: { int64_t b; memcpy(&b, &e->f64, 8); push64(b); break; }
+      case OP_FIELD: op(BC_FIELD, e->col, e->t); break;
+      case OP_EV_KEY: op(BC_EV_KEY); break;
+      case OP_EV_TS: op(BC_EV_TS); break;
+      case OP_EV_OFFSET: op(BC_EV_OFFSET); break;
+      case OP_EV_PARTITION: op(BC_EV_PARTITION); break;
+      case OP_EV_TOPIC_EQ: op(BC_TOPIC_EQ); code.push_back(e->i32); break;
+      case OP_STATE_GET: op(BC_STATE_GET, e->name, e->ct); break;
+      case OP_STATE_GET_OR_ELSE: {
+        op(BC_STATE_GET_OR_ELSE, e->name, e->ct);
+        code.push_back(0);
+        const int at = int(code.size()) - 1;
+        gen(e->a);
+        patch(at);
+        break;
+      }
+      case OP_FOLD_CURR: op(BC_FOLD_CURR, 0, e->ct); break;
+      case OP_SEQ_AVG: op(BC_SEQ_AVG, e->col); break;
+      case OP_NOT: gen(e->a); op(BC_NOT); break;
+      case OP_AND: { gen(e->a); int j = jump(BC_JZ_KEEP); gen(e->b); patch(j); break; }
+      case OP_OR: { gen(e->a); int j = jump(BC_JNZ_KEEP); gen(e->b); patch(j); break; }
+      case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_REM:
+        gen(e->a); cvt(e->a->t, e->t); gen(e->b); cvt(e->b->t, e->t); arith(e->op, e->t); break;
+      case OP_NEG: gen(e->a); arith(OP_NEG, e->t); break;
+      case OP_EQ: case OP_NE: case OP_LT: case OP_LE: case OP_GT: case OP_GE: {
+        if (e->a->t == T_BOOL) {
+          gen(e->a); gen(e->b); op(e->op == OP_EQ ? BC_EQ_B : BC_NE_B);
+          break;
+        }
+        const uint8_t t = std::max(e->a->t, e->b->t);
+        gen(e->a); cvt(e->a->t, t); gen(e->b); cvt(e->b->t, t);
+        const int off = e->op - OP_EQ;
+        op(uint8_t((t == T_F64 ? BC_EQ_F : BC_EQ_I) + off));
+        break;
+      }
+      case OP_CAST: gen(e->a); cvt(e->a->t, e->ct); break;
+      default: ok = false; why = "unsupported expression opcode"; break;
+    }
+  }
+  int emit(const ExprP& e, uint8_t result_type = 0xFF) {
+    const int at = int(code.size());
+    gen(e);
+    if (result_type != 0xFF) cvt(e->t, result_type);
+    op(BC_END);
+    return at;
+  }
+};
+
 }  // namespace
+
+int lower_general(Program& P, std::string& why) {
+  DevProgram& D = P.dev;
+  memset(&D, 0, sizeof D);
+  if (P.stages.size() > size_t(NFA_MAX_STAGES)) { why = "too many stages"; return CEP_E_UNSUPPORTED; }
+  if (P.states.size() > size_t(NFA_MAX_STATES)) { why = "too many states"; return CEP_E_UNSUPPORTED; }
+  if (P.coltypes.size() > 16) { why = "too many columns"; return CEP_E_UNSUPPORTED; }
+  D.nstages = int32_t(P.stages.size());
+  D.begin = P.begin;
+  D.nstates = int32_t(P.states.size());
+  D.ncols = int32_t(P.coltypes.size());
+  D.maxdepth = D.nstages + 2;
+  for (size_t c = 0; c < P.coltypes.size(); c++) D.coltype[c] = P.coltypes[c];
+  D.ndefined = int32_t(P.defined_states.size());
+  for (size_t i = 0; i < P.defined_states.size(); i++) D.defined[i] = P.defined_states[i];
+  // buffer-node slots: one per (stage name, stage type) pair (Matched.java:31-35)
+  std::vector<std::pair<int, int>> slots;
+  CodeGen cg;
+  for (auto& s : P.stages) {
+    DevStage& d = D.st[s.id];
+    d.name = s.name;
+    d.type = s.type;
+    auto key = std::make_pair(s.name, int(s.type));
+    auto it = std::find(slots.begin(), slots.end(), key);
+    if (it == slots.end()) { slots.push_back(key); it = slots.end() - 1; }
+    d.slot = int32_t(it - slots.begin());
+    if (s.edges.size() > size_t(NFA_MAX_EDGES)) { why = "too many edges"; return CEP_E_UNSUPPORTED; }
+    d.nedges = int32_t(s.edges.size());
+    for (size_t e = 0; e < s.edges.size(); e++) {
+      d.op[e] = s.edges[e].op;
+      d.target[e] = s.edges[e].target;
+      d.pred[e] = s.edges[e].pred ? cg.emit(s.edges[e].pred) : -1;
+    }
+    if (s.pattern >= 0) {
+      const auto& folds = P.pats[s.pattern].folds;
+      if (folds.size() > size_t(NFA_MAX_FOLDS)) { why = "too many folds"; return CEP_E_UNSUPPORTED; }
+      d.nfolds = int32_t(folds.size());
+      for (size_t f = 0; f < folds.size(); f++) {
+        d.fold_state[f] = folds[f].state;
+        d.fold_type[f] = folds[f].type;
+        d.fold_code[f] = cg.emit(folds[f].expr, folds[f].type);
+      }
+    }
+  }
+  if (!cg.ok) { why = cg.why; return CEP_E_UNSUPPORTED; }
+  if (slots.size() > size_t(NFA_MAX_SLOTS)) { why = "too many buffer slots"; return CEP_E_UNSUPPORTED; }
+  if (cg.code.size() > size_t(NFA_MAX_CODE)) { why = "predicate code too large"; return CEP_E_UNSUPPORTED; }
+  D.nslots = int32_t(slots.size());
+  for (size_t i = 0; i < slots.size(); i++) D.slot_name[i] = slots[i].first;
+  memcpy(D.code, cg.code.data(), cg.code.size() * sizeof(int32_t));
+  return CEP_OK;
+}
 
 int compile_ir(const uint8_t* ir, size_t len, Program& P, std::string& err) {
   Reader r{ir, len};
@@ -443,6 +645,7 @@ int compile_ir(const uint8_t* ir, size_t len, Program& P, std::string& err) {
         P.defined_states.push_back(f.state);
   }
   analyse_stencil(P);
+  P.general_ok = lower_general(P, P.general_why) == CEP_OK;
   return CEP_OK;
 }
 

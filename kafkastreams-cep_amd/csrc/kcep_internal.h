@@ -87,6 +87,58 @@ struct StencilProgram {
   StencilAtomF vf[STENCIL_MAX_K][STENCIL_MAX_TERMS];
   StencilAtomI tp[STENCIL_MAX_K][STENCIL_MAX_TERMS];
   int32_t name[STENCIL_MAX_K];       // stage name id of pattern s
+  // Interval table: the breakpoints of every value/topic atom cut the value
+  // (topic) axis into intervals on which each stage predicate is constant, so
+  // a record's k-bit stage mask is table[it * 16 + iv] with iv = #{value
+  // breakpoints <= v} and it = #{topic breakpoints <= topic}.
+  int32_t nbp;                       // value breakpoints (<= 15), sorted ascending
+  int32_t ntbp;                      // topic breakpoints (<= 3)
+  int64_t bpi[15];                   // integer columns (clamped to int32 for i32 columns)
+  double bpf[15];                    // double columns
+  int32_t tbp[3];
+  uint8_t table[64];
+  uint8_t nan_mask[4];               // double columns: mask of a NaN value per topic interval
+};
+
+// ---- general NFA path: flat device program ----
+// Predicates and folds become postfix bytecode over 64-bit slots (ints kept
+// sign-extended, doubles as bits); the compiler inserts Java's binary numeric
+// promotions.  AND/OR short-circuit with conditional jumps so that exceptions
+// (unknown state, / by zero, ...) are raised exactly when Java would.
+enum : uint8_t {
+  BC_END = 0, BC_PUSH, BC_FIELD, BC_EV_KEY, BC_EV_TS, BC_EV_OFFSET, BC_EV_PARTITION, BC_TOPIC_EQ,
+  BC_STATE_GET, BC_STATE_GET_OR_ELSE, BC_FOLD_CURR, BC_SEQ_AVG, BC_NOT, BC_JZ_KEEP, BC_JNZ_KEEP, BC_POP,
+  BC_ADD_I32, BC_SUB_I32, BC_MUL_I32, BC_DIV_I32, BC_REM_I32, BC_NEG_I32,
+  BC_ADD_I64, BC_SUB_I64, BC_MUL_I64, BC_DIV_I64, BC_REM_I64, BC_NEG_I64,
+  BC_ADD_F64, BC_SUB_F64, BC_MUL_F64, BC_DIV_F64, BC_REM_F64, BC_NEG_F64,
+  BC_EQ_I, BC_NE_I, BC_LT_I, BC_LE_I, BC_GT_I, BC_GE_I,
+  BC_EQ_F, BC_NE_F, BC_LT_F, BC_LE_F, BC_GT_F, BC_GE_F,
+  BC_EQ_B, BC_NE_B,
+  BC_I64_TO_I32, BC_I_TO_F64, BC_F64_TO_I32, BC_F64_TO_I64,
+};
+// instruction word: op | a << 8 | b << 16 (a, b: small operands); BC_PUSH is
+// followed by two words (lo, hi); jumps carry a signed word offset in the next word.
+
+constexpr int NFA_MAX_STAGES = 64;
+constexpr int NFA_MAX_EDGES = 4;
+constexpr int NFA_MAX_FOLDS = 8;
+constexpr int NFA_MAX_STATES = 16;
+constexpr int NFA_MAX_SLOTS = 64;
+constexpr int NFA_MAX_CODE = 4096;
+
+struct DevStage {
+  int32_t name, type, slot, nedges, nfolds;
+  int32_t op[NFA_MAX_EDGES], target[NFA_MAX_EDGES], pred[NFA_MAX_EDGES];   // pred: code offset, -1 = TRUE
+  int32_t fold_state[NFA_MAX_FOLDS], fold_type[NFA_MAX_FOLDS], fold_code[NFA_MAX_FOLDS];
+};
+
+struct DevProgram {
+  int32_t nstages, begin, nslots, nstates, ndefined, ncols, mode, maxdepth;
+  int32_t slot_name[NFA_MAX_SLOTS];
+  int32_t defined[NFA_MAX_STATES];
+  int32_t coltype[16];
+  DevStage st[NFA_MAX_STAGES];
+  int32_t code[NFA_MAX_CODE];
 };
 
 struct Program {
@@ -97,12 +149,62 @@ struct Program {
   std::vector<std::string> states;   // aggregate state names
   std::vector<int> defined_states;   // Stages.getDefinedStates()
   int begin = -1;
+  bool general_ok = false;
+  std::string general_why;
+  DevProgram dev{};
   bool stencil_ok = false;
   std::string stencil_why;           // reason the stencil path does not apply
   StencilProgram stencil{};
 };
 
+// ---- launch interfaces shared by abi.cpp and the .hip files ----
+struct StencilLaunch {
+  const int32_t* key;
+  const void* val;
+  const int32_t* topic;
+  int64_t n;
+  const StencilProgram* prog_dev;
+  int k, coltype, use_topic;
+  int32_t* out;
+  int64_t out_cap;
+  uint64_t* status;
+  uint32_t* counter;
+  int64_t* total;
+  uint32_t epoch;
+};
+
+struct NfaCaps {                  // per-key arena capacities, as base + mult * records (words)
+  int32_t q_base, q_mult, seq_base, seq_mult, heap_base, heap_mult, out_base, out_mult;
+};
+
+struct NfaArgs {
+  const DevProgram* P;
+  const int32_t* key;
+  const uint8_t* valid;
+  const int32_t* topic;
+  const int32_t* partition;
+  const int64_t* offset;
+  const int64_t* ts;
+  const void* cols[16];
+  int64_t n;
+  int32_t mode;
+  int32_t nlist;
+  const int64_t* seg_start;       // nseg + 1
+  const int32_t* seg_list;        // segments handled by this launch (nullptr: segment = list index)
+  int32_t* arena;
+  const int64_t* arena_off;       // per list entry, word offset
+  NfaCaps cap;
+  int64_t* res_matches;           // per segment
+  int64_t* res_words;
+  int64_t* res_out;               // device address of the key's output region
+  int32_t* res_err;
+  int64_t* res_err_rec;
+  int32_t* res_overflow;
+  int32_t* overflow_count;
+};
+
 // compile.cpp
+int lower_general(Program& P, std::string& why);
 int compile_ir(const uint8_t* ir, size_t len, Program& out, std::string& err);
 
 }  // namespace kcep

@@ -8,17 +8,21 @@
 // P1..Pk (the traversal is final -> begin, one event per stage).
 //
 // HBM-bound integer streaming: 4 B key + 4/8 B value per record in, 4*k B per
-// match out.  One pass, ordered output:
-//   * 256-thread workgroups, 4096 records per tile, tile ids drawn in launch
-//     order from an atomic counter (so every predecessor tile is resident:
-//     the look-back never waits on an unscheduled tile);
-//   * coalesced 16-B loads of key/value (lane-contiguous), predicate bitmask
-//     per record computed in registers, staged to LDS with a (k-1) halo;
-//   * each thread then scans 16 consecutive records from LDS, block scan of
-//     match counts, decoupled look-back over 8-byte {epoch, flag, count}
-//     granules (agent-scope relaxed atomics, no fences: the granule is the
-//     flag, MI355X_MICROARCH.md "R2"), matches staged in LDS and written as
-//     one contiguous, coalesced run per tile.
+// match out, one pass, ordered output:
+//   * 256-thread workgroups draw a super-tile of ST_SUB x 4096 records with one
+//     atomic (a single counter word saturates near 88 dequeues/us,
+//     MI355X_MICROARCH.md "dequeue"), in launch order, so every predecessor is
+//     resident when a workgroup looks back;
+//   * count phase, per 4096-record tile: lane-contiguous 16-B non-temporal
+//     loads (the next tile is in flight while this one is scanned), stage
+//     bitmask per record from an interval table, keys + masks staged in LDS
+//     with an 8-record halo, 16 consecutive records per thread tested in
+//     registers, block scan; the tile's count is published as soon as known;
+//   * one decoupled look-back per super-tile over 8-byte {epoch, flag, count}
+//     granules (agent-scope relaxed atomics: the granule is the flag, no fence,
+//     MI355X_MICROARCH.md "R2"), then the inclusive prefixes of its tiles;
+//   * write phase: each tile's matches compacted in LDS and written as one
+//     contiguous, coalesced run.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,43 +33,153 @@
 namespace kcep {
 
 constexpr int ST_THREADS = 256;
-constexpr int ST_EPT = 16;                        // records per thread
+constexpr int ST_EPT = 16;                        // records per thread per tile
 constexpr int ST_TILE = ST_THREADS * ST_EPT;      // 4096
+constexpr int ST_SUB = 4;                         // tiles per workgroup (one atomic)
 
 // look-back granule: [63:48] epoch, [47:46] flag, [45:0] value
 constexpr uint64_t LB_AGG = 1, LB_INC = 2;
 __device__ __forceinline__ uint64_t lb_pack(uint32_t epoch, uint64_t flag, uint64_t v) {
   return (uint64_t(epoch) << 48) | (flag << 46) | (v & ((1ull << 46) - 1));
 }
-
-template <class VT>
-__device__ __forceinline__ uint32_t stage_mask(const StencilProgram* __restrict__ P, int k, VT v, int32_t topic,
-                                               bool use_topic) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int s = 0; s < STENCIL_MAX_K; s++) {
-    if (s >= k) break;
-    const int nt = P->nterms[s];
-    bool any = false;
-    for (int t = 0; t < nt; t++) {
-      bool ok;
-      if (!P->hasv[s][t]) ok = true;
-      else if constexpr (std::is_same<VT, double>::value) ok = P->vf[s][t].lo <= double(v) && double(v) <= P->vf[s][t].hi;
-      else ok = P->vi[s][t].lo <= int64_t(v) && int64_t(v) <= P->vi[s][t].hi;
-      if (use_topic) ok = ok && P->tp[s][t].lo <= int64_t(topic) && int64_t(topic) <= P->tp[s][t].hi;
-      any |= ok;
-    }
-    m |= uint32_t(any) << s;
-  }
-  return m;
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t w) {
+  __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// LDS image of the tile: record r of the tile sits at r' = r + 16 (the 8
-// halo records before the tile at r' = 8..15); keys are padded by 4 words
-// per 16 so that both the lane-striped int4 writes of phase 1 and the
-// thread-blocked int4 reads of phase 2 are bank-conflict free.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef long long v2l __attribute__((ext_vector_type(2)));
+// streamed once: non-temporal 16-B loads
+__device__ __forceinline__ v4i ld_nt4(const void* p) { return __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p)); }
+__device__ __forceinline__ v2l ld_nt2(const void* p) { return __builtin_nontemporal_load(reinterpret_cast<const v2l*>(p)); }
+
+// LDS image of a tile: record r of the tile sits at r' = r + 16 (the 8 halo
+// records before the tile at r' = 8..15); keys are padded by 4 words per 16 so
+// that both the lane-striped int4 writes of the load and the thread-blocked
+// int4 reads of the scan are bank-conflict free.
 __device__ __forceinline__ int kpos(int rp) { return rp + 4 * (rp >> 4); }
 constexpr int ST_KWORDS = (ST_TILE + 16) + 4 * ((ST_TILE + 16) >> 4) + 16;
+
+// ---- one tile of records in registers (16-B vectors, compile-time indices) ----
+template <class VT>
+struct VVec;
+template <>
+struct VVec<int32_t> { v4i a; };
+template <>
+struct VVec<int64_t> { v2l a, b; };
+template <>
+struct VVec<double> { v2l a, b; };
+
+// the element is copied out before __builtin_bit_cast: bit-casting a
+// vector-element lvalue directly reads element 0 with this clang
+template <class VT>
+__device__ __forceinline__ VT vget(const VVec<VT>& x, int i) {
+  if constexpr (sizeof(VT) == 4) {
+    const int32_t e = x.a[i];
+    return __builtin_bit_cast(VT, e);
+  } else {
+    const long long e = i < 2 ? x.a[i] : x.b[i - 2];
+    return __builtin_bit_cast(VT, e);
+  }
+}
+
+template <class VT, bool TOPIC>
+struct Chunk {
+  v4i k[ST_EPT / 4];
+  VVec<VT> v[ST_EPT / 4];
+  v4i t[TOPIC ? ST_EPT / 4 : 1];
+};
+
+template <class VT, bool TOPIC>
+__device__ __forceinline__ void load_chunk(Chunk<VT, TOPIC>& c, const int32_t* __restrict__ key,
+                                           const VT* __restrict__ val, const int32_t* __restrict__ topic,
+                                           int64_t base, int64_t n, int tid) {
+#pragma unroll
+  for (int q = 0; q < ST_EPT / 4; q++) {
+    const int64_t g = base + q * (ST_THREADS * 4) + tid * 4;
+    if (g + 3 < n) {
+      c.k[q] = ld_nt4(key + g);
+      if constexpr (sizeof(VT) == 4) {
+        c.v[q].a = ld_nt4(val + g);
+      } else {
+        c.v[q].a = ld_nt2(val + g);
+        c.v[q].b = ld_nt2(val + g + 2);
+      }
+      if constexpr (TOPIC) c.t[q] = ld_nt4(topic + g);
+    } else {
+      // tail of the stream: clamped element loads; records >= n get an empty mask
+      const int64_t g0 = g < n ? g : n - 1, g1 = g + 1 < n ? g + 1 : n - 1;
+      const int64_t g2 = g + 2 < n ? g + 2 : n - 1, g3 = g + 3 < n ? g + 3 : n - 1;
+      c.k[q] = v4i{key[g0], key[g1], key[g2], key[g3]};
+      if constexpr (sizeof(VT) == 4) {
+        c.v[q].a = v4i{__builtin_bit_cast(int32_t, val[g0]), __builtin_bit_cast(int32_t, val[g1]),
+                       __builtin_bit_cast(int32_t, val[g2]), __builtin_bit_cast(int32_t, val[g3])};
+      } else {
+        c.v[q].a = v2l{__builtin_bit_cast(long long, val[g0]), __builtin_bit_cast(long long, val[g1])};
+        c.v[q].b = v2l{__builtin_bit_cast(long long, val[g2]), __builtin_bit_cast(long long, val[g3])};
+      }
+      if constexpr (TOPIC) c.t[q] = v4i{topic[g0], topic[g1], topic[g2], topic[g3]};
+    }
+  }
+}
+
+// interval index of a value: number of breakpoints <= v (breakpoints uniform, in SGPRs)
+template <class VT>
+__device__ __forceinline__ VT bp_at(const StencilProgram* __restrict__ P, int b) {
+  if constexpr (std::is_same<VT, double>::value) return P->bpf[b];
+  else return VT(P->bpi[b]);
+}
+
+template <class VT, bool TOPIC>
+__device__ __forceinline__ void masks_of_chunk(const Chunk<VT, TOPIC>& c, const StencilProgram* __restrict__ P,
+                                               const uint8_t* s_tab, const uint8_t* s_nan, uint32_t (&packed)[4]) {
+  int iv[ST_EPT], it[ST_EPT];
+#pragma unroll
+  for (int e = 0; e < ST_EPT; e++) { iv[e] = 0; it[e] = 0; }
+  const int nbp = P->nbp;
+  for (int b = 0; b < nbp; b++) {                 // scalar loop: breakpoint in an SGPR, 16 records per step
+    const VT bp = bp_at<VT>(P, b);
+#pragma unroll
+    for (int e = 0; e < ST_EPT; e++) iv[e] += bp <= vget<VT>(c.v[e >> 2], e & 3) ? 1 : 0;
+  }
+  if constexpr (TOPIC) {
+    const int ntbp = P->ntbp;
+    for (int b = 0; b < ntbp; b++) {
+      const int32_t tb = P->tbp[b];
+#pragma unroll
+      for (int e = 0; e < ST_EPT; e++) {
+        const int32_t tv = c.t[e >> 2][e & 3];
+        it[e] += tb <= tv ? 1 : 0;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int e = 4 * q + i;
+      uint32_t m = s_tab[it[e] * 16 + iv[e]];
+      if constexpr (std::is_same<VT, double>::value) {
+        const double v = vget<VT>(c.v[q], i);
+        if (v != v) m = s_nan[it[e]];
+      }
+      w |= m << (8 * i);
+    }
+    packed[q] = w;
+  }
+}
+
+template <class VT, bool TOPIC>
+__device__ __forceinline__ uint32_t mask_of(const StencilProgram* __restrict__ P, const uint8_t* s_tab,
+                                            const uint8_t* s_nan, VT v, int32_t t) {
+  int iv = 0, it = 0;
+  for (int b = 0; b < P->nbp; b++) iv += bp_at<VT>(P, b) <= v ? 1 : 0;
+  if constexpr (TOPIC)
+    for (int b = 0; b < P->ntbp; b++) it += P->tbp[b] <= t ? 1 : 0;
+  if constexpr (std::is_same<VT, double>::value)
+    if (v != v) return s_nan[it];
+  return s_tab[it * 16 + iv];
+}
 
 template <int K, class VT, bool TOPIC>
 __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
@@ -73,132 +187,116 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
     const StencilProgram* __restrict__ P, int32_t* __restrict__ out, int64_t out_cap,
     uint64_t* __restrict__ status, uint32_t* __restrict__ tile_counter, int64_t* __restrict__ total_out,
     uint32_t epoch, int64_t ntiles) {
-  __shared__ __attribute__((aligned(16))) int32_t s_key[ST_KWORDS];   // reused for the match list
+  __shared__ __attribute__((aligned(16))) int32_t s_key[ST_KWORDS];   // keys; then the match list
   __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];
-  __shared__ int32_t s_wsum[ST_THREADS / 64];
+  __shared__ int32_t s_wsum[ST_SUB][ST_THREADS / 64];
+  __shared__ uint8_t s_tab[64];
+  __shared__ uint8_t s_nan[4];
   __shared__ int64_t s_prefix;
-  __shared__ uint32_t s_tile;
+  __shared__ uint32_t s_super;
 
   const int tid = threadIdx.x;
-  if (tid == 0) s_tile = atomicAdd(tile_counter, 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
-  const int64_t base = tile * ST_TILE;
-
-  // ---- phase 1: coalesced lane-striped loads, predicate masks -> LDS ----
-#pragma unroll
-  for (int c = 0; c < ST_EPT / 4; c++) {
-    const int local = c * (ST_THREADS * 4) + tid * 4;
-    const int64_t g = base + local;
-    int32_t kk[4];
-    VT vv[4];
-    int32_t tt[4] = {0, 0, 0, 0};
-    if (g + 3 < n) {
-      const int4 k4 = *reinterpret_cast<const int4*>(key + g);
-      kk[0] = k4.x; kk[1] = k4.y; kk[2] = k4.z; kk[3] = k4.w;
-      if constexpr (sizeof(VT) == 4) {
-        const int4 v4 = *reinterpret_cast<const int4*>(val + g);
-        vv[0] = __builtin_bit_cast(VT, v4.x); vv[1] = __builtin_bit_cast(VT, v4.y);
-        vv[2] = __builtin_bit_cast(VT, v4.z); vv[3] = __builtin_bit_cast(VT, v4.w);
-      } else {
-        const longlong2 a = *reinterpret_cast<const longlong2*>(val + g);
-        const longlong2 b = *reinterpret_cast<const longlong2*>(val + g + 2);
-        vv[0] = __builtin_bit_cast(VT, a.x); vv[1] = __builtin_bit_cast(VT, a.y);
-        vv[2] = __builtin_bit_cast(VT, b.x); vv[3] = __builtin_bit_cast(VT, b.y);
-      }
-      if constexpr (TOPIC) {
-        const int4 t4 = *reinterpret_cast<const int4*>(topic + g);
-        tt[0] = t4.x; tt[1] = t4.y; tt[2] = t4.z; tt[3] = t4.w;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const bool in = g + i < n;
-        kk[i] = in ? key[g + i] : INT32_MIN;
-        vv[i] = in ? val[g + i] : VT(0);
-        if constexpr (TOPIC) tt[i] = in ? topic[g + i] : 0;
-      }
-    }
-    uint32_t packed = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const bool in = g + i < n;
-      const uint32_t m = in ? stage_mask<VT>(P, K, vv[i], tt[i], TOPIC) : 0u;
-      packed |= m << (8 * i);
-    }
-    *reinterpret_cast<int4*>(&s_key[kpos(16 + local)]) = make_int4(kk[0], kk[1], kk[2], kk[3]);
-    *reinterpret_cast<uint32_t*>(&s_mask[16 + local]) = packed;
-  }
-  if (tid < 16) {                               // halo: the 8 records before the tile (r' = 8..15)
-    const int64_t g = base - 16 + tid;
-    int32_t kk = INT32_MIN;
-    uint32_t m = 0;
-    if (tid >= 16 - (K - 1) && g >= 0) {
-      kk = key[g];
-      m = stage_mask<VT>(P, K, val[g], TOPIC ? topic[g] : 0, TOPIC);
-    }
-    s_key[kpos(tid)] = kk;
-    s_mask[tid] = uint8_t(m);
-  }
-  __syncthreads();
-
-  // ---- phase 2: 16 consecutive records per thread (+ 8 of history) ----
-  const int lb = ST_EPT * tid + 8;
-  int32_t wk[24];
-  uint8_t wm[24];
-#pragma unroll
-  for (int q = 0; q < 6; q++) {
-    const int4 k4 = *reinterpret_cast<const int4*>(&s_key[kpos(lb + 4 * q)]);
-    wk[4 * q] = k4.x; wk[4 * q + 1] = k4.y; wk[4 * q + 2] = k4.z; wk[4 * q + 3] = k4.w;
-  }
-#pragma unroll
-  for (int q = 0; q < 3; q++) {
-    const uint64_t m8 = *reinterpret_cast<const uint64_t*>(&s_mask[lb + 8 * q]);
-#pragma unroll
-    for (int b = 0; b < 8; b++) wm[8 * q + b] = uint8_t(m8 >> (8 * b));
-  }
-  uint32_t hit = 0;
-#pragma unroll
-  for (int i = 0; i < ST_EPT; i++) {
-    bool ok = true;
-#pragma unroll
-    for (int s = 0; s < K; s++) {
-      const int w = 8 + i - (K - 1) + s;
-      ok = ok && ((wm[w] >> s) & 1) && wk[w] == wk[8 + i];
-    }
-    hit |= uint32_t(ok) << i;
-  }
-  const int cnt = __popc(hit);
-
-  // ---- block exclusive scan of per-thread counts ----
   const int lane = tid & 63, wid = tid >> 6;
-  int incl = cnt;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) s_wsum[wid] = incl;
-  __syncthreads();                               // also: every thread has read s_key/s_mask
-  int woff = 0, tile_total = 0;
-#pragma unroll
-  for (int w = 0; w < ST_THREADS / 64; w++) {
-    const int x = s_wsum[w];
-    woff += w < wid ? x : 0;
-    tile_total += x;
-  }
-  const int excl = woff + incl - cnt;
+  if (tid == 0) s_super = atomicAdd(tile_counter, 1u);
+  if (tid < 64) s_tab[tid] = P->table[tid];
+  if (tid < 4) s_nan[tid] = P->nan_mask[tid];
+  __syncthreads();
+  const int64_t tile0 = int64_t(s_super) * ST_SUB;
+  const int64_t nsuper = (ntiles + ST_SUB - 1) / ST_SUB;
+  const int ntl = int(ntiles - tile0 < ST_SUB ? ntiles - tile0 : ST_SUB);   // tiles of this workgroup
 
-  // ---- decoupled look-back (wave 0) ----
+  Chunk<VT, TOPIC> cur;
+  load_chunk<VT, TOPIC>(cur, key, val, topic, tile0 * ST_TILE, n, tid);
+
+  uint32_t hits[ST_SUB];
+  int excl[ST_SUB], total[ST_SUB];
+
+  // ================= count phase =================
+#pragma unroll
+  for (int j = 0; j < ST_SUB; j++) {
+    hits[j] = 0; excl[j] = 0; total[j] = 0;
+    if (j < ntl) {                                // uniform
+      const int64_t tile = tile0 + j;
+      const int64_t base = tile * ST_TILE;
+      uint32_t packed[4];
+      masks_of_chunk<VT, TOPIC>(cur, P, s_tab, s_nan, packed);
+#pragma unroll
+      for (int q = 0; q < ST_EPT / 4; q++) {
+        const int local = q * (ST_THREADS * 4) + tid * 4;
+        uint32_t w = packed[q];
+        const int64_t left = n - (base + local);  // records >= n match nothing
+        if (left < 4) w &= left <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - left)));
+        *reinterpret_cast<v4i*>(&s_key[kpos(16 + local)]) = cur.k[q];
+        *reinterpret_cast<uint32_t*>(&s_mask[16 + local]) = w;
+      }
+      if (tid < 16) {                             // halo: the 8 records before the tile (r' = 8..15)
+        const int64_t g = base - 16 + tid;
+        int32_t kk = INT32_MIN;
+        uint32_t m = 0;
+        if (tid >= 16 - (K - 1) && g >= 0) {
+          kk = key[g];
+          m = mask_of<VT, TOPIC>(P, s_tab, s_nan, val[g], TOPIC ? topic[g] : 0);
+        }
+        s_key[kpos(tid)] = kk;
+        s_mask[tid] = uint8_t(m);
+      }
+      __syncthreads();
+      if (j + 1 < ntl) load_chunk<VT, TOPIC>(cur, key, val, topic, base + ST_TILE, n, tid);   // prefetch
+
+      const int lb = ST_EPT * tid + 8;            // 16 records of this thread + 8 of history
+      int32_t wk[24];
+      uint8_t wm[24];
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const v4i k4 = *reinterpret_cast<const v4i*>(&s_key[kpos(lb + 4 * q)]);
+        wk[4 * q] = k4[0]; wk[4 * q + 1] = k4[1]; wk[4 * q + 2] = k4[2]; wk[4 * q + 3] = k4[3];
+      }
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const uint64_t m8 = *reinterpret_cast<const uint64_t*>(&s_mask[lb + 8 * q]);
+#pragma unroll
+        for (int b = 0; b < 8; b++) wm[8 * q + b] = uint8_t(m8 >> (8 * b));
+      }
+      uint32_t hit = 0;
+#pragma unroll
+      for (int i = 0; i < ST_EPT; i++) {
+        bool ok = true;
+#pragma unroll
+        for (int s = 0; s < K; s++) {
+          const int w = 8 + i - (K - 1) + s;
+          ok = ok && ((wm[w] >> s) & 1) && wk[w] == wk[8 + i];
+        }
+        hit |= uint32_t(ok) << i;
+      }
+      const int cnt = __popc(hit);
+      int incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      if (lane == 63) s_wsum[j][wid] = incl;
+      __syncthreads();                            // LDS tile free for the next tile; wave sums visible
+      int woff = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < ST_THREADS / 64; w++) {
+        const int x = s_wsum[j][w];
+        woff += w < wid ? x : 0;
+        tot += x;
+      }
+      hits[j] = hit;
+      excl[j] = woff + incl - cnt;
+      total[j] = tot;
+      // publish the count as soon as it is known (tile 0 has no predecessor: inclusive)
+      if (tid == 0) lb_store(&status[tile], lb_pack(epoch, tile == 0 ? LB_INC : LB_AGG, uint64_t(tot)));
+    }
+  }
+
+  // ================= one look-back per super-tile =================
   if (wid == 0) {
     int64_t prefix = 0;
-    if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&status[0], lb_pack(epoch, LB_INC, uint64_t(tile_total)), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&status[tile], lb_pack(epoch, LB_AGG, uint64_t(tile_total)), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-      int64_t idx = tile - 1;
+    if (tile0 > 0) {
+      int64_t idx = tile0 - 1;
       for (;;) {
         const int64_t p = idx - lane;
         uint64_t w = 0;
@@ -208,7 +306,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
           flag = p < 0 ? uint32_t(LB_INC) : ((w >> 48) == epoch ? uint32_t((w >> 46) & 3) : 0u);
           const uint64_t inc_mask = __ballot(flag == LB_INC);
           const uint64_t bad_mask = __ballot(flag == 0);
-          // lanes nearer than the first inclusive predecessor must all be ready
+          // every predecessor up to the nearest inclusive one must have published
           const uint64_t first_inc = inc_mask ? (inc_mask & (~inc_mask + 1)) : 0;
           const uint64_t need = first_inc ? (first_inc - 1) | first_inc : ~0ull;
           if ((bad_mask & need) == 0) break;
@@ -223,60 +321,57 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         if (inc_mask) break;
         idx -= 64;
       }
-      if (lane == 0) __hip_atomic_store(&status[tile], lb_pack(epoch, LB_INC, uint64_t(prefix + tile_total)),
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) {
-      s_prefix = prefix;
-      if (tile == ntiles - 1) {
-        *total_out = prefix + tile_total;
-        *tile_counter = 0;                        // every tile id has been drawn: reset for the next launch
+      int64_t run = prefix;
+#pragma unroll
+      for (int j = 0; j < ST_SUB; j++) {
+        if (j < ntl) {
+          run += total[j];
+          lb_store(&status[tile0 + j], lb_pack(epoch, LB_INC, uint64_t(run)));
+        }
       }
-    }
-  }
-
-  // ---- stage the tile's matches (final record index) in LDS ----
-  int32_t* s_match = s_key;                       // safe: the barrier above ordered all key reads
-  {
-    int o = excl;
-    uint32_t h = hit;
-    while (h) {
-      const int i = __ffs(h) - 1;
-      h &= h - 1;
-      s_match[o++] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+      s_prefix = prefix;
+      if (tile0 + ntl == ntiles) *total_out = run;
     }
   }
   __syncthreads();
-  const int64_t pre = s_prefix;
-  // coalesced write-out: K ints per match, contiguous across the tile
-  const int words = tile_total * K;
-  for (int w = tid; w < words; w += ST_THREADS) {
-    const int m = w / K, s = w - m * K;
-    const int64_t gm = pre + m;
-    if (gm < out_cap) out[gm * K + s] = s_match[m] - (K - 1) + s;
+
+  // ================= write phase =================
+  int64_t pre = s_prefix;
+  int32_t* const s_match = s_key;
+#pragma unroll
+  for (int j = 0; j < ST_SUB; j++) {
+    if (j < ntl) {
+      const int64_t base = (tile0 + j) * ST_TILE;
+      int o = excl[j];
+      uint32_t h = hits[j];
+      while (h) {
+        const int i = __ffs(h) - 1;
+        h &= h - 1;
+        s_match[o++] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+      }
+      __syncthreads();
+      const int words = total[j] * K;              // K ints per match, contiguous across the tile
+      for (int w = tid; w < words; w += ST_THREADS) {
+        const int m = w / K, s = w - m * K;
+        const int64_t gm = pre + m;
+        if (gm < out_cap) out[gm * K + s] = s_match[m] - (K - 1) + s;
+      }
+      pre += total[j];
+      __syncthreads();
+    }
   }
+  if (tid == 0 && s_super == nsuper - 1) *tile_counter = 0;   // every super-tile drawn: reset for the next launch
 }
 
 // ---- launcher ------------------------------------------------------------
-struct StencilLaunch {
-  const int32_t* key;
-  const void* val;
-  const int32_t* topic;
-  int64_t n;
-  const StencilProgram* prog_dev;
-  int k, coltype, use_topic;
-  int32_t* out;
-  int64_t out_cap;
-  uint64_t* status;
-  uint32_t* counter;
-  int64_t* total;
-  uint32_t epoch;
-};
 
 template <int K, class VT, bool TP>
 static hipError_t launch_kt(const StencilLaunch& L, hipStream_t st) {
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
-  hipLaunchKernelGGL((stencil_kernel<K, VT, TP>), dim3(unsigned(ntiles)), dim3(ST_THREADS), 0, st, L.key,
+  const int64_t nsuper = (ntiles + ST_SUB - 1) / ST_SUB;
+  hipLaunchKernelGGL((stencil_kernel<K, VT, TP>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
                      static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.out, L.out_cap, L.status, L.counter,
                      L.total, L.epoch, ntiles);
   return hipGetLastError();
