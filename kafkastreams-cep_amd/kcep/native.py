@@ -187,7 +187,11 @@ class Session:
         self._keep = (key, cols, valid, topic, partition, offset, ts, colptrs, b)
         check(lib().cep_push_batch(self.h, C.byref(b), C.c_void_p(stream) if stream else None))
 
-    def collect(self):
+    def collect(self, raise_on_error=True):
+        """Matches of the last batch as numpy arrays.  When the reference would have thrown
+        inside ``process()`` this raises ``CepError`` (code, record); with
+        ``raise_on_error=False`` the dict carries ``err``/``err_record`` instead, and the
+        matches emitted before ``err_record`` are the ones the reference forwarded."""
         m = Matches()
         check(lib().cep_collect(self.h, C.byref(m)))
         nm, ne = m.n_matches, m.n_entries
@@ -199,8 +203,9 @@ class Session:
 
         out = dict(match_record=arr(m.match_record, nm, np.int64), match_key=arr(m.match_key, nm, np.int32),
                    ent_off=arr(m.ent_off, nm + 1, np.int64), ent_name=arr(m.ent_name, ne, np.int32),
-                   ent_record=arr(m.ent_record, ne, np.int64), path=m.path)
-        if m.err:
+                   ent_record=arr(m.ent_record, ne, np.int64), path=m.path, err=m.err,
+                   err_record=m.err_record)
+        if m.err and raise_on_error:
             raise CepError(m.err, lib().cep_last_error().decode(), m.err_record)
         return out
 

@@ -126,14 +126,22 @@ def test_device_resident_batch_and_checksum():
     assert (nm, cs) == (want_n, want_cs)
 
 
-def test_unsupported_batches_fail_loudly():
-    key = np.zeros(4, np.int32)
-    val = np.zeros(4, np.int32)
-    cp = N.CompiledPattern(c2_ir())
-    s = N.Session(cp, 4)
-    with pytest.raises(N.CepError) as ei:
-        s.push(4, key, [val], valid=np.ones(4, np.uint8))
-    assert ei.value.code == 12
-    with pytest.raises(N.CepError) as ei:
-        s.push(4, key, [val], offset=np.arange(4, dtype=np.int64))   # not flagged monotone
-    assert ei.value.code == 12
+def test_irregular_batches_route_to_general_path():
+    """Null records and unflagged offsets break the stencil's contiguity assumption:
+    the session hands those batches to the general NFA kernel, with the same result."""
+    from test_general_gpu import run_both
+    import oracle as O
+    rng = np.random.default_rng(3)
+    key = np.repeat(np.arange(50, dtype=np.int32), 40)
+    val = rng.integers(0, 3, len(key)).astype(np.int32)
+    valid = (rng.random(len(key)) > 0.05).astype(np.uint8)
+    off = np.arange(len(key), dtype=np.int64)
+    for kw in (dict(valid=valid), dict(offset=off)):
+        cp = N.CompiledPattern(c2_ir())
+        s = N.Session(cp, len(key))
+        assert s.path == N.PATH_STENCIL
+        s.push(len(key), key, [val], **kw)
+        out = s.collect()
+        assert out["path"] == N.PATH_GENERAL
+        want, got, oerr, gerr = run_both(c2_ir(), O.MODE_PROCESSOR, key, [val], [1], force=0, **kw)
+        assert oerr is None and gerr is None and got == want and len(got) > 0
