@@ -1,0 +1,55 @@
+"""Summarise one gpu_prof.sh run into profiles/.
+
+usage: python tools/pmc_summary.py TAG KERNEL EVENTS OUT_PREFIX
+
+Reads gpurun_out/prof/TAG/{trace_kernel_stats,pmc_fetch_counter_collection,
+pmc_write_counter_collection}.csv and writes
+  profiles/OUT_PREFIX_kernel_stats.csv   (copy of the rocprofv3 --stats summary)
+  profiles/OUT_PREFIX_pmc.json           (per-kernel mean FETCH/WRITE bytes per launch)
+  profiles/pmc_traffic.json              (the bench kernel's HBM bytes per launch)
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch; FETCH_SIZE is doubled (gfx950
+reports half the bytes of a wide streaming read, MI355X_MICROARCH.md §HBM).
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path, counter):
+    agg = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0]
+            agg.setdefault(name, []).append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    tag, kernel, events, prefix = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    d = os.path.join(ROOT, "gpurun_out", "prof", tag)
+    prof = os.path.join(ROOT, "profiles")
+    shutil.copy(os.path.join(d, "trace_kernel_stats.csv"), os.path.join(prof, f"{prefix}_kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(d, "pmc_fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, "pmc_write_counter_collection.csv"), "WRITE_SIZE")
+    rows = {k: {"fetch_bytes_raw": fetch.get(k), "fetch_bytes_corrected": 2 * fetch[k] if k in fetch else None,
+                "write_bytes": write.get(k)} for k in sorted(set(fetch) | set(write))}
+    with open(os.path.join(prof, f"{prefix}_pmc.json"), "w") as f:
+        json.dump({"tag": tag, "per_launch": rows}, f, indent=1)
+    k = rows[kernel]
+    out = {"kernel": kernel, "events": events, "source": f"profiles/{prefix}_pmc.json",
+           "fetch_bytes_per_launch": k["fetch_bytes_corrected"], "write_bytes_per_launch": k["write_bytes"],
+           "hbm_bytes_per_launch": k["fetch_bytes_corrected"] + k["write_bytes"]}
+    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
