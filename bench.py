@@ -39,6 +39,24 @@ def parse():
     return ap.parse_args()
 
 
+def shard(rank: int, n: int, K: int):
+    """Rank r owns keys [r*K, (r+1)*K) and the counter range [r*n, (r+1)*n) of the
+    C2 generator: disjoint key sets, so per-key NFAs never cross ranks."""
+    return rank * K, rank * n
+
+
+def gather_stats(stats, world: int):
+    """The path's one exchange step: all-gather per-rank (events, matches, seconds);
+    returns (total events, total matches, max seconds over ranks)."""
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        allg = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(allg, stats)
+        return (sum(float(x[0]) for x in allg), sum(float(x[1]) for x in allg), max(float(x[2]) for x in allg))
+    return float(stats[0]), float(stats[1]), float(stats[2])
+
+
 def main():
     args = parse()
     import numpy as np
@@ -59,7 +77,8 @@ def main():
     n, K = args.events, args.keys
     # rank r owns keys [r*K, (r+1)*K) and the counter range [r*n, (r+1)*n) of the
     # C2 generator (key-hash sharding of one node-wide stream)
-    key, val, order = synth.c2_stream_torch(n, K, dev, key_offset=rank * K, lo=rank * n)
+    key_offset, lo = shard(rank, n, K)
+    key, val, order = synth.c2_stream_torch(n, K, dev, key_offset=key_offset, lo=lo)
     torch.cuda.synchronize(dev)
 
     ir = synth.c2_pattern().to_ir(Schema([("value", "i32")]))
@@ -91,14 +110,7 @@ def main():
 
     n_matches, csum = sess.checksum()
     stats = torch.tensor([float(n), float(n_matches), elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        allg = [torch.zeros_like(stats) for _ in range(world)]
-        dist.all_gather(allg, stats)          # per-rank counts: the path's one exchange step
-        tot_events = sum(float(x[0]) for x in allg)
-        tot_matches = sum(float(x[1]) for x in allg)
-        t_max = max(float(x[2]) for x in allg)
-    else:
-        tot_events, tot_matches, t_max = float(n), float(n_matches), elapsed
+    tot_events, tot_matches, t_max = gather_stats(stats, world)
 
     if rank == 0:
         algo_bytes = 8.0 * n + 4.0 * 3 * n_matches         # 8 B/event + 12 B/match
@@ -119,7 +131,8 @@ def main():
             "dtype": "int32",
             "data": "synthetic (splitmix64 counter RNG, BASELINE.md §3 C2)",
             "config": {"workload": "C2: 3-stage strict A->B->C, processor mode", "events_per_gpu": n,
-                       "keys_per_gpu": K, "matches_per_gpu": int(n_matches), "path": "stencil",
+                       "keys_per_gpu": K, "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
+                       "path": "stencil",
                        "parallelism": f"key-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
