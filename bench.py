@@ -7,8 +7,11 @@
 
 One process per GPU (torch.distributed over RCCL when launched with
 torch.distributed.run).  Keys are sharded across ranks (weak scaling: every
-rank owns 1M keys and 100M events); the only collective is the all-gather of
-per-rank (events, matches) and the max-reduction of the timed interval.
+rank owns its own keys and events); the only collective is the all-gather of
+per-rank (events, matches, seconds) after the timed region.
+
+``--config c3|c4|c5`` measures the other BASELINE configs on the general NFA
+kernel (not the headline line; DESIGN.md reports them).
 
 Prints ONE JSON line on rank 0.
 """
@@ -24,24 +27,34 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kafkastreams-cep_amd"))
 
 PEAK_HBM_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "events/sec (whole node), 3-stage A->B->C over 1M keys; achieved HBM GB/s"
+
+# per-GPU shapes (BASELINE.md §3 / SURVEY §8(d)); C5's 10M keys are the node-wide
+# total over 8 GPUs, so one GPU owns 1.25M keys x 100 events
+CONFIGS = {
+    "c2": dict(keys=1_000_000, events=100_000_000, desc="C2: 3-stage strict A->B->C, processor mode"),
+    "c3": dict(keys=100_000, per_key=100, desc="C3: stock oneOrMore + sum/count state + within(60s)"),
+    "c4": dict(keys=100_000, per_key=12, desc="C4: skip-till-any times(3) + zeroOrMore"),
+    "c5": dict(keys=1_250_000, per_key=100, desc="C5: AND/OR + optional(), strict (1/8 of the 10M-key node)"),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--events", type=int, default=100_000_000, help="events per GPU")
-    ap.add_argument("--keys", type=int, default=1_000_000, help="keys per GPU")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--events", type=int, default=None, help="events per GPU (c2)")
+    ap.add_argument("--keys", type=int, default=None, help="keys per GPU")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-steps", action="store_true", help="minimal run for rocprofv3")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def shard(rank: int, n: int, K: int):
     """Rank r owns keys [r*K, (r+1)*K) and the counter range [r*n, (r+1)*n) of the
-    C2 generator: disjoint key sets, so per-key NFAs never cross ranks."""
+    generator: disjoint key sets, so per-key NFAs never cross ranks."""
     return rank * K, rank * n
 
 
@@ -57,12 +70,29 @@ def gather_stats(stats, world: int):
     return float(stats[0]), float(stats[1]), float(stats[2])
 
 
+def workload(cfg: str, rank: int, K: int, n: int | None, dev):
+    """Device-resident batch of one rank: (key, [cols], ts, ir, schema_types, stream_np_fn)."""
+    from kcep import synth, Schema
+    I32 = Schema([("value", "i32")])
+    if cfg == "c2":
+        ko, lo = shard(rank, n, K)
+        key, val, order = synth.c2_stream_torch(n, K, dev, key_offset=ko, lo=lo)
+        return key, [val], order, synth.c2_pattern().to_ir(I32), \
+            lambda m: synth.c2_stream_np(n, K, key_offset=ko, lo=lo)
+    L = CONFIGS[cfg]["per_key"]
+    gen_t = {"c3": synth.c3_stream_torch, "c4": synth.c4_stream_torch, "c5": synth.c5_stream_torch}[cfg]
+    gen_n = {"c3": synth.c3_stream_np, "c4": synth.c4_stream_np, "c5": synth.c5_stream_np}[cfg]
+    pat = {"c3": synth.c3_pattern, "c4": synth.c4_pattern, "c5": synth.c5_pattern}[cfg]()
+    ko, lo = rank * K, rank * K
+    key, val, ts = gen_t(K, dev, L=L, key_offset=ko, lo=lo)
+    return key, [val], ts, pat.to_ir(I32), lambda kk: gen_n(kk, L=L, key_offset=ko, lo=lo)
+
+
 def main():
     args = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
-    from kcep import native as N, synth, Schema
+    from kcep import native as N
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -74,38 +104,42 @@ def main():
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
 
-    n, K = args.events, args.keys
-    # rank r owns keys [r*K, (r+1)*K) and the counter range [r*n, (r+1)*n) of the
-    # C2 generator (key-hash sharding of one node-wide stream)
-    key_offset, lo = shard(rank, n, K)
-    key, val, order = synth.c2_stream_torch(n, K, dev, key_offset=key_offset, lo=lo)
+    C = CONFIGS[args.config]
+    K = args.keys or C["keys"]
+    n_req = args.events or C.get("events")
+    key, cols, ts, ir, gen_np = workload(args.config, rank, K, n_req, dev)
+    n = int(key.numel())
     torch.cuda.synchronize(dev)
 
-    ir = synth.c2_pattern().to_ir(Schema([("value", "i32")]))
     pat = N.CompiledPattern(ir)
     sess = N.Session(pat, n, mode=N.MODE_PROCESSOR, device=local)
-    assert sess.path == N.PATH_STENCIL
+    if args.config == "c2":
+        assert sess.path == N.PATH_STENCIL
 
     def step():
-        sess.push(n, key.data_ptr(), [val.data_ptr()], mem=N.MEM_DEVICE, stream=stream.cuda_stream)
+        sess.push(n, key.data_ptr(), [c.data_ptr() for c in cols], mem=N.MEM_DEVICE, stream=stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize(dev)
+    kernel_ms = []
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
+    for _ in range(args.steps):
         step()
-        ev[i][1].record(stream)
+        if sess.path == N.PATH_GENERAL:      # the general push syncs internally; read its kernel time
+            kernel_ms.append(sess.last_kernel_ms())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    if sess.path == N.PATH_STENCIL:
+        # one more pass per step under HIP events on the launch stream (cep_last_kernel_ms)
+        for _ in range(args.steps):
+            step()
+            kernel_ms.append(sess.last_kernel_ms())
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
 
     n_matches, csum = sess.checksum()
@@ -113,12 +147,18 @@ def main():
     tot_events, tot_matches, t_max = gather_stats(stats, world)
 
     if rank == 0:
-        algo_bytes = 8.0 * n + 4.0 * 3 * n_matches         # 8 B/event + 12 B/match
+        if sess.path == N.PATH_STENCIL:
+            k = pat.info.stencil_k
+            algo_bytes = 8.0 * n + 4.0 * k * n_matches          # 8 B/event + 4k B/match
+        else:
+            out = sess.collect(raise_on_error=False)
+            n_ent = len(out["ent_record"])
+            # 8 B/event in (key + i32 value); CSR out: 20 B/match + 12 B/entry
+            algo_bytes = 8.0 * n + 20.0 * n_matches + 12.0 * n_ent
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
         value = tot_events * args.steps / t_max
-        traffic = _pmc_traffic(n)
         line = {
-            "metric": "events/sec (whole node), 3-stage A->B->C over 1M keys; achieved HBM GB/s",
+            "metric": METRIC if args.config == "c2" else f"events/sec (whole node), {C['desc']}",
             "value": value,
             "unit": "events/s",
             "n_gpus": world,
@@ -129,28 +169,32 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (splitmix64 counter RNG, BASELINE.md §3 C2)",
-            "config": {"workload": "C2: 3-stage strict A->B->C, processor mode", "events_per_gpu": n,
-                       "keys_per_gpu": K, "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
-                       "path": "stencil",
+            "data": "synthetic (splitmix64 counter RNG, BASELINE.md §3)",
+            "config": {"workload": C["desc"], "events_per_gpu": n, "keys_per_gpu": K,
+                       "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
+                       "path": "stencil" if sess.path == N.PATH_STENCIL else "general",
                        "parallelism": f"key-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
+                         "kernel": "stencil_kernel" if sess.path == N.PATH_STENCIL else "nfa_kernel",
                          "kernel_ms": avg_kernel_ms, "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",
         }
+        if sess.path == N.PATH_GENERAL:
+            line["batch_ms"] = sess.last_batch_ms()
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = _cpu_baseline(key, val, order, ir, args.cpu_threads, n_matches, csum)
+            line["cpu_baseline"] = _cpu_baseline(args.config, key, cols, ts, ir, args.cpu_threads, n_matches, csum,
+                                                 sess, stream)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def _pmc_traffic(n):
+def _pmc_traffic(cfg, n):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (if any),
     FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json" if cfg == "c2" else f"pmc_traffic_{cfg}.json")
     try:
         with open(p) as f:
             d = json.load(f)
@@ -161,28 +205,47 @@ def _pmc_traffic(n):
         return None
 
 
-def _cpu_baseline(key, val, order, ir, threads, gpu_matches, gpu_csum):
-    """The oracle (C restatement of the reference NFA) on the host cores over
-    the full workload (same arrays), plus a 1-core figure on a 4M-event prefix."""
+def _cpu_baseline(cfg, key, cols, ts, ir, threads, gpu_matches, gpu_csum, sess, stream):
+    """The oracle (C restatement of the reference NFA) on the host cores.
+
+    C2: the full workload (same arrays) on ``threads`` threads, parity by match
+    count + checksum against the GPU's full run.  General configs: a whole-key
+    prefix of ~4M events (bounded CPU time), parity against a GPU run of the
+    same prefix.  Plus a 1-core figure on a prefix of <= 4M events."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    hk, hv, ho = key.cpu().numpy(), val.cpu().numpy(), order.cpu().numpy()
+    from kcep import native as N
+    hk = key.cpu().numpy()
+    hc = [c.cpu().numpy() for c in cols]
+    ho = ts.cpu().numpy()
     p = O.OraclePattern(ir)
-    b = O.BatchArrays(hk, [hv], [1], offset=ho, ts=ho)
     threads = max(1, min(threads, os.cpu_count() or 1))
+
+    def prefix(m):
+        m = min(len(hk), m)
+        while 0 < m < len(hk) and hk[m] == hk[m - 1]:
+            m += 1
+        return m
+
+    m_all = len(hk) if cfg == "c2" else prefix(4_000_000)
+    b = O.BatchArrays(hk[:m_all], [c[:m_all] for c in hc], [1] * len(hc), offset=ho[:m_all] if cfg == "c2" else None,
+                      ts=ho[:m_all])
     t0 = time.perf_counter()
     nm, cs = O.baseline(p, b, O.MODE_PROCESSOR, threads)
     dt = time.perf_counter() - t0
-    m1 = min(len(hk), 4_000_000)
-    while 0 < m1 < len(hk) and hk[m1] == hk[m1 - 1]:
-        m1 += 1
-    b1 = O.BatchArrays(hk[:m1], [hv[:m1]], [1], offset=ho[:m1], ts=ho[:m1])
+    if cfg != "c2":
+        # the GPU on the same prefix
+        sess.push(m_all, key.data_ptr(), [c.data_ptr() for c in cols], mem=N.MEM_DEVICE, stream=stream.cuda_stream)
+        gpu_matches, gpu_csum = sess.checksum()
+    m1 = prefix(4_000_000)
+    b1 = O.BatchArrays(hk[:m1], [c[:m1] for c in hc], [1] * len(hc), offset=ho[:m1] if cfg == "c2" else None,
+                       ts=ho[:m1])
     t1 = time.perf_counter()
     O.baseline(p, b1, O.MODE_PROCESSOR, 1)
     dt1 = time.perf_counter() - t1
-    return {"value": len(hk) / dt, "unit": "events/s", "cores": threads, "kind": "port",
-            "sample": f"full C2 workload ({len(hk)} events) on {threads} threads; 1-core figure on a "
-                      f"{m1}-event whole-key prefix",
+    return {"value": m_all / dt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"{'full workload' if cfg == 'c2' else 'whole-key prefix'} ({m_all} events) on {threads} "
+                      f"threads; 1-core figure on a {m1}-event whole-key prefix",
             "value_1core": m1 / dt1, "parity": bool(nm == gpu_matches and cs == gpu_csum),
             "oracle_matches": int(nm)}
 

@@ -161,8 +161,13 @@ int cep_collect(cep_session* s, cep_matches* out);
  * the device (matches the oracle's orc_baseline checksum); waits. */
 int cep_checksum(cep_session* s, uint64_t* sum, int64_t* n_matches);
 
-/* Kernel timing of the last batch's dominant kernel (HIP events on the launch stream). */
+/* Kernel timing of the last batch's dominant kernel (HIP events on the launch stream):
+ * stencil_kernel on the stencil path, the first nfa_kernel launch on the general path. */
 int cep_last_kernel_ms(cep_session* s, float* ms);
+
+/* Device time of the whole last cep_push_batch (staging, segmentation, kernels,
+ * regrowth re-runs and compaction), HIP events on the launch stream. */
+int cep_last_batch_ms(cep_session* s, float* ms);
 
 const char* cep_last_error(void);
 const char* cep_version(void);

@@ -106,7 +106,7 @@ struct cep_session {
   hipStream_t stream = nullptr;
   int64_t n = 0;
   bool pending = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, eb0 = nullptr, eb1 = nullptr;
   // ---- stencil workspace ----
   DBuf prog, out, status, counter, total, sum, mkey;
   int64_t out_cap = 0;
@@ -165,6 +165,7 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   HIPCHECK(hipEventRecord(s->ev0, st));
   HIPCHECK(stencil_launch(L, st));
   HIPCHECK(hipEventRecord(s->ev1, st));
+  HIPCHECK(hipEventRecord(s->eb1, st));
   return CEP_OK;
 }
 
@@ -219,14 +220,18 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->g_matches = s->g_entries = 0;
   s->nseg = 0;
   s->rerun_arenas.clear();
-  if (n == 0) return CEP_OK;
+  if (n == 0) {
+    HIPCHECK(hipEventRecord(s->ev0, st));
+    HIPCHECK(hipEventRecord(s->ev1, st));
+    HIPCHECK(hipEventRecord(s->eb1, st));
+    return CEP_OK;
+  }
   // segments: one per key run of the grouped batch
   const size_t nb = size_t(n / 1024 + 2) * 8;
   if (s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->seg.ensure(size_t(n + 1) * 8) ||
       s->scan_tmp.ensure(nb) || s->scal.ensure(64))
     return fail(CEP_E_HIP, "allocation failed");
   int64_t* scal = s->scal.as<int64_t>();
-  HIPCHECK(hipEventRecord(s->ev0, st));
   HIPCHECK(nfa_segments(A.key, n, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
                         s->scan_tmp.as<int64_t>(), st));
   const int64_t nseg = read_i64(scal, st, &rc);
@@ -264,7 +269,9 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.res_err_rec = s->r_errrec.as<int64_t>();
   A.res_overflow = s->r_ovf.as<int32_t>();
   A.overflow_count = reinterpret_cast<int32_t*>(scal + 2);
+  HIPCHECK(hipEventRecord(s->ev0, st));
   HIPCHECK(nfa_launch(A, st));
+  HIPCHECK(hipEventRecord(s->ev1, st));
   // keys that outgrew their arena: re-run exactly those with a 4x larger one
   std::vector<int64_t> seg_host;
   for (int round = 0;; round++) {
@@ -326,7 +333,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
                               s->moff.as<int64_t>(), s->eoff.as<int64_t>(), s->o_record.as<int64_t>(),
                               s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
                               s->o_entrec.as<int64_t>(), st));
-  HIPCHECK(hipEventRecord(s->ev1, st));
+  HIPCHECK(hipEventRecord(s->eb1, st));
   // the reference fails the task at its first exception: report the earliest failing record
   std::vector<int32_t> err(static_cast<size_t>(nseg));
   std::vector<int64_t> erec(static_cast<size_t>(nseg));
@@ -438,7 +445,8 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
         hipMemcpy(s->dprog.p, &P.dev, sizeof(DevProgram), hipMemcpyHostToDevice))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   }
-  if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1)) return cleanup(fail(CEP_E_HIP, "event create failed"));
+  if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
+    return cleanup(fail(CEP_E_HIP, "event create failed"));
   *out = s;
   return CEP_OK;
 }
@@ -455,6 +463,8 @@ void cep_session_close(cep_session* s) {
   s->rerun_arenas.clear();
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->eb0) (void)hipEventDestroy(s->eb0);
+  if (s->eb1) (void)hipEventDestroy(s->eb1);
   delete s;
 }
 
@@ -473,6 +483,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   s->stream = st;
   s->n = b->n;
   s->pending = true;
+  HIPCHECK(hipEventRecord(s->eb0, st));
   // records the processor would drop (null key/value, re-delivered offsets)
   // break contiguity: the stencil only takes batches without them
   const bool stencil_batch = !b->valid && !(s->opts.mode == CEP_MODE_PROCESSOR && b->offset &&
@@ -493,6 +504,13 @@ int cep_last_kernel_ms(cep_session* s, float* ms) {
   if (!s || !ms) return fail(CEP_E_ARG, "null argument");
   HIPCHECK(hipEventSynchronize(s->ev1));
   HIPCHECK(hipEventElapsedTime(ms, s->ev0, s->ev1));
+  return CEP_OK;
+}
+
+int cep_last_batch_ms(cep_session* s, float* ms) {
+  if (!s || !ms) return fail(CEP_E_ARG, "null argument");
+  HIPCHECK(hipEventSynchronize(s->eb1));
+  HIPCHECK(hipEventElapsedTime(ms, s->eb0, s->eb1));
   return CEP_OK;
 }
 

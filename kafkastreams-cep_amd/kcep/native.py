@@ -61,7 +61,7 @@ class Matches(C.Structure):
 SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_pattern_name", "cep_pattern_stage",
            "cep_session_open",
            "cep_session_close", "cep_session_path", "cep_push_batch", "cep_device_match_count", "cep_collect",
-           "cep_checksum", "cep_last_kernel_ms", "cep_last_error", "cep_version"]
+           "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version"]
 
 _lib = None
 
@@ -101,6 +101,7 @@ def lib():
     L.cep_collect.argtypes = [P, C.POINTER(Matches)]
     L.cep_checksum.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]
     L.cep_last_kernel_ms.argtypes = [P, C.POINTER(C.c_float)]
+    L.cep_last_batch_ms.argtypes = [P, C.POINTER(C.c_float)]
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -218,4 +219,9 @@ class Session:
     def last_kernel_ms(self):
         ms = C.c_float()
         check(lib().cep_last_kernel_ms(self.h, C.byref(ms)))
+        return ms.value
+
+    def last_batch_ms(self):
+        ms = C.c_float()
+        check(lib().cep_last_batch_ms(self.h, C.byref(ms)))
         return ms.value

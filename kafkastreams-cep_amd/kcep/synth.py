@@ -108,3 +108,111 @@ def c2_pattern():
     return (QueryBuilder().select("A").where(Event.value() == 0).then()
             .select("B").where(Event.value() == 1).then()
             .select("C").where(Event.value() == 2).build())
+
+
+# ---- C3-C5: fixed-length key segments ----
+# Records are laid out key-major: record i belongs to key i // L and is that
+# key's (i % L)-th event, so the batch is already grouped by (key, ts).
+
+C3_SEED, C4_SEED, C5_SEED = 0xC3, 0xC4, 0xC5
+
+
+def _segmented(n_keys, L, key_offset, lo):
+    """global counter range of this shard's records and their key ids."""
+    first = lo * L
+    return first, first + n_keys * L
+
+
+def c3_stream_np(n_keys: int, L: int = 100, key_offset: int = 0, lo: int = 0):
+    """C3 stock ticker: per key, ts += 1 + rng % 30000 (ms), price = 100 + random
+    walk of steps rng % 11 - 5 (i32).  ``lo`` = index of this shard's first key."""
+    a, b = _segmented(n_keys, L, key_offset, lo)
+    r = rng_np(C3_SEED, a, b)
+    dts = (r % np.uint64(30000)).astype(np.int64) + 1
+    step = ((r >> np.uint64(32)) % np.uint64(11)).astype(np.int64) - 5
+    ts = np.cumsum(dts.reshape(n_keys, L), axis=1).reshape(-1)
+    price = (100 + np.cumsum(step.reshape(n_keys, L), axis=1)).reshape(-1).astype(np.int32)
+    key = (np.repeat(np.arange(n_keys, dtype=np.int64), L) + key_offset).astype(np.int32)
+    return key, price, ts
+
+
+def c4_stream_np(n_keys: int, L: int = 12, key_offset: int = 0, lo: int = 0):
+    """C4 run-explosion stress: v = rng % 4, L events per key (kept small, Q6)."""
+    a, b = _segmented(n_keys, L, key_offset, lo)
+    val = (rng_np(C4_SEED, a, b) % np.uint64(4)).astype(np.int32)
+    key = (np.repeat(np.arange(n_keys, dtype=np.int64), L) + key_offset).astype(np.int32)
+    return key, val, np.tile(np.arange(L, dtype=np.int64), n_keys)
+
+
+def c5_stream_np(n_keys: int, L: int = 100, key_offset: int = 0, lo: int = 0):
+    """C5 AND/OR + optional: v = rng % 64, L events per key."""
+    a, b = _segmented(n_keys, L, key_offset, lo)
+    val = (rng_np(C5_SEED, a, b) % np.uint64(64)).astype(np.int32)
+    key = (np.repeat(np.arange(n_keys, dtype=np.int64), L) + key_offset).astype(np.int32)
+    return key, val, np.tile(np.arange(L, dtype=np.int64), n_keys)
+
+
+def _key_torch(n_keys, L, key_offset, device):
+    import torch
+    return (torch.arange(n_keys, dtype=torch.int32, device=device).repeat_interleave(L) + key_offset).contiguous()
+
+
+def c3_stream_torch(n_keys: int, device, L: int = 100, key_offset: int = 0, lo: int = 0):
+    import torch
+    a, b = _segmented(n_keys, L, key_offset, lo)
+    r = rng_torch(C3_SEED, a, b, device)
+    dts = umod_torch(r, 30000) + 1
+    step = umod_torch(_srl(r, 32), 11) - 5
+    ts = torch.cumsum(dts.view(n_keys, L), dim=1).reshape(-1)
+    price = (100 + torch.cumsum(step.view(n_keys, L), dim=1)).reshape(-1).to(torch.int32)
+    return _key_torch(n_keys, L, key_offset, device), price.contiguous(), ts.contiguous()
+
+
+def _uniform_stream_torch(seed, m, n_keys, L, key_offset, lo, device):
+    import torch
+    a, b = _segmented(n_keys, L, key_offset, lo)
+    val = umod_torch(rng_torch(seed, a, b, device), m).to(torch.int32)
+    ts = torch.arange(L, dtype=torch.int64, device=device).repeat(n_keys)
+    return _key_torch(n_keys, L, key_offset, device), val.contiguous(), ts.contiguous()
+
+
+def c4_stream_torch(n_keys: int, device, L: int = 12, key_offset: int = 0, lo: int = 0):
+    return _uniform_stream_torch(C4_SEED, 4, n_keys, L, key_offset, lo, device)
+
+
+def c5_stream_torch(n_keys: int, device, L: int = 100, key_offset: int = 0, lo: int = 0):
+    return _uniform_stream_torch(C5_SEED, 64, n_keys, L, key_offset, lo, device)
+
+
+def c3_pattern():
+    """C3: first v>0 (sum=v, count=1) -> second.oneOrMore (avg >= v; sum+=v, count+=1)
+    -> latest (avg < v), within(60 s).  Shape of NFATest.java:66-87."""
+    from .pattern import QueryBuilder, TimeUnit
+    from .expr import Event, States, Curr
+    avg = (States.getInt("sum") / States.getInt("count")).asDouble()
+    return (QueryBuilder().select("first").where(Event.value() > 0)
+            .fold("sum", Event.value()).fold("count", 1).then()
+            .select("second").oneOrMore().where(avg >= Event.value())
+            .fold("sum", Curr.int() + Event.value()).fold("count", Curr.int() + 1).then()
+            .select("latest").where(avg < Event.value()).within(60, TimeUnit.SECONDS).build())
+
+
+def c4_pattern():
+    """C4: a strict v==0 -> b skip-till-any times(3) v==1 -> c skip-till-any
+    zeroOrMore v==2 -> d skip-till-any v==3."""
+    from .pattern import QueryBuilder, Selected
+    from .expr import Event
+    return (QueryBuilder().select("a").where(Event.value() == 0).then()
+            .select("b", Selected.withSkipTilAnyMatch()).times(3).where(Event.value() == 1).then()
+            .select("c", Selected.withSkipTilAnyMatch()).zeroOrMore().where(Event.value() == 2).then()
+            .select("d", Selected.withSkipTilAnyMatch()).where(Event.value() == 3).build())
+
+
+def c5_pattern():
+    """C5: s1 10<=v<20 -> s2.optional() v==5 or v==6 -> s3 (30<=v<40) or v==63, strict."""
+    from .pattern import QueryBuilder
+    from .expr import Event
+    v = Event.value()
+    return (QueryBuilder().select("s1").where((v >= 10) & (v < 20)).then()
+            .select("s2").optional().where((v == 5) | (v == 6)).then()
+            .select("s3").where(((v >= 30) & (v < 40)) | (v == 63)).build())

@@ -4,31 +4,7 @@ from kcep import QueryBuilder, Selected, Schema, TimeUnit, Event, States, Curr, 
 I32 = Schema([("value", "i32")])
 
 
-def c3_stock():
-    """C3: first v>0 (sum=v, count=1) -> second.oneOrMore (avg >= v; sum+=v, count+=1)
-    -> latest (avg < v), within(60 s).  Shape of NFATest.java:66-87."""
-    avg = (States.getInt("sum") / States.getInt("count")).asDouble()
-    return (QueryBuilder().select("first").where(Event.value() > 0)
-            .fold("sum", Event.value()).fold("count", 1).then()
-            .select("second").oneOrMore().where(avg >= Event.value())
-            .fold("sum", Curr.int() + Event.value()).fold("count", Curr.int() + 1).then()
-            .select("latest").where(avg < Event.value()).within(60, TimeUnit.SECONDS).build())
-
-
-def c4_any():
-    """C4: a strict v==0 -> b skip-till-any times(3) v==1 -> c skip-till-any zeroOrMore v==2
-    -> d skip-till-any v==3."""
-    return (QueryBuilder().select("a").where(Event.value() == 0).then()
-            .select("b", Selected.withSkipTilAnyMatch()).times(3).where(Event.value() == 1).then()
-            .select("c", Selected.withSkipTilAnyMatch()).zeroOrMore().where(Event.value() == 2).then()
-            .select("d", Selected.withSkipTilAnyMatch()).where(Event.value() == 3).build())
-
-
-def c5_optional():
-    """C5: s1 10<=v<20 -> s2.optional() v==5 or v==6 -> s3 (30<=v<40) or v==63, strict."""
-    return (QueryBuilder().select("s1").where((Event.value() >= 10) & (Event.value() < 20)).then()
-            .select("s2").optional().where((Event.value() == 5) | (Event.value() == 6)).then()
-            .select("s3").where(((Event.value() >= 30) & (Event.value() < 40)) | (Event.value() == 63)).build())
+from kcep.synth import c3_pattern as c3_stock, c4_pattern as c4_any, c5_pattern as c5_optional  # noqa: E402,F401
 
 
 def next_one_or_more():
