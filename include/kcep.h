@@ -55,6 +55,8 @@ extern "C" {
 /* execution path chosen by cep_session_open */
 #define CEP_PATH_STENCIL 1        /* strict single-cardinality patterns: k-event stencil */
 #define CEP_PATH_GENERAL 2        /* full NFA: runs, Dewey versions, shared versioned buffer */
+#define CEP_PATH_CHAIN 3          /* strict single-cardinality patterns with optional() stages: the stencil
+                                     kernel with deterministic per-start runs (variable-length matches) */
 
 typedef struct cep_pattern cep_pattern;
 typedef struct cep_session cep_session;
@@ -65,7 +67,8 @@ typedef struct {
   int32_t n_patterns;      /* user stages (select() calls) */
   int32_t n_cols;
   int32_t stencil_ok;      /* 1 if the strict stencil path applies */
-  int32_t stencil_k;       /* number of events per stencil match */
+  int32_t stencil_k;       /* number of stages of a stencil/chain pattern */
+  int32_t chain_ok;        /* 1 if the chain path (strict + optional stages) applies */
 } cep_pattern_info;
 
 typedef struct {

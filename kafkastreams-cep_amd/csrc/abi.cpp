@@ -159,7 +159,7 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   // epoch tags the look-back granules of this launch; reset the status words when it wraps
   s->epoch = (s->epoch % 0xFFFFu) + 1;
   if (s->epoch == 1) HIPCHECK(hipMemsetAsync(s->status.p, 0, s->status.cap, st));
-  StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic,
+  StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic, SP.chain,
                   s->out.as<int32_t>(), s->out_cap, s->status.as<uint64_t>(), s->counter.as<uint32_t>(),
                   s->total.as<int64_t>(), s->epoch};
   HIPCHECK(hipEventRecord(s->ev0, st));
@@ -378,8 +378,9 @@ int cep_pattern_get_info(const cep_pattern* p, cep_pattern_info* o) {
   o->n_names = int32_t(P.names.size());
   o->n_patterns = int32_t(P.pats.size());
   o->n_cols = int32_t(P.coltypes.size());
-  o->stencil_ok = P.stencil_ok ? 1 : 0;
+  o->stencil_ok = P.stencil_ok && !P.stencil.chain ? 1 : 0;
   o->stencil_k = P.stencil_ok ? P.stencil.k : 0;
+  o->chain_ok = P.stencil_ok && P.stencil.chain ? 1 : 0;
   return CEP_OK;
 }
 
@@ -409,12 +410,14 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   if (opts->mode != CEP_MODE_NFA && opts->mode != CEP_MODE_PROCESSOR) return fail(CEP_E_ARG, "bad mode");
   const Program& P = p->prog;
   int path = opts->force_path;
-  if (path == 0) path = P.stencil_ok ? CEP_PATH_STENCIL : CEP_PATH_GENERAL;
-  if (path == CEP_PATH_STENCIL && !P.stencil_ok)
+  const int fast = P.stencil.chain ? CEP_PATH_CHAIN : CEP_PATH_STENCIL;   // the streaming kernel's flavour
+  if (path == 0) path = P.stencil_ok ? fast : CEP_PATH_GENERAL;
+  if ((path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN) && !P.stencil_ok)
     return fail(CEP_E_UNSUPPORTED, "stencil path does not apply: " + P.stencil_why);
+  if (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN) path = fast;
   if (path == CEP_PATH_GENERAL && !P.general_ok)
     return fail(CEP_E_UNSUPPORTED, "pattern cannot be lowered to the device NFA: " + P.general_why);
-  if (path != CEP_PATH_STENCIL && path != CEP_PATH_GENERAL) return fail(CEP_E_ARG, "bad path");
+  if (path != CEP_PATH_STENCIL && path != CEP_PATH_CHAIN && path != CEP_PATH_GENERAL) return fail(CEP_E_ARG, "bad path");
   HIPCHECK(hipSetDevice(opts->device));
   auto* s = new cep_session();
   s->pat = p;
@@ -428,7 +431,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   const int64_t cap = std::max<int64_t>(opts->max_events, 1);
   if (cap >= (int64_t(1) << 31)) return cleanup(fail(CEP_E_ARG, "max_events must be < 2^31 per batch"));
   if (s->scal.ensure(64) || hipMemset(s->scal.p, 0, 64)) return cleanup(fail(CEP_E_HIP, "device allocation failed"));
-  if (P.stencil_ok && path == CEP_PATH_STENCIL) {
+  if (P.stencil_ok && path != CEP_PATH_GENERAL) {
     const int k = P.stencil.k;
     if (s->prog.ensure(sizeof(StencilProgram)) || s->status.ensure(sizeof(uint64_t) * (stencil_tiles(cap) + 1)) ||
         s->counter.ensure(64) || s->total.ensure(64) || s->sum.ensure(64) ||
@@ -488,8 +491,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   // break contiguity: the stencil only takes batches without them
   const bool stencil_batch = !b->valid && !(s->opts.mode == CEP_MODE_PROCESSOR && b->offset &&
                                             !(b->flags & CEP_BATCH_OFFSETS_MONOTONE));
-  if (s->path == CEP_PATH_STENCIL && stencil_batch) {
-    s->last_path = CEP_PATH_STENCIL;
+  if (s->path != CEP_PATH_GENERAL && stencil_batch) {
+    s->last_path = s->path;
     return push_stencil(s, b, st);
   }
   if (!P.general_ok)
@@ -559,24 +562,31 @@ int cep_collect(cep_session* s, cep_matches* o) {
       HIPCHECK(hipMemcpyAsync(s->match_key.data(), s->mkey.p, size_t(nm) * 4, hipMemcpyDeviceToHost, s->stream));
       HIPCHECK(hipStreamSynchronize(s->stream));
     }
-    // traversal order of SharedVersionedBufferStoreImpl.peek: final stage first
+    // traversal order of SharedVersionedBufferStoreImpl.peek: final stage first;
+    // chain matches carry -1 for the optional stages they skipped
     s->match_record.resize(size_t(nm));
     s->ent_off.resize(size_t(nm) + 1);
     s->ent_name.resize(size_t(nm) * k);
     s->ent_record.resize(size_t(nm) * k);
+    int64_t ne = 0;
     for (int64_t m = 0; m < nm; m++) {
       s->match_record[m] = s->out_host[m * k + k - 1];
-      s->ent_off[m] = m * k;
+      s->ent_off[m] = ne;
       for (int i = 0; i < k; i++) {
         const int st = k - 1 - i;
-        s->ent_name[m * k + i] = SP.name[st];
-        s->ent_record[m * k + i] = s->out_host[m * k + st];
+        const int32_t r = s->out_host[m * k + st];
+        if (r < 0) continue;
+        s->ent_name[ne] = SP.name[st];
+        s->ent_record[ne] = r;
+        ne++;
       }
     }
-    s->ent_off[nm] = nm * k;
+    s->ent_off[nm] = ne;
+    s->ent_name.resize(size_t(ne));
+    s->ent_record.resize(size_t(ne));
     o->n_matches = nm;
-    o->n_entries = nm * k;
-    o->path = CEP_PATH_STENCIL;
+    o->n_entries = ne;
+    o->path = s->last_path;
     o->err = CEP_OK;
     o->err_record = -1;
   }

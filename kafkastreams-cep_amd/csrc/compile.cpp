@@ -349,7 +349,7 @@ bool build_table(StencilProgram& S) {
   std::vector<int64_t> bi;
   std::vector<double> bf;
   std::vector<int64_t> tb;
-  for (int s = 0; s < S.k; s++)
+  for (int s = 0; s < STENCIL_MAX_K; s++)
     for (int t = 0; t < S.nterms[s]; t++) {
       if (S.hasv[s][t]) {
         if (isf) {
@@ -387,48 +387,72 @@ bool build_table(StencilProgram& S) {
       if (isf) vf = iv == 0 ? -INFINITY : bf[iv - 1];
       else vi = iv == 0 ? (nb ? bi[0] - (bi[0] > IMIN ? 1 : 0) : 0) : bi[iv - 1];
       uint8_t m = 0;
-      for (int s = 0; s < S.k; s++) m |= uint8_t(stage_accepts(S, s, isf, vi, vf, trep)) << s;
+      for (int s = 0; s < STENCIL_MAX_K; s++) m |= uint8_t(stage_accepts(S, s, isf, vi, vf, trep)) << s;
       S.table[it * 16 + iv] = m;
     }
     uint8_t m = 0;
-    for (int s = 0; s < S.k; s++) m |= uint8_t(stage_accepts(S, s, isf, 0, NAN, trep)) << s;
+    for (int s = 0; s < STENCIL_MAX_K; s++) m |= uint8_t(stage_accepts(S, s, isf, 0, NAN, trep)) << s;
     S.nan_mask[it] = m;
   }
   return true;
 }
 
+// Chain extension of Q9: with optional() stages (not the first; a final
+// optional is already rejected by StagesFactory) and nothing else that adds
+// TAKE or IGNORE edges, no edge combination is branching (NFA.java:392-397), so
+// every run is deterministic: on each record it either consumes it (BEGIN of
+// its stage) or skips optional stages on it (SKIP_PROCEED, :222-237) until a
+// BEGIN consumes it, or dies.  A run started at record j therefore emits at
+// most one match, made of consecutive records; runs are queued oldest first,
+// so matches of one record come out in ascending start order.  Every run
+// carries its own first Dewey digit and nodes are shared only at a stage both
+// runs consume, so the first-compatible traversal (MatchedEvent.java:90-99)
+// always returns the run's own predecessors.
 void analyse_stencil(Program& P) {
   auto no = [&](const std::string& w) { P.stencil_ok = false; P.stencil_why = w; };
   const int k = int(P.pats.size());
   if (k > STENCIL_MAX_K) return no("more than 8 stages");
+  uint32_t opt = 0;
   for (int i = 0; i < k; i++) {
     const auto& p = P.pats[i];
     if (p.strategy != S_STRICT) return no("non-strict selection strategy");
-    if (p.one_or_more || p.times > 1 || p.optional) return no("quantifier");
+    if (p.one_or_more || p.times > 1) return no("quantifier");
+    if (p.optional) {
+      if (i == 0) return no("optional first stage");
+      opt |= 1u << i;
+    }
     if (!p.folds.empty()) return no("fold");
     for (int j = 0; j < i; j++)
       if (P.pats[j].name_id == p.name_id) return no("duplicate stage names");
   }
+  if (opt && k > CHAIN_MAX_K) return no("optional stages in a pattern of more than 4 stages");
   Lowering L;
   StencilProgram& S = P.stencil;
   memset(&S, 0, sizeof S);
   S.k = k;
-  for (int i = 0; i < k && L.ok; i++) {
-    const auto& p = P.pats[i];
-    ExprP pred = p.topic >= 0 ? mk(OP_AND, mk_topic(p.topic), p.pred) : p.pred;
+  S.chain = opt ? 1 : 0;
+  S.optmask = int32_t(opt);
+  auto lower_slot = [&](int slot, const ExprP& pred) {
     DNF d = L.lower(pred, false);
-    if (!L.ok) break;
-    if (d.size() > STENCIL_MAX_TERMS) { L.fail("too many terms"); break; }
-    S.nterms[i] = int(d.size());
-    S.name[i] = p.name_id;
+    if (!L.ok) return;
+    if (d.size() > STENCIL_MAX_TERMS) { L.fail("too many terms"); return; }
+    S.nterms[slot] = int(d.size());
+    S.pslots |= 1 << slot;
     for (size_t t = 0; t < d.size(); t++) {
       const Term& tm = d[t];
-      S.vi[i][t] = tm.has_v ? StencilAtomI{tm.v.lo, tm.v.hi} : StencilAtomI{IMIN, IMAX};
-      S.vf[i][t] = tm.has_v ? StencilAtomF{tm.v.dlo, tm.v.dhi} : StencilAtomF{-INFINITY, INFINITY};
-      S.tp[i][t] = tm.has_t ? StencilAtomI{tm.t.lo, tm.t.hi} : StencilAtomI{IMIN, IMAX};
-      S.hasv[i][t] = tm.has_v ? 1 : 0;
+      S.vi[slot][t] = tm.has_v ? StencilAtomI{tm.v.lo, tm.v.hi} : StencilAtomI{IMIN, IMAX};
+      S.vf[slot][t] = tm.has_v ? StencilAtomF{tm.v.dlo, tm.v.dhi} : StencilAtomF{-INFINITY, INFINITY};
+      S.tp[slot][t] = tm.has_t ? StencilAtomI{tm.t.lo, tm.t.hi} : StencilAtomI{IMIN, IMAX};
+      S.hasv[slot][t] = tm.has_v ? 1 : 0;
       if (tm.has_t) S.use_topic = 1;
     }
+  };
+  for (int i = 0; i < k && L.ok; i++) {
+    const auto& p = P.pats[i];
+    S.name[i] = p.name_id;
+    lower_slot(i, p.topic >= 0 ? mk(OP_AND, mk_topic(p.topic), p.pred) : p.pred);
+    // SKIP_PROCEED of an optional stage: successor predicate without its topic (StagesFactory.java:165)
+    if (L.ok && (opt >> i & 1)) lower_slot(CHAIN_MAX_K + i, P.pats[i + 1].pred);
   }
   if (!L.ok) return no(L.why);
   if (L.col < 0) { L.col = 0; L.coltype = P.coltypes.empty() ? T_I32 : P.coltypes[0]; }
@@ -524,6 +548,17 @@ struct CodeGen {
   }
 };
 
+// an edge predicate that reads nothing but the current record's fields
+// (no States, fold accumulator or partial sequence) has one value per record
+// whatever run evaluates it
+bool event_only(const ExprP& e) {
+  if (!e) return true;
+  switch (e->op) {
+    case OP_STATE_GET: case OP_STATE_GET_OR_ELSE: case OP_FOLD_CURR: case OP_SEQ_AVG: return false;
+    default: return event_only(e->a) && event_only(e->b);
+  }
+}
+
 }  // namespace
 
 int lower_general(Program& P, std::string& why) {
@@ -557,6 +592,11 @@ int lower_general(Program& P, std::string& why) {
       d.op[e] = s.edges[e].op;
       d.target[e] = s.edges[e].target;
       d.pred[e] = s.edges[e].pred ? cg.emit(s.edges[e].pred) : -1;
+      d.sl[e] = -1;
+      if (d.pred[e] >= 0 && event_only(s.edges[e].pred) && D.nsl < NFA_MAX_SL) {
+        d.sl[e] = D.nsl;
+        D.sl_pc[D.nsl++] = d.pred[e];
+      }
     }
     if (s.pattern >= 0) {
       const auto& folds = P.pats[s.pattern].folds;

@@ -75,12 +75,20 @@ constexpr int STENCIL_MAX_ATOMS = 2;   // per term: one value-column range + one
 struct StencilAtomI { int64_t lo, hi; };
 struct StencilAtomF { double lo, hi; };
 
-// per stage s (pattern order, first..last): OR over terms of (value in [lo,hi] AND topic in [tlo,thi])
+// Predicate slot p (0..7): OR over terms of (value in [lo,hi] AND topic in [tlo,thi]).
+// Slots 0..k-1 are the stage predicates (BEGIN edges, topic filter included).
+// Chain patterns (strict with optional() stages, k <= 4) also use slot 4+i for
+// the SKIP_PROCEED edge of optional stage i: the successor's predicate without
+// its topic filter (StagesFactory.java:159-169); the edge is that AND NOT slot i.
+constexpr int CHAIN_MAX_K = 4;
 struct StencilProgram {
   int32_t k;
   int32_t col;                       // value column read by every predicate
   int32_t coltype;                   // T_I32 / T_I64 / T_F64
   int32_t use_topic;                 // 1 if any atom constrains the topic
+  int32_t chain;                     // 1: some stage is optional (variable-length matches)
+  int32_t optmask;                   // bit i: stage i is optional
+  int32_t pslots;                    // bit p: predicate slot p is in use
   int32_t nterms[STENCIL_MAX_K];
   int32_t hasv[STENCIL_MAX_K][STENCIL_MAX_TERMS];   // 0: term does not constrain the value
   StencilAtomI vi[STENCIL_MAX_K][STENCIL_MAX_TERMS];
@@ -125,15 +133,19 @@ constexpr int NFA_MAX_FOLDS = 8;
 constexpr int NFA_MAX_STATES = 16;
 constexpr int NFA_MAX_SLOTS = 64;
 constexpr int NFA_MAX_CODE = 4096;
+constexpr int NFA_MAX_SL = 64;     // event-only edge predicates evaluated once per record
 
 struct DevStage {
   int32_t name, type, slot, nedges, nfolds;
   int32_t op[NFA_MAX_EDGES], target[NFA_MAX_EDGES], pred[NFA_MAX_EDGES];   // pred: code offset, -1 = TRUE
+  int32_t sl[NFA_MAX_EDGES];       // index of the edge's event-only predicate, -1 = evaluate per run
   int32_t fold_state[NFA_MAX_FOLDS], fold_type[NFA_MAX_FOLDS], fold_code[NFA_MAX_FOLDS];
 };
 
 struct DevProgram {
   int32_t nstages, begin, nslots, nstates, ndefined, ncols, mode, maxdepth;
+  int32_t nsl;                      // event-only edge predicates (read only the current record's fields)
+  int32_t sl_pc[NFA_MAX_SL];        // their code offsets
   int32_t slot_name[NFA_MAX_SLOTS];
   int32_t defined[NFA_MAX_STATES];
   int32_t coltype[16];
@@ -164,7 +176,7 @@ struct StencilLaunch {
   const int32_t* topic;
   int64_t n;
   const StencilProgram* prog_dev;
-  int k, coltype, use_topic;
+  int k, coltype, use_topic, chain;
   int32_t* out;
   int64_t out_cap;
   uint64_t* status;

@@ -181,7 +181,79 @@ __device__ __forceinline__ uint32_t mask_of(const StencilProgram* __restrict__ P
   return s_tab[it * 16 + iv];
 }
 
-template <int K, class VT, bool TOPIC>
+// Chain patterns (strict, optional() stages, K <= 4; compile.cpp analyse_stencil),
+// evaluated bit-parallel over the thread's 24-record window (bit w = window
+// position w).  A run started at record a (stage 0 consumes a) is deterministic:
+// at stage i on record r, BEGIN (slot i) consumes r; else the SKIP_PROCEED edge
+// of an optional stage i (slot 4+i, and not slot i) moves on to stage i+1 on the
+// same record; else the run dies (NFA.java:190-341 without TAKE/IGNORE edges).
+// X[i] after d steps = runs started d records before bit p that consumed p and
+// wait at stage i; each start is one run, so the bits never merge.
+template <int K>
+struct ChainWin {
+  uint32_t b[K];      // slot i (BEGIN edge of stage i) per record
+  uint32_t s[K];      // slot 4+i (SKIP_PROCEED of optional stage i), 0 for mandatory stages
+  uint32_t same;      // record w has the key of record w-1
+};
+
+template <int K>
+__device__ __forceinline__ ChainWin<K> chain_window(const int32_t (&wk)[24], const uint8_t (&wm)[24], uint32_t opt) {
+  ChainWin<K> c;
+#pragma unroll
+  for (int i = 0; i < K; i++) { c.b[i] = 0; c.s[i] = 0; }
+  c.same = 0;
+#pragma unroll
+  for (int w = 0; w < 24; w++) {
+    const uint32_t m = wm[w];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      c.b[i] |= ((m >> i) & 1u) << w;
+      c.s[i] |= ((m >> (CHAIN_MAX_K + i)) & 1u) << w;
+    }
+    if (w) c.same |= uint32_t(wk[w] == wk[w - 1]) << w;
+  }
+#pragma unroll
+  for (int i = 0; i < K; i++)
+    if (!((opt >> i) & 1)) c.s[i] = 0;
+  return c;
+}
+
+// e[d]: bit p set iff the run started at p-d completes (consumes stage K-1) at p.
+// consumed(d, p): the stages the run started at p-d consumed (records p-d..p in order).
+template <int K>
+struct ChainEnds {
+  uint32_t e[K];
+  __device__ __forceinline__ void run(const ChainWin<K>& c, int want_d, int want_p, uint32_t* cm) {
+    uint32_t x[K + 1];
+#pragma unroll
+    for (int i = 0; i <= K; i++) x[i] = 0;
+    x[1] = c.b[0];
+    e[0] = 0;
+    if (cm) *cm = 1;
+#pragma unroll
+    for (int d = 1; d < K; d++) {
+      uint32_t y[K + 1];
+#pragma unroll
+      for (int i = 0; i <= K; i++) y[i] = 0;
+#pragma unroll
+      for (int i = 1; i < K; i++) {
+        uint32_t pass = (x[i] << 1) & c.same;       // the run's next record, same key
+#pragma unroll
+        for (int j = i; j < K; j++) {
+          const uint32_t take = pass & c.b[j];
+          y[j + 1] |= take;
+          if (cm && d <= want_d && ((take >> (want_p - want_d + d)) & 1)) *cm |= 1u << j;
+          pass &= c.s[j] & ~c.b[j];                   // skipped on this record
+        }
+      }
+#pragma unroll
+      for (int i = 0; i <= K; i++) x[i] = y[i];
+      e[d] = x[K];
+    }
+  }
+};
+
+template <int K, class VT, bool TOPIC, bool CHAIN>
 __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
     const int32_t* __restrict__ key, const VT* __restrict__ val, const int32_t* __restrict__ topic, int64_t n,
     const StencilProgram* __restrict__ P, int32_t* __restrict__ out, int64_t out_cap,
@@ -210,6 +282,8 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 
   uint32_t hits[ST_SUB];
   int excl[ST_SUB], total[ST_SUB];
+  uint32_t wpk[CHAIN ? ST_SUB : 1][2 * K], wsame[CHAIN ? ST_SUB : 1];   // chain: the window bits, kept for the write phase
+  const uint32_t opt = CHAIN ? uint32_t(P->optmask) : 0u;
 
   // ================= count phase =================
 #pragma unroll
@@ -258,17 +332,29 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         for (int b = 0; b < 8; b++) wm[8 * q + b] = uint8_t(m8 >> (8 * b));
       }
       uint32_t hit = 0;
+      int cnt = 0;
+      if constexpr (CHAIN) {
+        const ChainWin<K> cw = chain_window<K>(wk, wm, opt);
+        ChainEnds<K> ce;
+        ce.run(cw, 0, 0, nullptr);
 #pragma unroll
-      for (int i = 0; i < ST_EPT; i++) {
-        bool ok = true;
+        for (int d = 1; d < K; d++) cnt += __popc(ce.e[d] & 0xFFFF00u);   // ends at own records 8..23
 #pragma unroll
-        for (int s = 0; s < K; s++) {
-          const int w = 8 + i - (K - 1) + s;
-          ok = ok && ((wm[w] >> s) & 1) && wk[w] == wk[8 + i];
+        for (int i = 0; i < K; i++) { wpk[j][i] = cw.b[i]; wpk[j][K + i] = cw.s[i]; }
+        wsame[j] = cw.same;
+      } else {
+#pragma unroll
+        for (int i = 0; i < ST_EPT; i++) {
+          bool ok = true;
+#pragma unroll
+          for (int s = 0; s < K; s++) {
+            const int w = 8 + i - (K - 1) + s;
+            ok = ok && ((wm[w] >> s) & 1) && wk[w] == wk[8 + i];
+          }
+          hit |= uint32_t(ok) << i;
         }
-        hit |= uint32_t(ok) << i;
+        cnt = __popc(hit);
       }
-      const int cnt = __popc(hit);
       int incl = cnt;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -340,23 +426,58 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
   // ================= write phase =================
   int64_t pre = s_prefix;
   int32_t* const s_match = s_key;
+  uint8_t* const s_aux = s_mask;                  // chain: start distance | consumed stages << 2
 #pragma unroll
   for (int j = 0; j < ST_SUB; j++) {
     if (j < ntl) {
       const int64_t base = (tile0 + j) * ST_TILE;
       int o = excl[j];
-      uint32_t h = hits[j];
-      while (h) {
-        const int i = __ffs(h) - 1;
-        h &= h - 1;
-        s_match[o++] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+      if constexpr (CHAIN) {
+        ChainWin<K> cw;
+#pragma unroll
+        for (int i = 0; i < K; i++) { cw.b[i] = wpk[j][i]; cw.s[i] = wpk[j][K + i]; }
+        cw.same = wsame[j];
+        ChainEnds<K> ce;
+        ce.run(cw, 0, 0, nullptr);
+        uint32_t any = 0;
+#pragma unroll
+        for (int d = 1; d < K; d++) any |= ce.e[d];
+        any &= 0xFFFF00u;
+        while (any) {                                // record order; per record oldest start first
+          const int p = __ffs(any) - 1;
+          any &= any - 1;
+          for (int d = K - 1; d >= 1; d--) {
+            if ((ce.e[d] >> p) & 1) {
+              uint32_t cm;
+              ChainEnds<K> one;
+              one.run(cw, d, p, &cm);
+              s_match[o] = int32_t(base + tid * ST_EPT + (p - 8));
+              s_aux[o] = uint8_t(d | (cm << 2));
+              o++;
+            }
+          }
+        }
+      } else {
+        uint32_t h = hits[j];
+        while (h) {
+          const int i = __ffs(h) - 1;
+          h &= h - 1;
+          s_match[o++] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+        }
       }
       __syncthreads();
       const int words = total[j] * K;              // K ints per match, contiguous across the tile
       for (int w = tid; w < words; w += ST_THREADS) {
         const int m = w / K, s = w - m * K;
         const int64_t gm = pre + m;
-        if (gm < out_cap) out[gm * K + s] = s_match[m] - (K - 1) + s;
+        int32_t rec;
+        if constexpr (CHAIN) {                      // skipped optional stages: -1
+          const uint32_t aux = s_aux[m], d = aux & 3u, cm = aux >> 2;
+          rec = ((cm >> s) & 1) ? s_match[m] - int32_t(d) + __popc(cm & ((1u << s) - 1)) : -1;
+        } else {
+          rec = s_match[m] - (K - 1) + s;
+        }
+        if (gm < out_cap) out[gm * K + s] = rec;
       }
       pre += total[j];
       __syncthreads();
@@ -367,27 +488,34 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 
 // ---- launcher ------------------------------------------------------------
 
-template <int K, class VT, bool TP>
+template <int K, class VT, bool TP, bool CH>
 static hipError_t launch_kt(const StencilLaunch& L, hipStream_t st) {
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
   const int64_t nsuper = (ntiles + ST_SUB - 1) / ST_SUB;
-  hipLaunchKernelGGL((stencil_kernel<K, VT, TP>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
+  hipLaunchKernelGGL((stencil_kernel<K, VT, TP, CH>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
                      static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.out, L.out_cap, L.status, L.counter,
                      L.total, L.epoch, ntiles);
   return hipGetLastError();
 }
 
-template <int K>
+template <int K, bool CH = false>
 static hipError_t launch_k(const StencilLaunch& L, hipStream_t st) {
-  if (L.coltype == T_I32) return L.use_topic ? launch_kt<K, int32_t, true>(L, st) : launch_kt<K, int32_t, false>(L, st);
-  if (L.coltype == T_I64) return L.use_topic ? launch_kt<K, int64_t, true>(L, st) : launch_kt<K, int64_t, false>(L, st);
-  return L.use_topic ? launch_kt<K, double, true>(L, st) : launch_kt<K, double, false>(L, st);
+  if (L.coltype == T_I32)
+    return L.use_topic ? launch_kt<K, int32_t, true, CH>(L, st) : launch_kt<K, int32_t, false, CH>(L, st);
+  if (L.coltype == T_I64)
+    return L.use_topic ? launch_kt<K, int64_t, true, CH>(L, st) : launch_kt<K, int64_t, false, CH>(L, st);
+  return L.use_topic ? launch_kt<K, double, true, CH>(L, st) : launch_kt<K, double, false, CH>(L, st);
 }
 
 int64_t stencil_tiles(int64_t n) { return (n + ST_TILE - 1) / ST_TILE; }
 
 hipError_t stencil_launch(const StencilLaunch& L, hipStream_t st) {
   if (L.n <= 0) return hipMemsetAsync(L.total, 0, sizeof(int64_t), st);
+  if (L.chain) {                                  // an optional stage needs k >= 3 (first/last are never optional)
+    if (L.k == 3) return launch_k<3, true>(L, st);
+    if (L.k == 4) return launch_k<4, true>(L, st);
+    return hipErrorInvalidValue;
+  }
   switch (L.k) {
     case 1: return launch_k<1>(L, st);
     case 2: return launch_k<2>(L, st);
@@ -423,7 +551,10 @@ __global__ void stencil_checksum(const int32_t* __restrict__ out, int k, int64_t
   if (i < nm) {
     const int64_t j = out[i * k + k - 1];
     h = mix64(uint64_t(j) * 0x9e3779b97f4a7c15ULL);
-    for (int s = k - 1; s >= 0; s--) h = mix64(h ^ (uint64_t(out[i * k + s]) << 8) ^ uint64_t(P->name[s]));
+    for (int s = k - 1; s >= 0; s--) {
+      const int32_t r = out[i * k + s];
+      if (r >= 0) h = mix64(h ^ (uint64_t(r) << 8) ^ uint64_t(P->name[s]));   // -1: skipped optional stage
+    }
   }
   for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
   if ((threadIdx.x & 63) == 0 && h) atomicAdd(sum, (unsigned long long)h);

@@ -59,6 +59,24 @@ def test_stencil_eligibility():
         assert bool(cp.info.stencil_ok) == eligible, fx["name"]
 
 
+def test_chain_eligibility():
+    """Strict patterns whose middle stages are optional() take the chain path (k <= 4)."""
+    sch = Schema([("value", "i32")])
+    p = N.CompiledPattern(synth.c5_pattern().to_ir(sch))
+    assert p.info.chain_ok == 1 and p.info.stencil_ok == 0 and p.info.stencil_k == 3
+    assert N.CompiledPattern(synth.c2_pattern().to_ir(sch)).info.chain_ok == 0
+    for fx in scenarios():
+        cp = N.CompiledPattern(bytes.fromhex(fx["ir"]))
+        assert bool(cp.info.chain_ok) == (fx["name"] == "nfa_optional_strict"), fx["name"]
+    v = Event.value()
+    five = QueryBuilder().select("a").where(v == 0)
+    for i in range(1, 5):
+        five = five.then().select(f"s{i}").optional().where(v == i) if i < 4 else five.then().select("z").where(v == 9)
+    assert N.CompiledPattern(five.build().to_ir(sch)).info.chain_ok == 0    # 5 stages: general path
+    first_opt = (QueryBuilder().select("a").optional().where(v == 0).then().select("b").where(v == 1).build())
+    assert N.CompiledPattern(first_opt.to_ir(sch)).info.chain_ok == 0
+
+
 def test_bad_ir_rejected():
     sch = Schema([("value", "i32")])
     ir = synth.c2_pattern().to_ir(sch)
