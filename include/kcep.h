@@ -75,11 +75,19 @@ typedef struct {
   int32_t device;          /* HIP device ordinal */
   int32_t mode;            /* CEP_MODE_* */
   int32_t force_path;      /* 0 = auto, else CEP_PATH_* */
-  int32_t reserved;
+  int32_t flags;           /* CEP_SESSION_* */
   int64_t max_events;      /* capacity of one batch */
-  int64_t max_keys;        /* capacity of distinct keys per batch (0 = max_events) */
+  int64_t max_keys;        /* CEP_SESSION_CARRY: key ids are dense in [0, max_keys) */
   double arena_scale;      /* general path: per-key workspace multiplier (0 = default 1.0) */
 } cep_opts;
+
+/* Session flags */
+#define CEP_SESSION_CARRY 1  /* keep every key's NFA state across batches, as CEPProcessor does through its
+                                NFAStore/buffer/aggregate stores (CEPProcessor.java:111-124, 144-147): a batch
+                                continues each key's runs, Dewey versions, buffer and folds where the previous
+                                one stopped.  Record positions in cep_matches are then stream positions
+                                (records pushed before the batch + index in the batch).  Runs on the general
+                                path. */
 
 #define CEP_MEM_HOST 0
 #define CEP_MEM_DEVICE 1
@@ -109,7 +117,9 @@ typedef struct {
 } cep_batch;
 
 /* Emitted sequences of one batch, library-owned, valid until the next
- * push/collect/close on the session.  Match m was emitted while processing
+ * push/collect/close on the session.  Record positions are batch indices, or
+ * stream positions on CEP_SESSION_CARRY sessions (an entry may then name a
+ * record of an earlier batch).  Match m was emitted while processing
  * record match_record[m] (context.forward order of CEPProcessor.java:148),
  * for key match_key[m].  Its traversal of the shared buffer, final stage
  * first (SharedVersionedBufferStoreImpl.peek :176-201), is
@@ -171,6 +181,23 @@ int cep_last_kernel_ms(cep_session* s, float* ms);
 /* Device time of the whole last cep_push_batch (staging, segmentation, kernels,
  * regrowth re-runs and compaction), HIP events on the launch stream. */
 int cep_last_batch_ms(cep_session* s, float* ms);
+
+/* --- carried state (CEP_SESSION_CARRY): replaces NFAStoreImpl / NFAStates persistence
+ * (state/internal/NFAStoreImpl.java:34-85, NFAStates.java:33-109, NFAStateValueSerde.java:77-147)
+ * together with the buffer and aggregate stores the runs still reference. ---
+ * Serialises the state of keys in [key_lo, key_hi) into buf (library format "KCST"):
+ * with buf == NULL only *needed is set.  Fails with CEP_E_ARG if cap < *needed. */
+int cep_state_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed);
+/* Restores keys from an export (replacing their current state); the stream position
+ * continues from the exported one if that is later. */
+int cep_state_import(cep_session* s, const void* buf, size_t len);
+/* Drops every key's state (a fresh NFAStore). */
+int cep_state_clear(cep_session* s);
+/* NFA.getRuns() and the run-queue length of a key (NFATest assertNFA, NFATest.java:836-840);
+ * *queue_len = -1 if the key has no state yet. */
+int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len);
+/* Stream position the next batch's record 0 gets (0 for sessions without CEP_SESSION_CARRY). */
+int64_t cep_stream_position(const cep_session* s);
 
 const char* cep_last_error(void);
 const char* cep_version(void);

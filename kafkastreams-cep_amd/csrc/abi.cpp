@@ -32,15 +32,19 @@ hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t n
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
-hipError_t nfa_arena_sizes(const int64_t* seg_start, int64_t nseg, const NfaCaps& cap, int nslots, int nstates,
-                           int64_t* words, hipStream_t st);
 hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
                                    hipStream_t st);
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
-hipError_t nfa_compact_launch(const int64_t* seg_start, int64_t nseg, const int32_t* key, const int64_t* res_out,
+hipError_t nfa_compact_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_out,
                               const int64_t* res_matches, const int64_t* moff, const int64_t* eoff,
                               int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st);
+hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_carry,
+                               const int32_t* res_err, int64_t* ctab, hipStream_t st);
+hipError_t carry_sizes_launch(const int64_t* ctab, int64_t nkeys, const int32_t* cpool, int64_t* words,
+                              hipStream_t st);
+hipError_t carry_move_launch(int64_t* ctab, int64_t nkeys, const int32_t* src, const int64_t* off, int32_t* dst,
+                             hipStream_t st);
 }  // namespace kcep
 
 using namespace kcep;
@@ -88,9 +92,9 @@ uint64_t mix64(uint64_t x) {
   return x;
 }
 
-// default per-key capacities of the general path (words; scaled on overflow)
-constexpr NfaCaps kCaps{16, 2, 8, 4, 256, 48, 64, 16};
-constexpr int kMaxRegrow = 6;                      // x4 each: up to 4096x the default arena
+// first allocation of a key's workspace on the general path (grown on demand from the pool)
+constexpr NfaCaps kCaps{16, 64, 16, 32, 8, 16};
+constexpr int kMaxRetry = 8;                       // pool doublings before CEP_E_RUN_CAPACITY
 }  // namespace
 
 struct cep_pattern {
@@ -116,10 +120,15 @@ struct cep_session {
   DBuf h_key, h_valid, h_topic, h_part, h_off, h_ts;
   DBuf h_cols[16];
   // ---- general workspace ----
-  DBuf dprog, flag, idx, seg, scan_tmp, scal, words, aoff, arena, r_matches, r_words, r_out, r_err, r_errrec, r_ovf,
-      ents, moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec, list, list_off;
-  std::vector<std::unique_ptr<DBuf>> rerun_arenas;
+  DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_err, r_errrec, r_carry, ents,
+      moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec;
+  int64_t pool_words = 0;       // pool capacity to use (grows after an overflow)
   int64_t nseg = 0, g_matches = 0, g_entries = 0;
+  // ---- carried per-key state (CEP_SESSION_CARRY): NFAStore equivalent ----
+  bool carry = false;
+  int64_t base = 0;             // stream position of the next batch's record 0
+  DBuf ctab, cpool;             // per key id: blob offset (-1 none); blobs (int32 words)
+  int64_t cpool_words = 0, cpool_used = 0;
   int32_t g_err = CEP_OK;
   int64_t g_err_rec = -1;
   // ---- host CSR of the last collect ----
@@ -187,6 +196,33 @@ int64_t read_i64(const void* dev, hipStream_t st, int* rc) {
   return v;
 }
 
+// Carry pool: the live blobs move to a fresh buffer (dropping the blobs that
+// later batches superseded); the table is rewritten in place.
+int carry_gc(cep_session* s, int64_t min_words, hipStream_t st) {
+  const int64_t nk = s->opts.max_keys;
+  int rc = CEP_OK;
+  if (s->flag.ensure(size_t(nk) * 8) || s->idx.ensure(size_t(nk) * 8) ||
+      s->scan_tmp.ensure(size_t(nk / 1024 + 2) * 8) || s->scal.ensure(64))
+    return fail(CEP_E_HIP, "allocation failed");
+  int64_t* scal = s->scal.as<int64_t>();
+  HIPCHECK(carry_sizes_launch(s->ctab.as<int64_t>(), nk, s->cpool.as<int32_t>(), s->flag.as<int64_t>(), st));
+  HIPCHECK(exclusive_scan(s->flag.as<int64_t>(), nk, s->idx.as<int64_t>(), scal + 5, s->scan_tmp.as<int64_t>(), st));
+  const int64_t live = read_i64(scal + 5, st, &rc);
+  if (rc) return fail(rc, "carry size");
+  const int64_t cap = std::max<int64_t>({2 * live, min_words, int64_t(1) << 20});
+  DBuf fresh;
+  if (fresh.ensure(size_t(cap) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the carried-state pool");
+  HIPCHECK(carry_move_launch(s->ctab.as<int64_t>(), nk, s->cpool.as<int32_t>(), s->idx.as<int64_t>(),
+                             fresh.as<int32_t>(), st));
+  HIPCHECK(hipStreamSynchronize(st));
+  s->cpool.release();
+  s->cpool = fresh;
+  fresh.p = nullptr;
+  s->cpool_words = cap;
+  s->cpool_used = live;
+  return CEP_OK;
+}
+
 int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   const Program& P = s->pat->prog;
   const int64_t n = b->n;
@@ -219,7 +255,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->g_err_rec = -1;
   s->g_matches = s->g_entries = 0;
   s->nseg = 0;
-  s->rerun_arenas.clear();
+  A.base = s->carry ? s->base : 0;
   if (n == 0) {
     HIPCHECK(hipEventRecord(s->ev0, st));
     HIPCHECK(hipEventRecord(s->ev1, st));
@@ -229,7 +265,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   // segments: one per key run of the grouped batch
   const size_t nb = size_t(n / 1024 + 2) * 8;
   if (s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->seg.ensure(size_t(n + 1) * 8) ||
-      s->scan_tmp.ensure(nb) || s->scal.ensure(64))
+      s->scan_tmp.ensure(nb) || s->scal.ensure(64) || s->ctl.ensure(64))
     return fail(CEP_E_HIP, "allocation failed");
   int64_t* scal = s->scal.as<int64_t>();
   HIPCHECK(nfa_segments(A.key, n, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
@@ -238,83 +274,69 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   if (rc) return fail(rc, "segment count");
   if (nseg >= (int64_t(1) << 31)) return fail(CEP_E_ARG, "too many keys in one batch");
   s->nseg = nseg;
+  A.nseg = int32_t(nseg);
   A.seg_start = s->seg.as<int64_t>();
   const DevProgram& D = P.dev;
   NfaCaps cap = kCaps;
   const double scale = s->opts.arena_scale > 0 ? s->opts.arena_scale : 1.0;
-  cap.heap_mult = int32_t(cap.heap_mult * scale);
-  cap.out_mult = int32_t(cap.out_mult * scale);
-  cap.q_mult = int32_t(cap.q_mult * scale + 0.5);
-  cap.seq_mult = int32_t(cap.seq_mult * scale + 0.5);
+  cap.heap_mult = std::max<int32_t>(1, int32_t(cap.heap_mult * scale));
+  cap.out_mult = std::max<int32_t>(1, int32_t(cap.out_mult * scale));
   const size_t sb = size_t(nseg) * 8;
-  if (s->words.ensure(sb) || s->aoff.ensure(sb) || s->r_matches.ensure(sb) || s->r_words.ensure(sb) ||
-      s->r_out.ensure(sb) || s->r_err.ensure(sb) || s->r_errrec.ensure(sb) || s->r_ovf.ensure(sb) || s->ents.ensure(sb) ||
-      s->moff.ensure(sb) || s->eoff.ensure(sb))
+  if (s->r_matches.ensure(sb) || s->r_words.ensure(sb) || s->r_out.ensure(sb) || s->r_err.ensure(sb) ||
+      s->r_errrec.ensure(sb) || s->r_carry.ensure(sb) || s->ents.ensure(sb) || s->moff.ensure(sb) || s->eoff.ensure(sb))
     return fail(CEP_E_HIP, "allocation failed");
-  HIPCHECK(nfa_arena_sizes(A.seg_start, nseg, cap, D.nslots, D.nstates, s->words.as<int64_t>(), st));
-  HIPCHECK(exclusive_scan(s->words.as<int64_t>(), nseg, s->aoff.as<int64_t>(), scal + 1, s->scan_tmp.as<int64_t>(), st));
-  const int64_t total_words = read_i64(scal + 1, st, &rc);
-  if (rc) return fail(rc, "arena size");
-  if (s->arena.ensure(size_t(total_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA arena");
-  HIPCHECK(hipMemsetAsync(scal + 2, 0, 8, st));
-  A.nlist = int32_t(nseg);
-  A.seg_list = nullptr;
-  A.arena = s->arena.as<int32_t>();
-  A.arena_off = s->aoff.as<int64_t>();
+  // first-allocation words of every key (NfaCaps) plus the events carried into the batch
+  const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base;
+  const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 3 * D.nstates;
+  const int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
+  s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
   A.cap = cap;
+  A.carry = s->carry ? 1 : 0;
+  A.max_keys = int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX));
   A.res_matches = s->r_matches.as<int64_t>();
   A.res_words = s->r_words.as<int64_t>();
   A.res_out = s->r_out.as<int64_t>();
   A.res_err = s->r_err.as<int32_t>();
   A.res_err_rec = s->r_errrec.as<int64_t>();
-  A.res_overflow = s->r_ovf.as<int32_t>();
-  A.overflow_count = reinterpret_cast<int32_t*>(scal + 2);
-  HIPCHECK(hipEventRecord(s->ev0, st));
-  HIPCHECK(nfa_launch(A, st));
-  HIPCHECK(hipEventRecord(s->ev1, st));
-  // keys that outgrew their arena: re-run exactly those with a 4x larger one
-  std::vector<int64_t> seg_host;
-  for (int round = 0;; round++) {
-    int32_t novf = 0;
-    HIPCHECK(hipMemcpyAsync(&novf, scal + 2, 4, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    if (novf == 0) break;
-    if (round >= kMaxRegrow) return fail(CEP_E_RUN_CAPACITY, "a key exceeded the largest NFA arena");
-    std::vector<int32_t> ovf(static_cast<size_t>(nseg));
-    HIPCHECK(hipMemcpy(ovf.data(), s->r_ovf.p, sb / 2, hipMemcpyDeviceToHost));
-    if (seg_host.empty()) {
-      seg_host.resize(size_t(nseg) + 1);
-      HIPCHECK(hipMemcpy(seg_host.data(), s->seg.p, (size_t(nseg) + 1) * 8, hipMemcpyDeviceToHost));
+  A.res_carry = s->r_carry.as<int64_t>();
+  unsigned long long* ctl = s->ctl.as<unsigned long long>();
+  A.pool_top = ctl;
+  A.cpool_top = ctl + 1;
+  A.flags = reinterpret_cast<int32_t*>(ctl + 2);
+  bool timed = false;
+  for (int attempt = 0;; attempt++) {
+    if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
+    if (s->carry && s->cpool_used + nseg * 64 > s->cpool_words) {
+      if ((rc = carry_gc(s, 2 * (s->cpool_used + nseg * 64), st))) return rc;
     }
-    cap.q_mult *= 4; cap.q_base *= 4; cap.seq_mult *= 4; cap.seq_base *= 4;
-    cap.heap_mult *= 4; cap.heap_base *= 4; cap.out_mult *= 4; cap.out_base *= 4;
-    std::vector<int32_t> lst;
-    std::vector<int64_t> off;
-    int64_t tot = 0;
-    for (int64_t i = 0; i < nseg; i++)
-      if (ovf[size_t(i)]) {
-        int64_t a, b2, c, d, w;
-        const int64_t L = seg_host[size_t(i) + 1] - seg_host[size_t(i)];
-        a = cap.q_base + cap.q_mult * L; b2 = cap.seq_base + cap.seq_mult * L;
-        c = cap.heap_base + cap.heap_mult * L; d = cap.out_base + cap.out_mult * L;
-        w = 64 + 16 * a + 3 * int64_t(D.nslots) * L + 3 * int64_t(D.nstates) * b2 + c + d;
-        lst.push_back(int32_t(i));
-        off.push_back(tot);
-        tot += (w + 3) & ~int64_t(3);
-      }
-    auto ar = std::make_unique<DBuf>();
-    if (ar->ensure(size_t(tot) * 4) || s->list.ensure(lst.size() * 4) || s->list_off.ensure(off.size() * 8))
-      return fail(CEP_E_RUN_CAPACITY, "cannot allocate the regrown NFA arena");
-    HIPCHECK(hipMemcpy(s->list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->list_off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice));
-    HIPCHECK(hipMemsetAsync(scal + 2, 0, 8, st));
-    A.nlist = int32_t(lst.size());
-    A.seg_list = s->list.as<int32_t>();
-    A.arena = ar->as<int32_t>();
-    A.arena_off = s->list_off.as<int64_t>();
-    A.cap = cap;
+    A.pool = s->pool.as<int32_t>();
+    A.pool_cap = s->pool_words;
+    A.ctab = s->carry ? s->ctab.as<int64_t>() : nullptr;
+    A.cpool = s->carry ? s->cpool.as<int32_t>() : nullptr;
+    A.cpool_cap = s->carry ? s->cpool_words : 0;
+    unsigned long long init[4] = {0, (unsigned long long)s->cpool_used, 0, 0};
+    HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
+    if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
     HIPCHECK(nfa_launch(A, st));
-    s->rerun_arenas.push_back(std::move(ar));
+    if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
+    timed = true;
+    unsigned long long res[4];
+    HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const int32_t* fl = reinterpret_cast<const int32_t*>(res + 2);
+    if (fl[2]) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    if (!fl[0] && !fl[1]) {
+      if (s->carry) s->cpool_used = int64_t(res[1]);
+      break;
+    }
+    if (attempt >= kMaxRetry) return fail(CEP_E_RUN_CAPACITY, "a key exceeded the largest NFA workspace");
+    if (fl[0]) {                                   // workspace pool exhausted: twice the pool, same inputs
+      s->pool.release();
+      s->pool_words *= 2;
+    }
+    if (fl[1]) {                                   // carry pool exhausted: compact into a larger one
+      if ((rc = carry_gc(s, 2 * s->cpool_words, st))) return rc;
+    }
   }
   // compaction into the CSR
   HIPCHECK(nfa_entry_counts_launch(s->r_words.as<int64_t>(), s->r_matches.as<int64_t>(), nseg, s->ents.as<int64_t>(), st));
@@ -329,10 +351,15 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   if (s->o_record.ensure(nm * 8) || s->o_key.ensure(nm * 4) || s->o_entoff.ensure(nm * 8) ||
       s->o_name.ensure(ne * 4) || s->o_entrec.ensure(ne * 8))
     return fail(CEP_E_HIP, "allocation failed");
-  HIPCHECK(nfa_compact_launch(A.seg_start, nseg, A.key, s->r_out.as<int64_t>(), s->r_matches.as<int64_t>(),
+  HIPCHECK(nfa_compact_launch(nseg, A.key, A.seg_start, s->r_out.as<int64_t>(), s->r_matches.as<int64_t>(),
                               s->moff.as<int64_t>(), s->eoff.as<int64_t>(), s->o_record.as<int64_t>(),
                               s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
                               s->o_entrec.as<int64_t>(), st));
+  if (s->carry) {                                  // NFAStore.put of every key of the batch
+    HIPCHECK(carry_commit_launch(nseg, A.key, A.seg_start, s->r_carry.as<int64_t>(), s->r_err.as<int32_t>(),
+                                 s->ctab.as<int64_t>(), st));
+    s->base += n;
+  }
   HIPCHECK(hipEventRecord(s->eb1, st));
   // the reference fails the task at its first exception: report the earliest failing record
   std::vector<int32_t> err(static_cast<size_t>(nseg));
@@ -345,6 +372,9 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       s->g_err = err[size_t(i)];
       s->g_err_rec = erec[size_t(i)];
     }
+  if (s->carry && s->cpool_used > s->cpool_words / 4 * 3) {   // keep room for the next batch
+    if ((rc = carry_gc(s, 0, st))) return rc;
+  }
   return CEP_OK;
 }
 
@@ -418,6 +448,15 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   if (path == CEP_PATH_GENERAL && !P.general_ok)
     return fail(CEP_E_UNSUPPORTED, "pattern cannot be lowered to the device NFA: " + P.general_why);
   if (path != CEP_PATH_STENCIL && path != CEP_PATH_CHAIN && path != CEP_PATH_GENERAL) return fail(CEP_E_ARG, "bad path");
+  const bool carry = opts->flags & CEP_SESSION_CARRY;
+  if (carry && (opts->max_keys <= 0 || opts->max_keys > INT32_MAX))
+    return fail(CEP_E_ARG, "carry sessions need max_keys (dense key ids in [0, max_keys))");
+  if (carry && path != CEP_PATH_GENERAL) {
+    if (opts->force_path) return fail(CEP_E_UNSUPPORTED, "carried state runs on the general NFA path");
+    path = CEP_PATH_GENERAL;
+  }
+  if (carry && !P.general_ok)
+    return fail(CEP_E_UNSUPPORTED, "pattern cannot be lowered to the device NFA: " + P.general_why);
   HIPCHECK(hipSetDevice(opts->device));
   auto* s = new cep_session();
   s->pat = p;
@@ -448,6 +487,13 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
         hipMemcpy(s->dprog.p, &P.dev, sizeof(DevProgram), hipMemcpyHostToDevice))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   }
+  if (carry) {                                   // NFAStore: no key has state yet
+    s->carry = true;
+    s->cpool_words = std::max<int64_t>(int64_t(1) << 20, opts->max_keys * 64);
+    if (s->ctab.ensure(size_t(opts->max_keys) * 8) || s->cpool.ensure(size_t(s->cpool_words) * 4) ||
+        hipMemset(s->ctab.p, 0xFF, size_t(opts->max_keys) * 8))
+      return cleanup(fail(CEP_E_HIP, "device allocation failed"));
+  }
   if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
     return cleanup(fail(CEP_E_HIP, "event create failed"));
   *out = s;
@@ -458,12 +504,11 @@ void cep_session_close(cep_session* s) {
   if (!s) return;
   for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->h_key, &s->h_valid,
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
-                  &s->scal, &s->words, &s->aoff, &s->arena, &s->r_matches, &s->r_words, &s->r_out, &s->r_err,
-                  &s->r_errrec, &s->r_ovf, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff,
-                  &s->o_name, &s->o_entrec, &s->list, &s->list_off})
+                  &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
+                  &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
+                  &s->o_entrec, &s->ctab, &s->cpool})
     b->release();
   for (auto& c : s->h_cols) c.release();
-  s->rerun_arenas.clear();
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->eb0) (void)hipEventDestroy(s->eb0);
@@ -632,5 +677,129 @@ int cep_checksum(cep_session* s, uint64_t* sum, int64_t* n_matches) {
   if (n_matches) *n_matches = nm;
   return CEP_OK;
 }
+
+// ---- carried state (CEP_SESSION_CARRY) ----
+// export format: "KCST", version 1, int64 next stream position, int32 key count,
+// then per key: int32 key id, int32 words, the blob (kcep_internal.h CB_*)
+namespace {
+constexpr uint32_t kStateMagic = 0x5453434Bu;   // "KCST"
+int need_carry(cep_session* s) {
+  if (!s) return fail(CEP_E_ARG, "null argument");
+  if (!s->carry) return fail(CEP_E_ARG, "the session was not opened with CEP_SESSION_CARRY");
+  return CEP_OK;
+}
+}  // namespace
+
+int cep_state_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed) {
+  int rc = need_carry(s);
+  if (rc) return rc;
+  if (!needed) return fail(CEP_E_ARG, "null argument");
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  key_lo = std::max<int32_t>(key_lo, 0);
+  key_hi = int32_t(std::min<int64_t>(key_hi, s->opts.max_keys));
+  std::vector<int64_t> tab(size_t(std::max(0, key_hi - key_lo)));
+  if (!tab.empty()) HIPCHECK(hipMemcpy(tab.data(), s->ctab.as<int64_t>() + key_lo, tab.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<int32_t> pool(size_t(s->cpool_used));
+  if (!pool.empty()) HIPCHECK(hipMemcpy(pool.data(), s->cpool.p, pool.size() * 4, hipMemcpyDeviceToHost));
+  size_t bytes = 20;
+  int32_t nkeys = 0;
+  for (int64_t o : tab)
+    if (o >= 0) { bytes += 8 + size_t(pool[size_t(o) + CB_WORDS]) * 4; nkeys++; }
+  *needed = bytes;
+  if (!buf) return CEP_OK;
+  if (cap < bytes) return fail(CEP_E_ARG, "export buffer too small");
+  uint8_t* p = static_cast<uint8_t*>(buf);
+  const uint32_t ver = 1;
+  memcpy(p, &kStateMagic, 4); memcpy(p + 4, &ver, 4); memcpy(p + 8, &s->base, 8); memcpy(p + 16, &nkeys, 4);
+  p += 20;
+  for (size_t i = 0; i < tab.size(); i++) {
+    if (tab[i] < 0) continue;
+    const int32_t k = key_lo + int32_t(i), w = pool[size_t(tab[i]) + CB_WORDS];
+    memcpy(p, &k, 4); memcpy(p + 4, &w, 4);
+    memcpy(p + 8, pool.data() + tab[i], size_t(w) * 4);
+    p += 8 + size_t(w) * 4;
+  }
+  return CEP_OK;
+}
+
+int cep_state_import(cep_session* s, const void* buf, size_t len) {
+  int rc = need_carry(s);
+  if (rc) return rc;
+  if (!buf || len < 20) return fail(CEP_E_ARG, "bad state blob");
+  const uint8_t* p = static_cast<const uint8_t*>(buf);
+  uint32_t magic, ver;
+  int64_t base;
+  int32_t nkeys;
+  memcpy(&magic, p, 4); memcpy(&ver, p + 4, 4); memcpy(&base, p + 8, 8); memcpy(&nkeys, p + 16, 4);
+  if (magic != kStateMagic || ver != 1 || nkeys < 0) return fail(CEP_E_ARG, "bad state blob");
+  const DevProgram& D = s->pat->prog.dev;
+  std::vector<std::pair<int32_t, size_t>> keys;    // key, byte offset of its blob
+  size_t at = 20, words = 0;
+  for (int32_t i = 0; i < nkeys; i++) {
+    if (at + 8 > len) return fail(CEP_E_ARG, "truncated state blob");
+    int32_t k, w;
+    memcpy(&k, p + at, 4); memcpy(&w, p + at + 4, 4);
+    if (k < 0 || k >= s->opts.max_keys || w < CB_HDR || at + 8 + size_t(w) * 4 > len)
+      return fail(CEP_E_ARG, "bad key entry in the state blob");
+    int32_t hdr[CB_HDR];
+    memcpy(hdr, p + at + 8, sizeof hdr);
+    if (hdr[CB_WORDS] != w || hdr[CB_NCOLS] != D.ncols || hdr[CB_NSTATES] != D.nstates)
+      return fail(CEP_E_ARG, "state blob does not match this pattern");
+    keys.push_back({k, at + 8});
+    words += size_t(w);
+    at += 8 + size_t(w) * 4;
+  }
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  hipStream_t st = s->stream;
+  if (s->cpool_used + int64_t(words) > s->cpool_words && (rc = carry_gc(s, 2 * (s->cpool_used + int64_t(words)), st)))
+    return rc;
+  std::vector<int32_t> blobs(words);
+  std::vector<int64_t> tab(size_t(s->opts.max_keys));
+  HIPCHECK(hipMemcpy(tab.data(), s->ctab.p, tab.size() * 8, hipMemcpyDeviceToHost));
+  size_t w0 = 0;
+  for (auto& kb : keys) {
+    int32_t w;
+    memcpy(&w, p + kb.second, 4);
+    memcpy(blobs.data() + w0, p + kb.second, size_t(w) * 4);
+    tab[size_t(kb.first)] = s->cpool_used + int64_t(w0);
+    w0 += size_t(w);
+  }
+  if (words) HIPCHECK(hipMemcpy(s->cpool.as<int32_t>() + s->cpool_used, blobs.data(), words * 4, hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(s->ctab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+  s->cpool_used += int64_t(words);
+  s->base = std::max(s->base, base);
+  return CEP_OK;
+}
+
+int cep_state_clear(cep_session* s) {
+  int rc = need_carry(s);
+  if (rc) return rc;
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  HIPCHECK(hipMemset(s->ctab.p, 0xFF, size_t(s->opts.max_keys) * 8));
+  s->cpool_used = 0;
+  s->base = 0;
+  return CEP_OK;
+}
+
+int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len) {
+  int rc = need_carry(s);
+  if (rc) return rc;
+  if (!runs || !queue_len || key < 0 || key >= s->opts.max_keys) return fail(CEP_E_ARG, "bad argument");
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  int64_t off = -1;
+  HIPCHECK(hipMemcpy(&off, s->ctab.as<int64_t>() + key, 8, hipMemcpyDeviceToHost));
+  if (off < 0) { *runs = 0; *queue_len = -1; return CEP_OK; }
+  int32_t hdr[CB_HDR];
+  HIPCHECK(hipMemcpy(hdr, s->cpool.as<int32_t>() + off, sizeof hdr, hipMemcpyDeviceToHost));
+  *runs = int64_t(uint32_t(hdr[CB_RUNS_LO])) | (int64_t(hdr[CB_RUNS_HI]) << 32);
+  *queue_len = hdr[CB_QLEN];
+  return CEP_OK;
+}
+
+int64_t cep_stream_position(const cep_session* s) { return s ? s->base : -1; }
 
 }  // extern "C"

@@ -185,9 +185,33 @@ struct StencilLaunch {
   uint32_t epoch;
 };
 
-struct NfaCaps {                  // per-key arena capacities, as base + mult * records (words)
-  int32_t q_base, q_mult, seq_base, seq_mult, heap_base, heap_mult, out_base, out_mult;
+// Per-key workspace of the general NFA kernel.  Every key segment draws its
+// workspace from a batch-wide pool (one atomic per lane, aggregated per wave);
+// arrays that outgrow their first allocation are re-allocated from the pool at
+// twice the size (all internal references are offsets, so a copy relocates).
+struct NfaCaps {
+  int32_t q0;                     // initial run-queue capacity (runs)
+  int32_t heap_base, heap_mult;   // initial heap: base + mult * events (words)
+  int32_t out_base, out_mult;     // initial match output: base + mult * records (words)
+  int32_t seq_base;               // initial aggregate rows: seq_base + records
 };
+
+// Carried per-key state (CEP_SESSION_CARRY): the NFAStates of the key
+// (state/internal/NFAStates.java:33-109: run queue, runs counter, per-topic
+// high-water marks) plus the shared-buffer nodes and aggregates the queue can
+// still reach, as one relocatable blob of int32 words in the session's carry
+// pool.  Events referenced by the carried buffer travel with it
+// (MatchedEvent.java:29-34 keeps key/value/timestamp in the buffer too).
+enum : int32_t {
+  CB_WORDS = 0, CB_RUNS_LO, CB_RUNS_HI, CB_NHWM, CB_QLEN, CB_NEV, CB_NNODE, CB_NPRED, CB_NVER, CB_NSEQ,
+  CB_NCOLS, CB_NSTATES, CB_HDR
+};
+// sections after the header: hwm[3*nhwm] (topic, hwm lo, hi); queue[4*qlen]
+// (w0, version offset, event, seq); events[(8+2*ncols)*nev] (stream position,
+// topic, partition, offset, ts, columns as 64-bit); nodes[4*nnode] (slot, event,
+// refs, first pred); preds[4*npred] (version offset, prev slot, prev event, next
+// pred); versions[nver] ([len, digits...]); aggs[3*nstates*nseq] (tag, lo, hi).
+__host__ __device__ inline int32_t carry_evw(int32_t ncols) { return 8 + 2 * ncols; }
 
 struct NfaArgs {
   const DevProgram* P;
@@ -199,20 +223,27 @@ struct NfaArgs {
   const int64_t* ts;
   const void* cols[16];
   int64_t n;
+  int64_t base;                   // stream position of batch record 0 (carry sessions; else 0)
   int32_t mode;
-  int32_t nlist;
+  int32_t nseg;
   const int64_t* seg_start;       // nseg + 1
-  const int32_t* seg_list;        // segments handled by this launch (nullptr: segment = list index)
-  int32_t* arena;
-  const int64_t* arena_off;       // per list entry, word offset
+  int32_t* pool;                  // per-batch workspace pool
+  int64_t pool_cap;
+  unsigned long long* pool_top;
   NfaCaps cap;
+  int32_t carry;                  // 1: import/export carried state
+  int32_t max_keys;               // carry: key ids are dense in [0, max_keys)
+  const int64_t* ctab;            // carry: per key id, word offset of its blob in cpool (-1 none)
+  int32_t* cpool;
+  int64_t cpool_cap;
+  unsigned long long* cpool_top;
+  int64_t* res_carry;             // carry: per segment, offset of the new blob (-1 none)
   int64_t* res_matches;           // per segment
   int64_t* res_words;
   int64_t* res_out;               // device address of the key's output region
   int32_t* res_err;
   int64_t* res_err_rec;
-  int32_t* res_overflow;
-  int32_t* overflow_count;
+  int32_t* flags;                 // [0] pool overflow lanes, [1] carry-pool overflow lanes, [2] bad key ids
 };
 
 // compile.cpp

@@ -25,6 +25,7 @@ MODE_NFA, MODE_PROCESSOR = 0, 1
 PATH_STENCIL, PATH_GENERAL, PATH_CHAIN = 1, 2, 3
 MEM_HOST, MEM_DEVICE = 0, 1
 BATCH_OFFSETS_MONOTONE = 1
+SESSION_CARRY = 1
 
 
 class CepError(RuntimeError):
@@ -41,7 +42,7 @@ class PatternInfo(C.Structure):
 
 
 class Opts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("mode", C.c_int32), ("force_path", C.c_int32), ("reserved", C.c_int32),
+    _fields_ = [("device", C.c_int32), ("mode", C.c_int32), ("force_path", C.c_int32), ("flags", C.c_int32),
                 ("max_events", C.c_int64), ("max_keys", C.c_int64), ("arena_scale", C.c_double)]
 
 
@@ -62,7 +63,8 @@ class Matches(C.Structure):
 SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_pattern_name", "cep_pattern_stage",
            "cep_session_open",
            "cep_session_close", "cep_session_path", "cep_push_batch", "cep_device_match_count", "cep_collect",
-           "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version"]
+           "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version",
+           "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position"]
 
 _lib = None
 
@@ -103,6 +105,12 @@ def lib():
     L.cep_checksum.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]
     L.cep_last_kernel_ms.argtypes = [P, C.POINTER(C.c_float)]
     L.cep_last_batch_ms.argtypes = [P, C.POINTER(C.c_float)]
+    L.cep_state_export.argtypes = [P, C.c_int32, C.c_int32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.cep_state_import.argtypes = [P, C.c_void_p, C.c_size_t]
+    L.cep_state_clear.argtypes = [P]
+    L.cep_key_state.argtypes = [P, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.cep_stream_position.argtypes = [P]
+    L.cep_stream_position.restype = C.c_int64
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -154,10 +162,13 @@ class CompiledPattern:
 class Session:
     """One ``cep_session`` (one stream task's processor on one GPU)."""
 
-    def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0):
+    def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0,
+                 carry=False, max_keys=0):
+        """``carry=True``: every key's NFA state continues across batches (CEP_SESSION_CARRY);
+        key ids must then be dense in [0, max_keys) and record positions are stream positions."""
         self.pattern = pattern
         self.h = C.c_void_p()
-        o = Opts(device, mode, force_path, 0, max_events, 0, 0.0)
+        o = Opts(device, mode, force_path, SESSION_CARRY if carry else 0, max_events, max_keys, 0.0)
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)
         self._keep = None
@@ -216,6 +227,30 @@ class Session:
         n = C.c_int64()
         check(lib().cep_checksum(self.h, C.byref(s), C.byref(n)))
         return n.value, s.value
+
+    # ---- carried state (CEP_SESSION_CARRY) ----
+    def state_export(self, key_lo=0, key_hi=2**31 - 1) -> bytes:
+        L = lib()
+        need = C.c_size_t()
+        check(L.cep_state_export(self.h, key_lo, key_hi, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        check(L.cep_state_export(self.h, key_lo, key_hi, buf, need.value, C.byref(need)))
+        return buf.raw[:need.value]
+
+    def state_import(self, blob: bytes):
+        check(lib().cep_state_import(self.h, blob, len(blob)))
+
+    def state_clear(self):
+        check(lib().cep_state_clear(self.h))
+
+    def key_state(self, key: int):
+        """(NFA.getRuns(), run-queue length) of a key, or None if it has no state yet."""
+        runs, q = C.c_int64(), C.c_int64()
+        check(lib().cep_key_state(self.h, key, C.byref(runs), C.byref(q)))
+        return None if q.value < 0 else (runs.value, q.value)
+
+    def stream_position(self):
+        return lib().cep_stream_position(self.h)
 
     def last_kernel_ms(self):
         ms = C.c_float()

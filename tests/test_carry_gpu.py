@@ -1,0 +1,187 @@
+"""Per-key state carried across batches (CEP_SESSION_CARRY) against the oracle.
+
+The reference keeps every key's NFA between records in its stores and reloads
+it on the next record (CEPProcessor.loadNFA / NFAStore.put,
+CEPProcessor.java:111-124, 144-147).  A carry session must therefore produce,
+over a stream cut into batches at arbitrary points, exactly the matches of one
+uninterrupted run: the oracle processes the concatenated stream in one go and
+the device processes it batch by batch (each batch grouped by key), with
+record positions reported as stream positions.  The per-key run counter and
+queue length (NFATest assertNFA, NFATest.java:836-840) must agree too, and the
+state must survive an export/import round trip into a fresh session."""
+import numpy as np
+import pytest
+
+import oracle as O
+from kcep import native as N
+from kcep import synth
+from golden_util import scenarios, event_arrays
+import patterns_lib as PL
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_run(ir, key, cols, coltypes, mode, **kw):
+    p = O.OraclePattern(ir)
+    r = O.OracleRun(p, mode)
+    err = None
+    try:
+        r.process(O.BatchArrays(key, cols, coltypes, **kw))
+    except O.OracleError as e:
+        err = (e.code, e.record)
+    ms = [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)]
+    return ms, r, err
+
+
+def batches_of(key, cuts):
+    """Split the stream at `cuts`; every batch is grouped by key (stable), i.e. the
+    stream the device sees is the concatenation of the grouped batches."""
+    bounds = [0] + sorted(cuts) + [len(key)]
+    order = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        order.append(a + np.argsort(key[a:b], kind="stable"))
+    return bounds, np.concatenate(order) if order else np.zeros(0, np.int64)
+
+
+def run_carry(ir, key, cols, bounds, mode=N.MODE_PROCESSOR, max_keys=None, sess=None, **kw):
+    cp = N.CompiledPattern(ir) if sess is None else sess.pattern
+    if sess is None:
+        sess = N.Session(cp, max(1, max(b - a for a, b in zip(bounds[:-1], bounds[1:]))), mode=mode, carry=True,
+                         max_keys=max_keys or int(key.max()) + 1)
+    got = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        if b == a:
+            continue
+        kw_b = {k: (None if v is None else np.ascontiguousarray(v[a:b])) for k, v in kw.items()}
+        sess.push(b - a, np.ascontiguousarray(key[a:b]), [np.ascontiguousarray(c[a:b]) for c in cols], **kw_b)
+        out = sess.collect(raise_on_error=False)
+        for m in range(len(out["match_record"])):
+            x, y = out["ent_off"][m], out["ent_off"][m + 1]
+            got.append((int(out["match_record"][m]), int(out["match_key"][m]),
+                        [(cp.names[out["ent_name"][i]], int(out["ent_record"][i])) for i in range(x, y)]))
+        if out["err"]:
+            return got, sess, (int(out["err"]), int(out["err_record"]))
+    return got, sess, None
+
+
+def rand_stream(seed, n_keys, per_key, vmax):
+    rng = np.random.default_rng(seed)
+    lens = rng.poisson(per_key, n_keys) + 1
+    key = np.repeat(np.arange(n_keys, dtype=np.int32), lens)
+    rng.shuffle(key)                                    # interleaved arrival, like a topic partition
+    val = rng.integers(0, vmax, len(key)).astype(np.int32)
+    return key, val
+
+
+CASES = [
+    ("c3_stock", PL.c3_stock, 7, lambda rng, n: (100 + np.cumsum(rng.integers(-5, 6, n))).astype(np.int32)),
+    ("c4_any", PL.c4_any, 4, None),
+    ("c5_optional", PL.c5_optional, 64, None),
+    ("next_one_or_more", PL.next_one_or_more, 4, None),
+    ("any_any", PL.any_any, 4, None),
+    ("c2_strict", synth.c2_pattern, 4, None),
+]
+
+
+@pytest.mark.parametrize("nbatch", [2, 7])
+@pytest.mark.parametrize("mode", [N.MODE_PROCESSOR, N.MODE_NFA])
+@pytest.mark.parametrize("name,mk,vmax,gen", CASES, ids=[c[0] for c in CASES])
+def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch):
+    per_key = 8 if name in ("c4_any", "any_any") else 25
+    key, val = rand_stream(len(name) * 7 + nbatch, 150, per_key, vmax)
+    if gen is not None:
+        val = gen(np.random.default_rng(3), len(key))
+    rng = np.random.default_rng(nbatch)
+    bounds, order = batches_of(key, list(rng.choice(np.arange(1, len(key)), nbatch - 1, replace=False)))
+    key, val = key[order], val[order]
+    ir = mk().to_ir(PL.I32)
+    omode = O.MODE_PROCESSOR if mode == N.MODE_PROCESSOR else O.MODE_NFA_PER_KEY
+    want, r, oerr = oracle_run(ir, key, [val], [1], omode)
+    got, sess, gerr = run_carry(ir, key, [val], bounds, mode=mode)
+    assert oerr is None and gerr is None
+    assert len(want) > 0
+    assert got == want
+    for k in np.unique(key):                            # NFA.getRuns() and queue length per key
+        assert sess.key_state(int(k)) == r.state(int(k)), int(k)
+
+
+def test_record_at_a_time_integration_fixture():
+    """CEPStreamIntegrationTest.java:117-168 driven one record per batch, as the
+    reference's processor sees it."""
+    fx = [f for f in scenarios() if f["name"] == "integration_multiple_keys"][0]
+    a = event_arrays(fx)
+    ir = bytes.fromhex(fx["ir"])
+    key = a["key"].astype(np.int32)
+    kw = {f: a[f] for f in ("topic", "partition", "offset", "ts") if a[f] is not None}
+    want, _, _ = oracle_run(ir, key, a["cols"], a["coltypes"], O.MODE_PROCESSOR, **kw)
+    got, _, err = run_carry(ir, key, a["cols"], list(range(len(key) + 1)), **kw)
+    assert err is None and got == want
+    assert len(got) == len(fx["expected"]["sequences"])
+
+
+def test_export_import_roundtrip():
+    """Checkpoint after batch 1 (cep_state_export), restore into a fresh session
+    (cep_state_import), continue with batch 2: same matches and state as one session."""
+    key, val = rand_stream(5, 200, 30, 4)
+    bounds, order = batches_of(key, [len(key) // 2])
+    key, val = key[order], val[order]
+    ir = PL.next_one_or_more().to_ir(PL.I32)
+    whole, s1, _ = run_carry(ir, key, [val], bounds)
+    part1, s2, _ = run_carry(ir, key, [val], bounds[:2])
+    blob = s2.state_export()
+    s3 = N.Session(N.CompiledPattern(ir), len(key), carry=True, max_keys=200)
+    s3.state_import(blob)
+    assert s3.stream_position() == bounds[1]
+    part2, _, _ = run_carry(ir, key, [val], bounds[1:], sess=s3)
+    assert part1 + part2 == whole and len(part2) > 0
+    for k in range(200):
+        assert s3.key_state(k) == s1.key_state(k)
+    # a key range exports only those keys
+    lo = N.Session(N.CompiledPattern(ir), len(key), carry=True, max_keys=200)
+    lo.state_import(s1.state_export(0, 50))
+    assert all(lo.key_state(k) is None for k in range(50, 200))
+    assert all(lo.key_state(k) == s1.key_state(k) for k in range(50))
+
+
+def test_high_water_mark_across_batches():
+    """CEPProcessor.checkHighWaterMark (:152-160) remembers offsets across batches:
+    a record re-delivered in a later batch (same key, value and offset: Kafka
+    re-delivery after a failure) is dropped; null records are skipped."""
+    rng = np.random.default_rng(11)
+    key0, val0 = rand_stream(12, 80, 20, 4)
+    n0 = len(key0)
+    off0 = np.arange(n0, dtype=np.int64)
+    stream = list(range(n0))
+    for i in rng.choice(n0, n0 // 6, replace=False):   # re-deliver record i somewhere after it
+        j = int(rng.integers(stream.index(i) + 1, len(stream) + 1))
+        stream.insert(j, int(i))
+    idx = np.array(stream)
+    key, val, offset = key0[idx], val0[idx], off0[idx]
+    valid = (rng.random(len(idx)) > 0.1).astype(np.uint8)
+    bounds, order = batches_of(key, [len(key) // 3, 2 * len(key) // 3])
+    key, val, offset, valid = key[order], val[order], offset[order], valid[order]
+    ir = PL.any_any().to_ir(PL.I32)
+    want, r, _ = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR, offset=offset, valid=valid)
+    got, sess, err = run_carry(ir, key, [val], bounds, offset=offset, valid=valid)
+    assert err is None and got == want and len(got) > 0
+
+
+def test_sequence_condition_reads_carried_events():
+    """SequenceMatcher averages over the partial sequence (SequenceMatcher.java:21-26):
+    with batches of one record every event it averages comes from carried state."""
+    fx = [f for f in scenarios() if f["name"] == "nfa_sequence_condition"][0]
+    a = event_arrays(fx)
+    ir = bytes.fromhex(fx["ir"])
+    key = np.zeros(len(a["key"]), np.int32)
+    kw = {f: a[f] for f in ("topic", "partition", "offset", "ts") if a[f] is not None}
+    want, _, _ = oracle_run(ir, key, a["cols"], a["coltypes"], O.MODE_NFA_PER_KEY, **kw)
+    got, _, err = run_carry(ir, key, a["cols"], list(range(len(key) + 1)), mode=N.MODE_NFA, max_keys=1, **kw)
+    assert err is None and got == want and len(got) == len(fx["expected"]["sequences"])
+
+
+def test_key_id_out_of_range_is_rejected():
+    ir = PL.any_any().to_ir(PL.I32)
+    s = N.Session(N.CompiledPattern(ir), 10, carry=True, max_keys=4)
+    with pytest.raises(N.CepError) as e:
+        s.push(2, np.array([1, 9], np.int32), [np.zeros(2, np.int32)])
+    assert e.value.code == 11
