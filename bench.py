@@ -129,13 +129,13 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        if sess.path == N.PATH_GENERAL:      # the general push syncs internally; read its kernel time
+        if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):   # these pushes sync internally; read the kernel time
             kernel_ms.append(sess.last_kernel_ms())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if sess.path != N.PATH_GENERAL:
+    if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
         # one more pass per step under HIP events on the launch stream (cep_last_kernel_ms)
         for _ in range(args.steps):
             step()
@@ -147,7 +147,7 @@ def main():
     tot_events, tot_matches, t_max = gather_stats(stats, world)
 
     if rank == 0:
-        if sess.path != N.PATH_GENERAL:
+        if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
             k = pat.info.stencil_k
             algo_bytes = 8.0 * n + 4.0 * k * n_matches          # 8 B/event + 4k B/match
         else:
@@ -172,16 +172,16 @@ def main():
             "data": "synthetic (splitmix64 counter RNG, BASELINE.md §3)",
             "config": {"workload": C["desc"], "events_per_gpu": n, "keys_per_gpu": K,
                        "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
-                       "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain"}.get(sess.path, "general"),
+                       "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain", N.PATH_RUNS: "runs"}.get(sess.path, "general"),
                        "parallelism": f"key-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
-                         "kernel": "nfa_kernel" if sess.path == N.PATH_GENERAL else "stencil_kernel",
+                         "kernel": {N.PATH_GENERAL: "nfa_kernel", N.PATH_RUNS: "runs_sim"}.get(sess.path, "stencil_kernel"),
                          "kernel_ms": avg_kernel_ms, "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",
         }
-        if sess.path == N.PATH_GENERAL:
+        if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):
             line["batch_ms"] = sess.last_batch_ms()
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = _cpu_baseline(args.config, key, cols, ts, ir, args.cpu_threads, n_matches, csum,

@@ -55,6 +55,8 @@ extern "C" {
 /* execution path chosen by cep_session_open */
 #define CEP_PATH_STENCIL 1        /* strict single-cardinality patterns: k-event stencil */
 #define CEP_PATH_GENERAL 2        /* full NFA: runs, Dewey versions, shared versioned buffer */
+#define CEP_PATH_RUNS 4           /* strict patterns whose runs never branch (stateful predicates, folds,
+                                     oneOrMore with exclusive TAKE/PROCEED): one lane per start record */
 #define CEP_PATH_CHAIN 3          /* strict single-cardinality patterns with optional() stages: the stencil
                                      kernel with deterministic per-start runs (variable-length matches) */
 
@@ -69,6 +71,7 @@ typedef struct {
   int32_t stencil_ok;      /* 1 if the strict stencil path applies */
   int32_t stencil_k;       /* number of stages of a stencil/chain pattern */
   int32_t chain_ok;        /* 1 if the chain path (strict + optional stages) applies */
+  int32_t runs_ok;         /* 1 if the deterministic-runs path applies */
 } cep_pattern_info;
 
 typedef struct {

@@ -43,6 +43,15 @@ hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* 
                                const int32_t* res_err, int64_t* ctab, hipStream_t st);
 hipError_t carry_sizes_launch(const int64_t* ctab, int64_t nkeys, const int32_t* cpool, int64_t* words,
                               hipStream_t st);
+hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st);
+hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
+                               unsigned long long* out, hipStream_t st);
+hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
+                     size_t* tmp_bytes, hipStream_t st);
+hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,
+                             int64_t* ent_off, int64_t* total, int64_t* scan_tmp, int64_t* match_record,
+                             int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name, int64_t* ent_record,
+                             hipStream_t st, bool lengths_only);
 hipError_t carry_move_launch(int64_t* ctab, int64_t nkeys, const int32_t* src, const int64_t* off, int32_t* dst,
                              hipStream_t st);
 }  // namespace kcep
@@ -129,6 +138,8 @@ struct cep_session {
   int64_t base = 0;             // stream position of the next batch's record 0
   DBuf ctab, cpool;             // per key id: blob offset (-1 none); blobs (int32 words)
   int64_t cpool_words = 0, cpool_used = 0;
+  // ---- deterministic runs workspace ----
+  DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof;
   int32_t g_err = CEP_OK;
   int64_t g_err_rec = -1;
   // ---- host CSR of the last collect ----
@@ -223,13 +234,10 @@ int carry_gc(cep_session* s, int64_t min_words, hipStream_t st) {
   return CEP_OK;
 }
 
-int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
+// batch columns on the device (host batches staged through the session's buffers)
+int stage_inputs(cep_session* s, const cep_batch* b, hipStream_t st, NfaArgs& A) {
   const Program& P = s->pat->prog;
   const int64_t n = b->n;
-  NfaArgs A{};
-  A.P = s->dprog.as<DevProgram>();
-  A.n = n;
-  A.mode = s->opts.mode;
   int rc = CEP_OK;
   if (b->mem == CEP_MEM_HOST) {
     if ((rc = stage(s, s->h_key, b->key_id, n, st, &A.key)) || (rc = stage(s, s->h_valid, b->valid, n, st, &A.valid)) ||
@@ -250,6 +258,103 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.offset = b->offset; A.ts = b->ts;
     for (int c = 0; c < b->n_cols; c++) A.cols[c] = b->cols[c];
   }
+  return CEP_OK;
+}
+
+// Deterministic strict runs (runs.hip): one lane per start record, completed runs
+// ordered by (completing record, start), traversals written into the general CSR.
+int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
+  const int64_t n = b->n;
+  NfaArgs in{};
+  int rc = stage_inputs(s, b, st, in);
+  if (rc) return rc;
+  s->d_key = in.key;
+  s->g_err = CEP_OK;
+  s->g_err_rec = -1;
+  s->g_matches = s->g_entries = 0;
+  HIPCHECK(hipEventRecord(s->ev0, st));
+  if (n == 0) {
+    HIPCHECK(hipEventRecord(s->ev1, st));
+    HIPCHECK(hipEventRecord(s->eb1, st));
+    return CEP_OK;
+  }
+  if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
+      s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 2) * 8) ||
+      s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->r_endof.ensure(size_t(n) * 4))
+    return fail(CEP_E_HIP, "allocation failed");
+  RunsArgs A{};
+  A.P = s->dprog.as<DevProgram>();
+  A.key = in.key; A.topic = in.topic; A.partition = in.partition; A.offset = in.offset; A.ts = in.ts;
+  for (int c = 0; c < 16; c++) A.cols[c] = in.cols[c];
+  A.n = n;
+  A.base = 0;
+  unsigned long long* ctl = s->ctl.as<unsigned long long>();
+  A.nmatch = ctl;
+  A.err_min = ctl + 1;
+  A.match_key = s->rk.as<unsigned long long>();
+  A.match_cap = n;
+  A.err_code = s->r_errcode.as<int32_t>();
+  const unsigned long long init[2] = {0, ~0ull};
+  HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
+  HIPCHECK(runs_sim_launch(A, s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), st));
+  HIPCHECK(hipEventRecord(s->ev1, st));
+  int64_t* scal0 = s->scal.as<int64_t>();
+  HIPCHECK(exclusive_scan(s->flag.as<int64_t>(), n, s->idx.as<int64_t>(), scal0 + 3, s->scan_tmp.as<int64_t>(), st));
+  HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->r_endof.as<int32_t>(), n,
+                               s->rk.as<unsigned long long>(), st));
+  unsigned long long res[2];
+  HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(&res[0], scal0 + 3, 8, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const int64_t nm = int64_t(res[0]);
+  if (nm > n) return fail(CEP_E_RUN_CAPACITY, "more completed runs than records");
+  if (res[1] != ~0ull) {                           // the reference's first exception
+    const int64_t at = int64_t(res[1] >> 31), j = int64_t(res[1] & 0x7FFFFFFFull);
+    int32_t code = 0;
+    HIPCHECK(hipMemcpy(&code, s->r_errcode.as<int32_t>() + j, 4, hipMemcpyDeviceToHost));
+    if (code == CEP_E_UNSUPPORTED) return fail(CEP_E_UNSUPPORTED, "sequence condition on the runs path");
+    s->g_err = code;
+    s->g_err_rec = at;
+  }
+  int bits = 31;
+  while ((int64_t(1) << (bits - 31)) <= n) bits++;
+  size_t tmp_bytes = 0;
+  HIPCHECK(runs_sort(nullptr, nullptr, nm, bits, nullptr, &tmp_bytes, st));
+  if (s->rk_tmp.ensure(std::max<size_t>(tmp_bytes, 16)) || s->r_len.ensure(size_t(std::max<int64_t>(nm, 1)) * 8) ||
+      s->r_entoff.ensure(size_t(std::max<int64_t>(nm, 1)) * 8) || s->scan_tmp.ensure(size_t(nm / 1024 + 2) * 8))
+    return fail(CEP_E_HIP, "allocation failed");
+  if (nm > 0)
+    HIPCHECK(runs_sort(s->rk.as<unsigned long long>(), s->rk_sorted.as<unsigned long long>(), nm, bits, s->rk_tmp.p,
+                       &tmp_bytes, st));
+  int64_t* scal = s->scal.as<int64_t>();
+  HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
+                             s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
+                             nullptr, nullptr, nullptr, st, true));
+  const int64_t ne = read_i64(scal + 4, st, &rc);
+  if (rc) return fail(rc, "entry count");
+  const size_t nmb = size_t(std::max<int64_t>(nm, 1)), neb = size_t(std::max<int64_t>(ne, 1));
+  if (s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) || s->o_entoff.ensure(nmb * 8) ||
+      s->o_name.ensure(neb * 4) || s->o_entrec.ensure(neb * 8))
+    return fail(CEP_E_HIP, "allocation failed");
+  HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
+                             s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), s->o_record.as<int64_t>(),
+                             s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
+                             s->o_entrec.as<int64_t>(), st, false));
+  HIPCHECK(hipEventRecord(s->eb1, st));
+  s->g_matches = nm;
+  s->g_entries = ne;
+  return CEP_OK;
+}
+
+int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
+  const Program& P = s->pat->prog;
+  const int64_t n = b->n;
+  NfaArgs A{};
+  A.P = s->dprog.as<DevProgram>();
+  A.n = n;
+  A.mode = s->opts.mode;
+  int rc = stage_inputs(s, b, st, A);
+  if (rc) return rc;
   s->d_key = A.key;
   s->g_err = CEP_OK;
   s->g_err_rec = -1;
@@ -411,6 +516,7 @@ int cep_pattern_get_info(const cep_pattern* p, cep_pattern_info* o) {
   o->stencil_ok = P.stencil_ok && !P.stencil.chain ? 1 : 0;
   o->stencil_k = P.stencil_ok ? P.stencil.k : 0;
   o->chain_ok = P.stencil_ok && P.stencil.chain ? 1 : 0;
+  o->runs_ok = P.runs_ok ? 1 : 0;
   return CEP_OK;
 }
 
@@ -441,13 +547,15 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   const Program& P = p->prog;
   int path = opts->force_path;
   const int fast = P.stencil.chain ? CEP_PATH_CHAIN : CEP_PATH_STENCIL;   // the streaming kernel's flavour
-  if (path == 0) path = P.stencil_ok ? fast : CEP_PATH_GENERAL;
+  if (path == 0) path = P.stencil_ok ? fast : P.runs_ok ? CEP_PATH_RUNS : CEP_PATH_GENERAL;
+  if (path == CEP_PATH_RUNS && !P.runs_ok) return fail(CEP_E_UNSUPPORTED, "runs path does not apply: " + P.runs_why);
   if ((path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN) && !P.stencil_ok)
     return fail(CEP_E_UNSUPPORTED, "stencil path does not apply: " + P.stencil_why);
   if (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN) path = fast;
   if (path == CEP_PATH_GENERAL && !P.general_ok)
     return fail(CEP_E_UNSUPPORTED, "pattern cannot be lowered to the device NFA: " + P.general_why);
-  if (path != CEP_PATH_STENCIL && path != CEP_PATH_CHAIN && path != CEP_PATH_GENERAL) return fail(CEP_E_ARG, "bad path");
+  if (path != CEP_PATH_STENCIL && path != CEP_PATH_CHAIN && path != CEP_PATH_GENERAL && path != CEP_PATH_RUNS)
+    return fail(CEP_E_ARG, "bad path");
   const bool carry = opts->flags & CEP_SESSION_CARRY;
   if (carry && (opts->max_keys <= 0 || opts->max_keys > INT32_MAX))
     return fail(CEP_E_ARG, "carry sessions need max_keys (dense key ids in [0, max_keys))");
@@ -506,7 +614,8 @@ void cep_session_close(cep_session* s) {
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
-                  &s->o_entrec, &s->ctab, &s->cpool})
+                  &s->o_entrec, &s->ctab, &s->cpool, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
+                  &s->r_errcode, &s->r_endof})
     b->release();
   for (auto& c : s->h_cols) c.release();
   if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -536,7 +645,11 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   // break contiguity: the stencil only takes batches without them
   const bool stencil_batch = !b->valid && !(s->opts.mode == CEP_MODE_PROCESSOR && b->offset &&
                                             !(b->flags & CEP_BATCH_OFFSETS_MONOTONE));
-  if (s->path != CEP_PATH_GENERAL && stencil_batch) {
+  if (s->path == CEP_PATH_RUNS && stencil_batch) {
+    s->last_path = CEP_PATH_RUNS;
+    return push_runs(s, b, st);
+  }
+  if (s->path != CEP_PATH_GENERAL && s->path != CEP_PATH_RUNS && stencil_batch) {
     s->last_path = s->path;
     return push_stencil(s, b, st);
   }
@@ -566,7 +679,7 @@ int cep_collect(cep_session* s, cep_matches* o) {
   if (!s || !o) return fail(CEP_E_ARG, "null argument");
   memset(o, 0, sizeof *o);
   HIPCHECK(hipSetDevice(s->device));
-  if (s->last_path == CEP_PATH_GENERAL) {
+  if (s->last_path == CEP_PATH_GENERAL || s->last_path == CEP_PATH_RUNS) {
     HIPCHECK(hipStreamSynchronize(s->stream));
     const int64_t nm = s->g_matches, ne = s->g_entries;
     s->match_record.resize(size_t(nm));
@@ -586,7 +699,7 @@ int cep_collect(cep_session* s, cep_matches* o) {
     s->ent_off[size_t(nm)] = ne;
     o->n_matches = nm;
     o->n_entries = ne;
-    o->path = CEP_PATH_GENERAL;
+    o->path = s->last_path;
     o->err = s->g_err;
     o->err_record = s->g_err_rec;
     if (s->g_err) g_err = "the reference NFA raises an exception on this batch";
@@ -647,7 +760,7 @@ int cep_collect(cep_session* s, cep_matches* o) {
 int cep_checksum(cep_session* s, uint64_t* sum, int64_t* n_matches) {
   if (!s || !sum) return fail(CEP_E_ARG, "null argument");
   HIPCHECK(hipSetDevice(s->device));
-  if (s->last_path == CEP_PATH_GENERAL) {
+  if (s->last_path == CEP_PATH_GENERAL || s->last_path == CEP_PATH_RUNS) {
     cep_matches m;
     int rc = cep_collect(s, &m);
     if (rc) return rc;

@@ -463,13 +463,114 @@ void analyse_stencil(Program& P) {
   P.stencil_why.clear();
 }
 
+// ---------------------------------------------------------------- deterministic runs
+bool same_expr(const ExprP& a, const ExprP& b) {
+  if (!a || !b) return a == b;
+  if (a->op != b->op || a->t != b->t || a->ct != b->ct) return false;
+  switch (a->op) {
+    case OP_CONST_I32: case OP_EV_TOPIC_EQ: if (a->i32 != b->i32) return false; break;
+    case OP_CONST_I64: if (a->i64 != b->i64) return false; break;
+    case OP_CONST_F64: if (memcmp(&a->f64, &b->f64, sizeof(double)) != 0) return false; break;
+    case OP_FIELD: case OP_SEQ_AVG: if (a->col != b->col) return false; break;
+    case OP_STATE_GET: case OP_STATE_GET_OR_ELSE: if (a->name != b->name) return false; break;
+    default: break;
+  }
+  return same_expr(a->a, b->a) && same_expr(a->b, b->b);
+}
+bool is_cmp(uint8_t op) { return op >= OP_EQ && op <= OP_GE; }
+bool complementary(uint8_t x, uint8_t y) {
+  auto c = [](uint8_t o) -> uint8_t {
+    switch (o) { case OP_EQ: return OP_NE; case OP_NE: return OP_EQ; case OP_LT: return OP_GE;
+                 case OP_GE: return OP_LT; case OP_GT: return OP_LE; case OP_LE: return OP_GT; }
+    return 0;
+  };
+  return c(x) == y;
+}
+uint8_t flip_cmp(uint8_t o) {
+  switch (o) { case OP_LT: return OP_GT; case OP_LE: return OP_GE; case OP_GT: return OP_LT; case OP_GE: return OP_LE; }
+  return o;
+}
+// p AND q can never both be true (whatever the run's states): structural
+// complements, different topics, or disjoint value intervals of one column
+bool disjoint(const ExprP& p, const ExprP& q) {
+  if (!p || !q) return false;                                   // TRUE
+  if (p->op == OP_FALSE || q->op == OP_FALSE) return true;
+  if (p->op == OP_AND) return disjoint(p->a, q) || disjoint(p->b, q);
+  if (q->op == OP_AND) return disjoint(p, q->a) || disjoint(p, q->b);
+  if (p->op == OP_OR) return disjoint(p->a, q) && disjoint(p->b, q);
+  if (q->op == OP_OR) return disjoint(p, q->a) && disjoint(p, q->b);
+  if (p->op == OP_NOT && same_expr(p->a, q)) return true;
+  if (q->op == OP_NOT && same_expr(q->a, p)) return true;
+  if (p->op == OP_EV_TOPIC_EQ && q->op == OP_EV_TOPIC_EQ) return p->i32 != q->i32;
+  if (is_cmp(p->op) && is_cmp(q->op)) {
+    if (same_expr(p->a, q->a) && same_expr(p->b, q->b) && complementary(p->op, q->op)) return true;
+    if (same_expr(p->a, q->b) && same_expr(p->b, q->a) && complementary(p->op, flip_cmp(q->op))) return true;
+  }
+  Lowering L;
+  DNF a = L.lower(p, false), b = L.lower(q, false);
+  if (!L.ok) return false;
+  for (auto& ta : a)
+    for (auto& tb : b) {
+      Term t = ta;
+      if (L.intersect(t, tb)) return false;
+    }
+  return true;
+}
+bool uses_seq(const ExprP& e) { return e && (e->op == OP_SEQ_AVG || uses_seq(e->a) || uses_seq(e->b)); }
+
+// Strict patterns whose stages never take a branching edge combination
+// (NFA.java:392-397): without IGNORE edges that needs TAKE and PROCEED of a
+// oneOrMore stage to exclude each other, i.e. its predicate and its successor's
+// to be disjoint (PROCEED = succ OR NOT pred, StagesFactory.java:131-137).  Then
+// every run is one deterministic walk over consecutive records from the record
+// its begin stage consumed: it owns a fresh run sequence (so its aggregates),
+// its Dewey versions start with a digit no other run has, and its buffer
+// traversal returns exactly the records it consumed.
+void analyse_runs(Program& P) {
+  auto no = [&](const std::string& w) { P.runs_ok = false; P.runs_why = w; };
+  if (!P.general_ok) return no("not lowered to the device NFA");
+  if (P.states.size() > size_t(RUNS_MAX_STATES)) return no("more than 8 aggregate states");
+  const int k = int(P.pats.size());
+  for (int i = 0; i < k; i++) {
+    const auto& p = P.pats[i];
+    if (p.strategy != S_STRICT) return no("non-strict selection strategy");
+    if (i == 0 && (p.one_or_more || p.times > 1 || p.optional)) return no("quantifier on the first stage");
+    if (p.one_or_more && (p.optional || p.times > 1)) return no("zeroOrMore");
+    if (uses_seq(p.pred)) return no("sequence condition");
+    for (auto& f : p.folds)
+      if (uses_seq(f.expr)) return no("sequence condition");
+    if (p.one_or_more) {
+      const auto& q = P.pats[i + 1];
+      ExprP pw = p.topic >= 0 ? mk(OP_AND, mk_topic(p.topic), p.pred) : p.pred;
+      ExprP qw = q.topic >= 0 ? mk(OP_AND, mk_topic(q.topic), q.pred) : q.pred;
+      if (!disjoint(pw, qw)) return no("oneOrMore predicate not provably exclusive of its successor's");
+    }
+  }
+  P.runs_ok = true;
+  P.runs_why.clear();
+}
+
 // ---------------------------------------------------------------- bytecode
 struct CodeGen {
   std::vector<int32_t> code;
   bool ok = true;
   std::string why;
+  int depth = 0, maxdepth = 0;      // operand-stack depth (the device keeps <= NFA_STACK slots in registers)
 
-  void op(uint8_t o, int a = 0, int b = 0) { code.push_back(int32_t(o) | (a << 8) | (b << 16)); }
+  static int effect(uint8_t o) {
+    switch (o) {
+      case BC_PUSH: case BC_FIELD: case BC_EV_KEY: case BC_EV_TS: case BC_EV_OFFSET: case BC_EV_PARTITION:
+      case BC_TOPIC_EQ: case BC_STATE_GET: case BC_FOLD_CURR: case BC_SEQ_AVG: return 1;
+      case BC_END: case BC_STATE_GET_OR_ELSE: case BC_NOT: case BC_NEG_I32: case BC_NEG_I64: case BC_NEG_F64:
+      case BC_I64_TO_I32: case BC_I_TO_F64: case BC_F64_TO_I32: case BC_F64_TO_I64: return 0;
+      default: return -1;           // binary operators, POP, and the fall-through of JZ/JNZ_KEEP
+    }
+  }
+  void op(uint8_t o, int a = 0, int b = 0) {
+    code.push_back(int32_t(o) | (a << 8) | (b << 16));
+    depth += effect(o);
+    maxdepth = std::max(maxdepth, depth);
+  }
   void push64(int64_t v) {
     op(BC_PUSH);
     code.push_back(int32_t(uint32_t(uint64_t(v))));
@@ -541,6 +642,7 @@ struct CodeGen {
   }
   int emit(const ExprP& e, uint8_t result_type = 0xFF) {
     const int at = int(code.size());
+    depth = 0;
     gen(e);
     if (result_type != 0xFF) cvt(e->t, result_type);
     op(BC_END);
@@ -571,7 +673,19 @@ int lower_general(Program& P, std::string& why) {
   D.begin = P.begin;
   D.nstates = int32_t(P.states.size());
   D.ncols = int32_t(P.coltypes.size());
-  D.maxdepth = D.nstages + 2;
+  // NFA.evaluate recurses along PROCEED / SKIP_PROCEED edges, which always lead
+  // to a later pattern's stage: the longest such path bounds the frame stack
+  {
+    std::vector<int> depth(P.stages.size(), 1);
+    for (int id = 0; id < int(P.stages.size()); id++)           // targets have smaller ids (built last-first)
+      for (auto& e : P.stages[id].edges)
+        if ((e.op == E_PROCEED || e.op == E_SKIP_PROCEED) && e.target >= 0)
+          depth[id] = std::max(depth[id], depth[e.target] + 1);
+    int m = 0;
+    for (int d : depth) m = std::max(m, d);
+    D.maxdepth = m + 1;                                          // + the epsilon frame a run starts on
+    if (D.maxdepth > NFA_MAX_FRAMES) { why = "PROCEED chain deeper than the device frame stack"; return CEP_E_UNSUPPORTED; }
+  }
   for (size_t c = 0; c < P.coltypes.size(); c++) D.coltype[c] = P.coltypes[c];
   D.ndefined = int32_t(P.defined_states.size());
   for (size_t i = 0; i < P.defined_states.size(); i++) D.defined[i] = P.defined_states[i];
@@ -610,6 +724,7 @@ int lower_general(Program& P, std::string& why) {
     }
   }
   if (!cg.ok) { why = cg.why; return CEP_E_UNSUPPORTED; }
+  if (cg.maxdepth > NFA_STACK) { why = "expression nests deeper than the device operand stack"; return CEP_E_UNSUPPORTED; }
   if (slots.size() > size_t(NFA_MAX_SLOTS)) { why = "too many buffer slots"; return CEP_E_UNSUPPORTED; }
   if (cg.code.size() > size_t(NFA_MAX_CODE)) { why = "predicate code too large"; return CEP_E_UNSUPPORTED; }
   D.nslots = int32_t(slots.size());
@@ -686,6 +801,7 @@ int compile_ir(const uint8_t* ir, size_t len, Program& P, std::string& err) {
   }
   analyse_stencil(P);
   P.general_ok = lower_general(P, P.general_why) == CEP_OK;
+  analyse_runs(P);
   return CEP_OK;
 }
 

@@ -1,0 +1,299 @@
+// interp.h — device interpreter of the predicate / fold bytecode (compile.cpp CodeGen).
+//
+// Java semantics of Matcher.accept / Aggregator.aggregate bodies: 32/64-bit
+// wrap-around, integer "/ by zero" -> ArithmeticException, boxed-type checks on
+// state reads (ClassCastException), States.get on an unset state ->
+// UnknownAggregateException (States.java:56-60), short-circuit && and ||.
+// The operand stack is a shift register of NFA_STACK slots (s[0] is the top):
+// the compiler bounds every program's depth, so it stays in registers.
+//
+// Env supplies the record and run context:
+//   int64_t field(int col, int type); int64_t key(); int64_t ts(); int64_t off();
+//   int64_t part(); int32_t topic();
+//   bool state(int idx, int32_t& tag, int64_t& bits);   // false: failure already recorded
+//   bool seq_avg(int col, int64_t& bits);
+//   void fail(int code);
+//   bool in_fold; int32_t curr_tag; int64_t curr;        // Aggregator's current value
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/kcep.h"
+#include "kcep_internal.h"
+
+namespace kcep {
+
+__device__ __forceinline__ double bc_f(int64_t b) { return __builtin_bit_cast(double, b); }
+__device__ __forceinline__ int64_t bc_b(double d) { return __builtin_bit_cast(int64_t, d); }
+__device__ __forceinline__ int64_t bc_sx32(int64_t x) { return int64_t(int32_t(uint32_t(uint64_t(x)))); }
+
+struct BcStack {
+  int64_t s[NFA_STACK];
+  __device__ __forceinline__ void push(int64_t v) {
+#pragma unroll
+    for (int i = NFA_STACK - 1; i > 0; i--) s[i] = s[i - 1];
+    s[0] = v;
+  }
+  __device__ __forceinline__ void pop() {
+#pragma unroll
+    for (int i = 0; i < NFA_STACK - 1; i++) s[i] = s[i + 1];
+  }
+};
+
+template <class Env>
+__device__ __forceinline__ bool interp(const int32_t* __restrict__ code, int pc, Env& env, int64_t& result) {
+  BcStack st;
+#pragma unroll
+  for (int i = 0; i < NFA_STACK; i++) st.s[i] = 0;
+  for (;;) {
+    const int32_t w = code[pc++];
+    const int op = w & 0xFF, a = (w >> 8) & 0xFF, b = (w >> 16) & 0xFF;
+    switch (op) {
+      case BC_END: result = st.s[0]; return true;
+      case BC_PUSH: st.push(int64_t(uint32_t(code[pc])) | (int64_t(code[pc + 1]) << 32)); pc += 2; break;
+      case BC_FIELD: st.push(env.field(a, b)); break;
+      case BC_EV_KEY: st.push(env.key()); break;
+      case BC_EV_TS: st.push(env.ts()); break;
+      case BC_EV_OFFSET: st.push(env.off()); break;
+      case BC_EV_PARTITION: st.push(env.part()); break;
+      case BC_TOPIC_EQ: st.push(env.topic() == code[pc] ? 1 : 0); pc++; break;
+      case BC_STATE_GET: case BC_STATE_GET_OR_ELSE: {          // States.get / getOrElse (States.java:56-78)
+        int32_t tag;
+        int64_t v;
+        if (!env.state(a, tag, v)) return false;
+        if (tag == 0) {
+          if (op == BC_STATE_GET) { env.fail(CEP_E_UNKNOWN_AGGREGATE); return false; }
+          pc++;                                                  // evaluate the default
+          break;
+        }
+        if (tag != b) { env.fail(CEP_E_CLASS_CAST); return false; }
+        st.push(v);
+        if (op == BC_STATE_GET_OR_ELSE) pc += 1 + code[pc];
+        break;
+      }
+      case BC_FOLD_CURR:
+        if (!env.in_fold || env.curr_tag == 0) { env.fail(CEP_E_NPE); return false; }
+        if (env.curr_tag != b) { env.fail(CEP_E_CLASS_CAST); return false; }
+        st.push(env.curr);
+        break;
+      case BC_SEQ_AVG: {
+        int64_t v;
+        if (!env.seq_avg(a, v)) return false;
+        st.push(v);
+        break;
+      }
+      case BC_NOT: st.s[0] = st.s[0] ? 0 : 1; break;
+      case BC_JZ_KEEP: if (st.s[0] == 0) pc += 1 + code[pc]; else { st.pop(); pc++; } break;
+      case BC_JNZ_KEEP: if (st.s[0] != 0) pc += 1 + code[pc]; else { st.pop(); pc++; } break;
+      case BC_POP: st.pop(); break;
+      case BC_NEG_I32: st.s[0] = bc_sx32(0 - st.s[0]); break;
+      case BC_NEG_I64: st.s[0] = int64_t(0ull - uint64_t(st.s[0])); break;
+      case BC_NEG_F64: st.s[0] = bc_b(-bc_f(st.s[0])); break;
+      case BC_I64_TO_I32: st.s[0] = bc_sx32(st.s[0]); break;
+      case BC_I_TO_F64: st.s[0] = bc_b(double(st.s[0])); break;
+      case BC_F64_TO_I32: {
+        const double d = bc_f(st.s[0]);
+        st.s[0] = d != d ? 0 : d >= 2147483647.0 ? INT32_MAX : d <= -2147483648.0 ? INT32_MIN : int64_t(int32_t(d));
+        break;
+      }
+      case BC_F64_TO_I64: {
+        const double d = bc_f(st.s[0]);
+        st.s[0] = d != d ? 0 : d >= 9223372036854775807.0 ? INT64_MAX : d <= -9223372036854775808.0 ? INT64_MIN : int64_t(d);
+        break;
+      }
+      default: {
+        const int64_t y = st.s[0], x = st.s[1];
+        int64_t z = 0;
+        switch (op) {
+          case BC_ADD_I32: z = bc_sx32(x + y); break;
+          case BC_SUB_I32: z = bc_sx32(x - y); break;
+          case BC_MUL_I32: z = bc_sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
+          case BC_DIV_I32:
+            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
+            z = (x == INT32_MIN && y == -1) ? INT32_MIN : x / y;
+            break;
+          case BC_REM_I32:
+            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
+            z = y == -1 ? 0 : x % y;
+            break;
+          case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
+          case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
+          case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
+          case BC_DIV_I64:
+            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
+            z = (x == INT64_MIN && y == -1) ? INT64_MIN : x / y;
+            break;
+          case BC_REM_I64:
+            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
+            z = y == -1 ? 0 : x % y;
+            break;
+          case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;
+          case BC_SUB_F64: z = bc_b(bc_f(x) - bc_f(y)); break;
+          case BC_MUL_F64: z = bc_b(bc_f(x) * bc_f(y)); break;
+          case BC_DIV_F64: z = bc_b(bc_f(x) / bc_f(y)); break;
+          case BC_REM_F64: z = bc_b(fmod(bc_f(x), bc_f(y))); break;
+          case BC_EQ_I: z = x == y; break;
+          case BC_NE_I: z = x != y; break;
+          case BC_LT_I: z = x < y; break;
+          case BC_LE_I: z = x <= y; break;
+          case BC_GT_I: z = x > y; break;
+          case BC_GE_I: z = x >= y; break;
+          case BC_EQ_F: z = bc_f(x) == bc_f(y); break;
+          case BC_NE_F: z = bc_f(x) != bc_f(y); break;
+          case BC_LT_F: z = bc_f(x) < bc_f(y); break;
+          case BC_LE_F: z = bc_f(x) <= bc_f(y); break;
+          case BC_GT_F: z = bc_f(x) > bc_f(y); break;
+          case BC_GE_F: z = bc_f(x) >= bc_f(y); break;
+          case BC_EQ_B: z = (x != 0) == (y != 0); break;
+          case BC_NE_B: z = (x != 0) != (y != 0); break;
+          default: env.fail(CEP_E_BAD_IR); return false;
+        }
+        st.pop();
+        st.s[0] = z;
+      }
+    }
+  }
+}
+
+// Lock-step variant: every lane of the wave walks the same program with a
+// wave-uniform pc (the opcode switch is a scalar branch, no divergence); lanes
+// not taking part (active = false) or jumped over a region (short-circuit &&,
+// ||, getOrElse) follow along inactive until their resume point.  Jumps are
+// forward and nested, so a lane resumes exactly at its target instruction.
+// Returns false for a lane that raised (env.fail) -- only active lanes raise.
+template <class Env>
+__device__ __forceinline__ bool interp_ls(const int32_t* __restrict__ code, int pc0, Env& env, bool active,
+                                          int64_t& result) {
+  BcStack st;
+#pragma unroll
+  for (int i = 0; i < NFA_STACK; i++) st.s[i] = 0;
+  int pc = __builtin_amdgcn_readfirstlane(pc0);
+  int resume = active ? -1 : 0x7FFFFFFF;
+  bool ok = true;
+  result = 0;
+  for (;;) {
+    if (resume == pc) resume = -1;
+    const bool on = resume < 0 && ok;
+    const int32_t w = code[pc];
+    const int op = w & 0xFF, a = (w >> 8) & 0xFF, b = (w >> 16) & 0xFF;
+    pc++;
+    switch (op) {
+      case BC_END: if (on) result = st.s[0]; return ok;
+      case BC_PUSH: if (on) st.push(int64_t(uint32_t(code[pc])) | (int64_t(code[pc + 1]) << 32)); pc += 2; break;
+      case BC_FIELD: if (on) st.push(env.field(a, b)); break;
+      case BC_EV_KEY: if (on) st.push(env.key()); break;
+      case BC_EV_TS: if (on) st.push(env.ts()); break;
+      case BC_EV_OFFSET: if (on) st.push(env.off()); break;
+      case BC_EV_PARTITION: if (on) st.push(env.part()); break;
+      case BC_TOPIC_EQ: if (on) st.push(env.topic() == code[pc] ? 1 : 0); pc++; break;
+      case BC_STATE_GET: {
+        if (on) {
+          int32_t tag;
+          int64_t v;
+          if (!env.state(a, tag, v)) ok = false;
+          else if (tag == 0) { env.fail(CEP_E_UNKNOWN_AGGREGATE); ok = false; }
+          else if (tag != b) { env.fail(CEP_E_CLASS_CAST); ok = false; }
+          else st.push(v);
+        }
+        break;
+      }
+      case BC_STATE_GET_OR_ELSE: {                              // the default's code follows; skip it if set
+        const int target = pc + 1 + code[pc];
+        if (on) {
+          int32_t tag;
+          int64_t v;
+          if (!env.state(a, tag, v)) ok = false;
+          else if (tag != 0) {
+            if (tag != b) { env.fail(CEP_E_CLASS_CAST); ok = false; }
+            else { st.push(v); resume = target; }
+          }
+        }
+        pc++;
+        break;
+      }
+      case BC_FOLD_CURR:
+        if (on) {
+          if (!env.in_fold || env.curr_tag == 0) { env.fail(CEP_E_NPE); ok = false; }
+          else if (env.curr_tag != b) { env.fail(CEP_E_CLASS_CAST); ok = false; }
+          else st.push(env.curr);
+        }
+        break;
+      case BC_SEQ_AVG: {
+        if (on) {
+          int64_t v;
+          if (!env.seq_avg(a, v)) ok = false;
+          else st.push(v);
+        }
+        break;
+      }
+      case BC_NOT: if (on) st.s[0] = st.s[0] ? 0 : 1; break;
+      case BC_JZ_KEEP: case BC_JNZ_KEEP: {
+        const int target = pc + 1 + code[pc];
+        if (on) {
+          const bool jump = op == BC_JZ_KEEP ? st.s[0] == 0 : st.s[0] != 0;
+          if (jump) resume = target;
+          else st.pop();
+        }
+        pc++;
+        break;
+      }
+      case BC_POP: if (on) st.pop(); break;
+      case BC_NEG_I32: if (on) st.s[0] = bc_sx32(0 - st.s[0]); break;
+      case BC_NEG_I64: if (on) st.s[0] = int64_t(0ull - uint64_t(st.s[0])); break;
+      case BC_NEG_F64: if (on) st.s[0] = bc_b(-bc_f(st.s[0])); break;
+      case BC_I64_TO_I32: if (on) st.s[0] = bc_sx32(st.s[0]); break;
+      case BC_I_TO_F64: if (on) st.s[0] = bc_b(double(st.s[0])); break;
+      case BC_F64_TO_I32: {
+        const double d = bc_f(st.s[0]);
+        if (on) st.s[0] = d != d ? 0 : d >= 2147483647.0 ? INT32_MAX : d <= -2147483648.0 ? INT32_MIN : int64_t(int32_t(d));
+        break;
+      }
+      case BC_F64_TO_I64: {
+        const double d = bc_f(st.s[0]);
+        if (on) st.s[0] = d != d ? 0 : d >= 9223372036854775807.0 ? INT64_MAX : d <= -9223372036854775808.0 ? INT64_MIN : int64_t(d);
+        break;
+      }
+      default: {
+        const int64_t y = st.s[0], x = st.s[1];
+        int64_t z = 0;
+        bool bad = false;
+        switch (op) {
+          case BC_ADD_I32: z = bc_sx32(x + y); break;
+          case BC_SUB_I32: z = bc_sx32(x - y); break;
+          case BC_MUL_I32: z = bc_sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
+          case BC_DIV_I32: if (y == 0) bad = true; else z = (x == INT32_MIN && y == -1) ? INT32_MIN : x / y; break;
+          case BC_REM_I32: if (y == 0) bad = true; else z = y == -1 ? 0 : x % y; break;
+          case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
+          case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
+          case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
+          case BC_DIV_I64: if (y == 0) bad = true; else z = (x == INT64_MIN && y == -1) ? INT64_MIN : x / y; break;
+          case BC_REM_I64: if (y == 0) bad = true; else z = y == -1 ? 0 : x % y; break;
+          case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;
+          case BC_SUB_F64: z = bc_b(bc_f(x) - bc_f(y)); break;
+          case BC_MUL_F64: z = bc_b(bc_f(x) * bc_f(y)); break;
+          case BC_DIV_F64: z = bc_b(bc_f(x) / bc_f(y)); break;
+          case BC_REM_F64: z = bc_b(fmod(bc_f(x), bc_f(y))); break;
+          case BC_EQ_I: z = x == y; break;
+          case BC_NE_I: z = x != y; break;
+          case BC_LT_I: z = x < y; break;
+          case BC_LE_I: z = x <= y; break;
+          case BC_GT_I: z = x > y; break;
+          case BC_GE_I: z = x >= y; break;
+          case BC_EQ_F: z = bc_f(x) == bc_f(y); break;
+          case BC_NE_F: z = bc_f(x) != bc_f(y); break;
+          case BC_LT_F: z = bc_f(x) < bc_f(y); break;
+          case BC_LE_F: z = bc_f(x) <= bc_f(y); break;
+          case BC_GT_F: z = bc_f(x) > bc_f(y); break;
+          case BC_GE_F: z = bc_f(x) >= bc_f(y); break;
+          case BC_EQ_B: z = (x != 0) == (y != 0); break;
+          case BC_NE_B: z = (x != 0) != (y != 0); break;
+          default: if (on) { env.fail(CEP_E_BAD_IR); ok = false; } break;
+        }
+        if (on && bad) { env.fail(CEP_E_ARITHMETIC); ok = false; }
+        else if (on) { st.pop(); st.s[0] = z; }
+      }
+    }
+  }
+}
+
+}  // namespace kcep

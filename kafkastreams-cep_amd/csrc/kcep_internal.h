@@ -134,6 +134,9 @@ constexpr int NFA_MAX_STATES = 16;
 constexpr int NFA_MAX_SLOTS = 64;
 constexpr int NFA_MAX_CODE = 4096;
 constexpr int NFA_MAX_SL = 64;     // event-only edge predicates evaluated once per record
+constexpr int NFA_STACK = 8;       // operand stack of the device interpreter (registers)
+constexpr int NFA_MAX_FRAMES = 16; // NFA.evaluate recursion depth of the device kernel
+constexpr int RUNS_MAX_STATES = 8; // aggregate registers of one deterministic run
 
 struct DevStage {
   int32_t name, type, slot, nedges, nfolds;
@@ -166,6 +169,8 @@ struct Program {
   DevProgram dev{};
   bool stencil_ok = false;
   std::string stencil_why;           // reason the stencil path does not apply
+  bool runs_ok = false;              // deterministic strict runs (compile.cpp analyse_runs)
+  std::string runs_why;
   StencilProgram stencil{};
 };
 
@@ -244,6 +249,24 @@ struct NfaArgs {
   int32_t* res_err;
   int64_t* res_err_rec;
   int32_t* flags;                 // [0] pool overflow lanes, [1] carry-pool overflow lanes, [2] bad key ids
+};
+
+// deterministic-runs path (runs.hip)
+struct RunsArgs {
+  const DevProgram* P;
+  const int32_t* key;
+  const int32_t* topic;
+  const int32_t* partition;
+  const int64_t* offset;
+  const int64_t* ts;
+  const void* cols[16];
+  int64_t n;
+  int64_t base;
+  unsigned long long* nmatch;     // match counter (append position)
+  unsigned long long* match_key;  // appended (end << 31 | start), sorted afterwards
+  int64_t match_cap;
+  unsigned long long* err_min;    // min over failing runs of (record << 31 | start)
+  int32_t* err_code;              // per start record (valid where it failed)
 };
 
 // compile.cpp

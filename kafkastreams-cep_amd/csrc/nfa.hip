@@ -41,14 +41,14 @@
 
 #include "../../include/kcep.h"
 #include "kcep_internal.h"
+#include "interp.h"
 
 namespace kcep {
 
 namespace {
 
 constexpr int32_t EPS_NONE = 0xFF;
-constexpr int MAXD = NFA_MAX_STAGES + 2;
-constexpr int STK = 32;
+constexpr int MAXD = NFA_MAX_FRAMES;          // PROCEED/SKIP_PROCEED recursion depth (checked by the compiler)
 constexpr int NW = 4;                      // node words: refs, first pred, last pred, flags
 constexpr int32_t NF_EXISTS = 1, NF_MARK = 2, NF_NEED = 4;
 constexpr int PW = 6;                      // pred words: version, prev slot, prev event, next, |version|, version[0]
@@ -97,13 +97,13 @@ struct Lane {
 };
 
 // ---- pool ----
-__device__ int32_t* pool_alloc(Lane& l, int64_t words) {
+__device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words) {
   const unsigned long long at = atomicAdd(l.A->pool_top, (unsigned long long)words);
   if (at + (unsigned long long)words > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
   return l.A->pool + at;
 }
 // re-allocate `*a` (cap words used up to `used`) at >= need words
-__device__ bool regrow(Lane& l, int32_t*& a, int32_t& cap, int64_t used, int64_t need, int32_t fill = 0, bool zero = false) {
+__device__ __forceinline__ bool regrow(Lane& l, int32_t*& a, int32_t& cap, int64_t used, int64_t need, int32_t fill = 0, bool zero = false) {
   int64_t nc = int64_t(cap) * 2;
   if (nc < need) nc = need;
   if (nc > (int64_t(1) << 30)) { l.overflow = 1; return false; }
@@ -139,7 +139,7 @@ __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
   l.heap_top += words;
   return at;
 }
-__device__ int dw_add_stage(Lane& l, int v) {             // DeweyVersion.addStage :95-97
+__device__ __forceinline__ int dw_add_stage(Lane& l, int v) {             // DeweyVersion.addStage :95-97
   const int len = l.heap[v];
   const int n = heap_alloc(l, len + 2);
   if (n < 0) return -1;
@@ -148,7 +148,7 @@ __device__ int dw_add_stage(Lane& l, int v) {             // DeweyVersion.addSta
   l.heap[n + 1 + len] = 0;
   return n;
 }
-__device__ int dw_add_run(Lane& l, int v, int off) {      // DeweyVersion.addRun :62-67
+__device__ __forceinline__ int dw_add_run(Lane& l, int v, int off) {      // DeweyVersion.addRun :62-67
   const int len = l.heap[v];
   const int idx = len - off;
   if (idx < 0 || idx >= len) { l.err = CEP_E_INDEX; return -1; }
@@ -160,7 +160,7 @@ __device__ int dw_add_run(Lane& l, int v, int off) {      // DeweyVersion.addRun
   return n;
 }
 // a.isCompatible(b) (:73-93), with b's length and first digit known up front
-__device__ bool dw_compatible(const Lane& l, int a, int b, int lb, int b0) {
+__device__ __forceinline__ bool dw_compatible(const Lane& l, int a, int b, int lb, int b0) {
   const int la = l.heap[a];
   if (la < lb) return false;
   if (la == lb && la == 1) return l.heap[a + 1] >= b0;
@@ -182,7 +182,7 @@ __device__ __forceinline__ int32_t* node(Lane& l, int slot, int ev) {
 __device__ __forceinline__ int slot_of(const Lane& l, int sid) { return stg(l, sid).slot; }
 __device__ __forceinline__ bool exists(const int32_t* nd) { return nd[3] & NF_EXISTS; }
 
-__device__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslot, int pev) {   // MatchedEvent.addPredecessor
+__device__ __forceinline__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslot, int pev) {   // MatchedEvent.addPredecessor
   const int p = heap_alloc(l, PW);
   if (p < 0) return false;
   l.heap[p] = ver; l.heap[p + 1] = pslot; l.heap[p + 2] = pev; l.heap[p + 3] = -1;
@@ -193,7 +193,7 @@ __device__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslot, int pev) {   
   return true;
 }
 // put 5-arg (SharedVersionedBufferStoreImpl.java:101-126)
-__device__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_sid, int pev, int ver) {
+__device__ __forceinline__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_sid, int pev, int ver) {
   if (pev < 0) { l.err = CEP_E_NPE; return; }
   const int ps = slot_of(l, prev_sid);
   if (!exists(node(l, ps, pev))) { l.err = CEP_E_ILLEGAL_STATE; return; }
@@ -202,12 +202,12 @@ __device__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_sid, int pev, in
   add_pred(l, c, ver, ps, pev);
 }
 // put 3-arg (:149-157): a fresh node overwrites
-__device__ void buf_put3(Lane& l, int cur_sid, int ev, int ver) {
+__device__ __forceinline__ void buf_put3(Lane& l, int cur_sid, int ev, int ver) {
   int32_t* c = node(l, slot_of(l, cur_sid), ev);
   c[0] = 1; c[1] = -1; c[2] = -1; c[3] = NF_EXISTS;
   add_pred(l, c, ver, -1, 0);
 }
-__device__ int first_compatible(const Lane& l, const int32_t* nd, int ver, int* prevp) {   // getPointerByVersion
+__device__ __forceinline__ int first_compatible(const Lane& l, const int32_t* nd, int ver, int* prevp) {   // getPointerByVersion
   int pp = -1;
   for (int p = nd[1]; p >= 0; p = l.heap[p + 3]) {
     if (dw_compatible(l, ver, l.heap[p], l.heap[p + 4], l.heap[p + 5])) { if (prevp) *prevp = pp; return p; }
@@ -216,7 +216,7 @@ __device__ int first_compatible(const Lane& l, const int32_t* nd, int ver, int* 
   return -1;
 }
 // branch (:132-142)
-__device__ void buf_branch(Lane& l, int sid, int ev, int ver) {
+__device__ __forceinline__ void buf_branch(Lane& l, int sid, int ev, int ver) {
   if (ev < 0) { l.err = CEP_E_NPE; return; }
   int slot = slot_of(l, sid), e = ev, pv = ver;
   for (;;) {
@@ -229,7 +229,7 @@ __device__ void buf_branch(Lane& l, int sid, int ev, int ver) {
   }
 }
 // peek (:176-201).  emit: traversal (slot, event) pairs into dst; returns the count or -1.
-__device__ int buf_peek(Lane& l, int sid, int ev, int ver, bool remove, int32_t* dst, int dst_cap) {
+__device__ __forceinline__ int buf_peek(Lane& l, int sid, int ev, int ver, bool remove, int32_t* dst, int dst_cap) {
   if (ev < 0) { l.err = CEP_E_NPE; return -1; }
   int slot = slot_of(l, sid), e = ev, pv = ver, cnt = 0;
   for (;;) {
@@ -260,7 +260,7 @@ __device__ int buf_peek(Lane& l, int sid, int ev, int ver, bool remove, int32_t*
 }
 
 // ---- aggregates: row per run sequence ----
-__device__ int32_t* agg(Lane& l, int state, int seq) {
+__device__ __forceinline__ int32_t* agg(Lane& l, int state, int seq) {
   const int ns = l.P->nstates;
   if (seq < 0) { l.overflow = 1; return nullptr; }
   if (seq >= l.seqcap) {
@@ -300,10 +300,9 @@ __device__ __forceinline__ int64_t ev_field(const Lane& l, int col, int t, int e
 
 __device__ __forceinline__ double as_f(int64_t b) { return __builtin_bit_cast(double, b); }
 __device__ __forceinline__ int64_t as_b(double d) { return __builtin_bit_cast(int64_t, d); }
-__device__ __forceinline__ int64_t sx32(int64_t x) { return int64_t(int32_t(uint32_t(uint64_t(x)))); }
 
 // Event.compareTo (Event.java:118-122) == 0, for TreeSet de-duplication
-__device__ bool ev_same(const Lane& l, int a, int b) {
+__device__ __forceinline__ bool ev_same(const Lane& l, int a, int b) {
   if (ev_topic(l, a) != ev_topic(l, b) || ev_part(l, a) != ev_part(l, b)) return ev_ts(l, a) == ev_ts(l, b);
   return ev_off(l, a) == ev_off(l, b);
 }
@@ -317,7 +316,7 @@ struct Ctx {
 
 // SequenceMatcher: average of a column over buffer.get(Matched(prev, prevEvent), version)
 // (SequenceMatcher.java:21-26), with Sequence's per-stage TreeSet de-duplication.
-__device__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t& out) {
+__device__ __forceinline__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t& out) {
   if (c.prev_sid < 0 || c.pev < 0) { l.err = CEP_E_NPE; return false; }
   const int need = 2 * l.nev + 2;
   if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need))
@@ -343,126 +342,42 @@ __device__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t& out) {
   return true;
 }
 
-// bytecode interpreter over the current record; returns false on error (l.err / l.overflow set)
-__device__ bool run_code(Lane& l, int pc, const Ctx& c, int64_t& result) {
-  const int32_t* code = l.P->code;
-  int64_t st[STK];
-  int sp = 0;
-  const int64_t g = l.g;
-  for (;;) {
-    const int32_t w = code[pc++];
-    const int op = w & 0xFF, a = (w >> 8) & 0xFF, b = (w >> 16) & 0xFF;
-    if (sp >= STK - 1) { l.overflow = 1; return false; }
-    switch (op) {
-      case BC_END: result = st[sp - 1]; return true;
-      case BC_PUSH: st[sp++] = int64_t(uint32_t(code[pc])) | (int64_t(code[pc + 1]) << 32); pc += 2; break;
-      case BC_FIELD: st[sp++] = b_field(l, a, b, g); break;
-      case BC_EV_KEY: st[sp++] = l.A->key[g]; break;
-      case BC_EV_TS: st[sp++] = b_ts(l, g); break;
-      case BC_EV_OFFSET: st[sp++] = b_off(l, g); break;
-      case BC_EV_PARTITION: st[sp++] = b_part(l, g); break;
-      case BC_TOPIC_EQ: st[sp++] = b_topic(l, g) == code[pc] ? 1 : 0; pc++; break;
-      case BC_STATE_GET: case BC_STATE_GET_OR_ELSE: {          // States.get / getOrElse (States.java:56-78)
-        const int32_t* e = agg(l, a, c.seq);
-        if (!e) return false;
-        if (e[0] == 0) {
-          if (op == BC_STATE_GET) { l.err = CEP_E_UNKNOWN_AGGREGATE; return false; }
-          pc++;                                                  // evaluate the default
-          break;
-        }
-        if (e[0] != b) { l.err = CEP_E_CLASS_CAST; return false; }
-        st[sp++] = int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32);
-        if (op == BC_STATE_GET_OR_ELSE) pc += 1 + code[pc];
-        break;
-      }
-      case BC_FOLD_CURR:
-        if (!c.in_fold || c.curr_tag == 0) { l.err = CEP_E_NPE; return false; }
-        if (c.curr_tag != b) { l.err = CEP_E_CLASS_CAST; return false; }
-        st[sp++] = c.curr;
-        break;
-      case BC_SEQ_AVG: {
-        int64_t v;
-        if (!seq_avg(l, c, a, v)) return false;
-        st[sp++] = v;
-        break;
-      }
-      case BC_NOT: st[sp - 1] = st[sp - 1] ? 0 : 1; break;
-      case BC_JZ_KEEP: if (st[sp - 1] == 0) pc += 1 + code[pc]; else { sp--; pc++; } break;
-      case BC_JNZ_KEEP: if (st[sp - 1] != 0) pc += 1 + code[pc]; else { sp--; pc++; } break;
-      case BC_POP: sp--; break;
-      case BC_NEG_I32: st[sp - 1] = sx32(0 - st[sp - 1]); break;
-      case BC_NEG_I64: st[sp - 1] = int64_t(0ull - uint64_t(st[sp - 1])); break;
-      case BC_NEG_F64: st[sp - 1] = as_b(-as_f(st[sp - 1])); break;
-      case BC_I64_TO_I32: st[sp - 1] = sx32(st[sp - 1]); break;
-      case BC_I_TO_F64: st[sp - 1] = as_b(double(st[sp - 1])); break;
-      case BC_F64_TO_I32: {
-        const double d = as_f(st[sp - 1]);
-        st[sp - 1] = d != d ? 0 : d >= 2147483647.0 ? INT32_MAX : d <= -2147483648.0 ? INT32_MIN : int64_t(int32_t(d));
-        break;
-      }
-      case BC_F64_TO_I64: {
-        const double d = as_f(st[sp - 1]);
-        st[sp - 1] = d != d ? 0 : d >= 9223372036854775807.0 ? INT64_MAX : d <= -9223372036854775808.0 ? INT64_MIN : int64_t(d);
-        break;
-      }
-      default: {
-        const int64_t y = st[--sp], x = st[sp - 1];
-        int64_t z = 0;
-        switch (op) {
-          case BC_ADD_I32: z = sx32(x + y); break;
-          case BC_SUB_I32: z = sx32(x - y); break;
-          case BC_MUL_I32: z = sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
-          case BC_DIV_I32:
-            if (y == 0) { l.err = CEP_E_ARITHMETIC; return false; }
-            z = (x == INT32_MIN && y == -1) ? INT32_MIN : x / y;
-            break;
-          case BC_REM_I32:
-            if (y == 0) { l.err = CEP_E_ARITHMETIC; return false; }
-            z = y == -1 ? 0 : x % y;
-            break;
-          case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
-          case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
-          case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
-          case BC_DIV_I64:
-            if (y == 0) { l.err = CEP_E_ARITHMETIC; return false; }
-            z = (x == INT64_MIN && y == -1) ? INT64_MIN : x / y;
-            break;
-          case BC_REM_I64:
-            if (y == 0) { l.err = CEP_E_ARITHMETIC; return false; }
-            z = y == -1 ? 0 : x % y;
-            break;
-          case BC_ADD_F64: z = as_b(as_f(x) + as_f(y)); break;
-          case BC_SUB_F64: z = as_b(as_f(x) - as_f(y)); break;
-          case BC_MUL_F64: z = as_b(as_f(x) * as_f(y)); break;
-          case BC_DIV_F64: z = as_b(as_f(x) / as_f(y)); break;
-          case BC_REM_F64: z = as_b(fmod(as_f(x), as_f(y))); break;
-          case BC_EQ_I: z = x == y; break;
-          case BC_NE_I: z = x != y; break;
-          case BC_LT_I: z = x < y; break;
-          case BC_LE_I: z = x <= y; break;
-          case BC_GT_I: z = x > y; break;
-          case BC_GE_I: z = x >= y; break;
-          case BC_EQ_F: z = as_f(x) == as_f(y); break;
-          case BC_NE_F: z = as_f(x) != as_f(y); break;
-          case BC_LT_F: z = as_f(x) < as_f(y); break;
-          case BC_LE_F: z = as_f(x) <= as_f(y); break;
-          case BC_GT_F: z = as_f(x) > as_f(y); break;
-          case BC_GE_F: z = as_f(x) >= as_f(y); break;
-          case BC_EQ_B: z = (x != 0) == (y != 0); break;
-          case BC_NE_B: z = (x != 0) != (y != 0); break;
-          default: l.err = CEP_E_BAD_IR; return false;
-        }
-        st[sp - 1] = z;
-      }
-    }
+// interpreter environment of the general kernel: the lane's current record,
+// the evaluating run's aggregates and partial sequence
+struct LaneEnv {
+  Lane& l;
+  const Ctx& c;
+  bool in_fold;
+  int32_t curr_tag;
+  int64_t curr;
+  __device__ __forceinline__ int64_t field(int col, int t) { return b_field(l, col, t, l.g); }
+  __device__ __forceinline__ int64_t key() { return l.A->key[l.g]; }
+  __device__ __forceinline__ int64_t ts() { return b_ts(l, l.g); }
+  __device__ __forceinline__ int64_t off() { return b_off(l, l.g); }
+  __device__ __forceinline__ int64_t part() { return b_part(l, l.g); }
+  __device__ __forceinline__ int32_t topic() { return b_topic(l, l.g); }
+  __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) {
+    const int32_t* e = agg(l, idx, c.seq);
+    if (!e) return false;
+    tag = e[0];
+    v = int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32);
+    return true;
   }
+  __device__ __forceinline__ bool seq_avg(int col, int64_t& v) { return kcep::seq_avg(l, c, col, v); }
+  __device__ __forceinline__ void fail(int code) { l.err = code; }
+};
+
+// bytecode interpreter over the current record; returns false on error (l.err / l.overflow set)
+__device__ __forceinline__ bool run_code(Lane& l, int pc, const Ctx& c, int64_t& result) {
+  LaneEnv env{l, c, c.in_fold, c.curr_tag, c.curr};
+  return interp(l.P->code, pc, env, result);
 }
 
 // event-only edge predicates of the current record, once for every run: all
 // lanes walk the same programs in the same order.  A predicate that throws is
 // left to per-run evaluation so the exception surfaces exactly where the
 // reference evaluates it (NFA.java:371-384).
-__device__ void eval_event_only(Lane& l) {
+__device__ __forceinline__ void eval_event_only(Lane& l) {
   l.slm = 0;
   l.sle = 0;
   const int nsl = l.P->nsl;
@@ -502,10 +417,10 @@ struct Frame {
 };
 
 // frame entry: matchEdgesAndGet (NFA.java:371-384) + isBranching (:392-397)
-__device__ bool frame_enter(Lane& l, Frame& f) {
+__device__ __forceinline__ bool frame_enter(Lane& l, Frame& f) {
   f.nm = 0; f.i = 0; f.pending = 0; f.consumed = 0; f.proceed = 0;
   f.nbase = l.tlen;
-  int has[5] = {0, 0, 0, 0, 0};
+  uint32_t has = 0;
   const bool eps = f.cur_eps != EPS_NONE;
   const DevStage& s = stg(l, f.cur_sid);
   const int ne = eps ? 1 : s.nedges;
@@ -524,16 +439,17 @@ __device__ bool frame_enter(Lane& l, Frame& f) {
         ok = v != 0;
       }
     }
-    if (ok) { f.medge[f.nm++] = int8_t(e); has[op] = 1; }
+    if (ok) { f.medge[f.nm++] = int8_t(e); has |= 1u << op; }
   }
-  f.branching = (has[E_PROCEED] && has[E_TAKE]) || (has[E_IGNORE] && has[E_TAKE]) || (has[E_IGNORE] && has[E_BEGIN]) ||
-                (has[E_IGNORE] && has[E_PROCEED]);
-  f.ignored = has[E_IGNORE];
+  auto H = [&](int o) { return (has >> o) & 1u; };
+  f.branching = (H(E_PROCEED) && H(E_TAKE)) || (H(E_IGNORE) && H(E_TAKE)) || (H(E_IGNORE) && H(E_BEGIN)) ||
+                (H(E_IGNORE) && H(E_PROCEED));
+  f.ignored = H(E_IGNORE);
   return true;
 }
 
 // NFA.evaluate (NFA.java:190-341) for one run; results appended to tq
-__device__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
+__device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
   int d = 0;
   fr[0].cs = run;
   fr[0].cur_sid = int16_t(r_sid(run));
@@ -651,7 +567,7 @@ __device__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
 
 // room for the longest buffer walk: it visits strictly earlier events, so at
 // most one node per event of the key
-__device__ bool reserve_walk(Lane& l) {
+__device__ __forceinline__ bool reserve_walk(Lane& l) {
   const int need_out = 3 + 3 * l.nev;
   if (l.out_top + need_out > l.outcap &&
       !regrow(l, l.out, l.outcap, l.out_top, int64_t(l.out_top) + need_out))
@@ -665,7 +581,7 @@ __device__ bool reserve_walk(Lane& l) {
 
 // matchConstruction of one final run: remove + Sequence entries (:151-158);
 // the walk's (slot, event) pairs go to scratch at the heap top first
-__device__ bool emit_match(Lane& l, const Run& y) {
+__device__ __forceinline__ bool emit_match(Lane& l, const Run& y) {
   if (!reserve_walk(l)) return false;
   int32_t* tmp = l.heap + l.heap_top;
   const int cnt = buf_peek(l, r_sid(y), y.ev, y.ver, true, tmp, l.nev + 1);
@@ -687,7 +603,7 @@ __device__ bool emit_match(Lane& l, const Run& y) {
 }
 
 // NFA.matchPattern(Event) (NFA.java:134-149) for local event r
-__device__ bool step(Lane& l, Frame* fr) {
+__device__ __forceinline__ bool step(Lane& l, Frame* fr) {
   const int n = l.qlen;
   int qn = 0;
   l.flen = 0;
@@ -732,7 +648,7 @@ __device__ __forceinline__ int hwm_find(const Lane& l, int32_t tp) {
   return h;
 }
 
-__device__ bool import_state(Lane& l, const int32_t* b) {
+__device__ __forceinline__ bool import_state(Lane& l, const int32_t* b) {
   const DevProgram* P = l.P;
   l.nhwm = b[CB_NHWM];
   const int qlen = b[CB_QLEN], nnode = b[CB_NNODE], npred = b[CB_NPRED], nver = b[CB_NVER], nseq = b[CB_NSEQ];
@@ -790,13 +706,13 @@ __device__ bool import_state(Lane& l, const int32_t* b) {
   return true;
 }
 
-__device__ void copy_version(const Lane& l, int v, int32_t* dst) {
+__device__ __forceinline__ void copy_version(const Lane& l, int v, int32_t* dst) {
   const int len = l.heap[v];
   for (int i = 0; i <= len; i++) dst[i] = l.heap[v + i];
 }
 
 // Compacts the key's state into a blob in the carry pool; returns its offset or -1.
-__device__ int64_t export_state(Lane& l) {
+__device__ __forceinline__ int64_t export_state(Lane& l) {
   const DevProgram* P = l.P;
   const int ns = P->nslots;
   // (1) nodes the queue can reach: roots are the runs' (stage, last event) nodes;
@@ -945,7 +861,7 @@ __device__ int64_t export_state(Lane& l) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void nfa_kernel(NfaArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nfa_kernel(NfaArgs A) {
   const int seg = blockIdx.x * blockDim.x + threadIdx.x;
   if (seg >= A.nseg) return;
   const DevProgram* P = A.P;

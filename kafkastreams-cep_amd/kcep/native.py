@@ -22,7 +22,7 @@ ERRORS = {
     12: "Unsupported",
 }
 MODE_NFA, MODE_PROCESSOR = 0, 1
-PATH_STENCIL, PATH_GENERAL, PATH_CHAIN = 1, 2, 3
+PATH_STENCIL, PATH_GENERAL, PATH_CHAIN, PATH_RUNS = 1, 2, 3, 4
 MEM_HOST, MEM_DEVICE = 0, 1
 BATCH_OFFSETS_MONOTONE = 1
 SESSION_CARRY = 1
@@ -38,7 +38,7 @@ class CepError(RuntimeError):
 class PatternInfo(C.Structure):
     _fields_ = [("n_stages", C.c_int32), ("n_names", C.c_int32), ("n_patterns", C.c_int32),
                 ("n_cols", C.c_int32), ("stencil_ok", C.c_int32), ("stencil_k", C.c_int32),
-                ("chain_ok", C.c_int32)]
+                ("chain_ok", C.c_int32), ("runs_ok", C.c_int32)]
 
 
 class Opts(C.Structure):

@@ -96,3 +96,18 @@ def test_null_strategy_is_npe():
     with pytest.raises(O.OracleError) as eo:
         O.OraclePattern(p.to_ir(sch))
     assert eo.value.code == 4
+
+
+def test_runs_eligibility():
+    """Deterministic strict patterns take the runs path (compile.cpp analyse_runs): C3's
+    oneOrMore predicate and its successor's are complementary comparisons."""
+    sch = Schema([("value", "i32")])
+    assert N.CompiledPattern(synth.c3_pattern().to_ir(sch)).info.runs_ok == 1
+    assert N.CompiledPattern(synth.c4_pattern().to_ir(sch)).info.runs_ok == 0     # skip-till-any
+    v = Event.value()
+    overlapping = (QueryBuilder().select("a").where(v == 0).then().select("b").oneOrMore().where(v >= 1)
+                   .then().select("c").where(v <= 2).build())                      # TAKE and PROCEED can both match
+    assert N.CompiledPattern(overlapping.to_ir(sch)).info.runs_ok == 0
+    runs = {f["name"] for f in scenarios() if N.CompiledPattern(bytes.fromhex(f["ir"])).info.runs_ok}
+    assert {"nfa_stateful_condition", "nfa_one_or_more", "nfa_times3", "nfa_strict3"} <= runs
+    assert not runs & {"nfa_sequence_condition", "nfa_zero_or_more", "nfa_any_any", "stock_demo"}
