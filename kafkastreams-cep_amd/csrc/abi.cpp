@@ -24,7 +24,7 @@
 #include "kcep_internal.h"
 
 namespace kcep {
-hipError_t stencil_launch(const StencilLaunch& L, hipStream_t st);
+hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
 int64_t stencil_tiles(int64_t n);
 hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t nm, int32_t* mkey,
                         const StencilProgram* P, unsigned long long* sum, hipStream_t st);
@@ -121,9 +121,8 @@ struct cep_session {
   bool pending = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, eb0 = nullptr, eb1 = nullptr;
   // ---- stencil workspace ----
-  DBuf prog, out, status, counter, total, sum, mkey;
+  DBuf prog, out, status, counter, total, sum, mkey, slots;   // status: tile counts + prefixes; counter: scan scratch
   int64_t out_cap = 0;
-  uint32_t epoch = 0;
   const int32_t* d_key = nullptr;
   // ---- staging of host-resident batches ----
   DBuf h_key, h_valid, h_topic, h_part, h_off, h_ts;
@@ -176,15 +175,12 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   if ((reinterpret_cast<uintptr_t>(key) | reinterpret_cast<uintptr_t>(col) | reinterpret_cast<uintptr_t>(topic)) & 15)
     return fail(CEP_E_ARG, "device columns must be 16-byte aligned");
   s->d_key = key;
-  // epoch tags the look-back granules of this launch; reset the status words when it wraps
-  s->epoch = (s->epoch % 0xFFFFu) + 1;
-  if (s->epoch == 1) HIPCHECK(hipMemsetAsync(s->status.p, 0, s->status.cap, st));
+  int64_t* tc = s->status.as<int64_t>();
+  const int64_t ntiles = stencil_tiles(b->n);
   StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic, SP.chain,
-                  s->out.as<int32_t>(), s->out_cap, s->status.as<uint64_t>(), s->counter.as<uint32_t>(),
-                  s->total.as<int64_t>(), s->epoch};
-  HIPCHECK(hipEventRecord(s->ev0, st));
-  HIPCHECK(stencil_launch(L, st));
-  HIPCHECK(hipEventRecord(s->ev1, st));
+                  s->slots.as<int32_t>(), tc, tc + ntiles + 1, s->counter.as<int64_t>(), s->out.as<int32_t>(),
+                  s->out_cap, s->total.as<int64_t>()};
+  HIPCHECK(stencil_launch(L, s->ev0, s->ev1, st));
   HIPCHECK(hipEventRecord(s->eb1, st));
   return CEP_OK;
 }
@@ -580,9 +576,11 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   if (s->scal.ensure(64) || hipMemset(s->scal.p, 0, 64)) return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   if (P.stencil_ok && path != CEP_PATH_GENERAL) {
     const int k = P.stencil.k;
-    if (s->prog.ensure(sizeof(StencilProgram)) || s->status.ensure(sizeof(uint64_t) * (stencil_tiles(cap) + 1)) ||
-        s->counter.ensure(64) || s->total.ensure(64) || s->sum.ensure(64) ||
-        s->out.ensure(sizeof(int32_t) * size_t(k) * size_t(cap)))
+    const int64_t nt = stencil_tiles(cap);
+    if (s->prog.ensure(sizeof(StencilProgram)) || s->status.ensure(sizeof(int64_t) * size_t(2 * nt + 2)) ||
+        s->counter.ensure(sizeof(int64_t) * size_t(nt / 1024 + 4)) || s->total.ensure(64) || s->sum.ensure(64) ||
+        s->out.ensure(sizeof(int32_t) * size_t(k) * size_t(cap)) ||
+        s->slots.ensure(sizeof(int32_t) * size_t(k) * size_t(nt) * 4096))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
     s->out_cap = cap;
     if (hipMemcpy(s->prog.p, &P.stencil, sizeof(StencilProgram), hipMemcpyHostToDevice) ||
@@ -610,7 +608,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 
 void cep_session_close(cep_session* s) {
   if (!s) return;
-  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->h_key, &s->h_valid,
+  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->h_key, &s->h_valid,
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,

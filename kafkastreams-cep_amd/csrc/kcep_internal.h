@@ -182,12 +182,13 @@ struct StencilLaunch {
   int64_t n;
   const StencilProgram* prog_dev;
   int k, coltype, use_topic, chain;
-  int32_t* out;
-  int64_t out_cap;
-  uint64_t* status;
-  uint32_t* counter;
-  int64_t* total;
-  uint32_t epoch;
+  int32_t* slots;                 // per-tile match slots, ST_TILE * k ints each
+  int64_t* tile_count;            // matches per tile
+  int64_t* tile_pre;              // their exclusive prefix
+  int64_t* scan_tmp;
+  int32_t* out;                   // contiguous output, k ints per match
+  int64_t out_cap;                // matches
+  int64_t* total;                 // device: number of matches
 };
 
 // Per-key workspace of the general NFA kernel.  Every key segment draws its

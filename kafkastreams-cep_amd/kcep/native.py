@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libkcep.so")
+LIB_PATH = os.environ.get("KCEP_LIB") or os.path.join(PKG_ROOT, "libkcep.so")   # KCEP_LIB: experiment builds
 
 CEP_OK = 0
 ERRORS = {
