@@ -1,12 +1,12 @@
 """Summarise one gpu_prof.sh run into profiles/.
 
-usage: python tools/pmc_summary.py TAG KERNEL EVENTS OUT_PREFIX
+usage: python tools/pmc_summary.py TAG_DIR KERNEL EVENTS OUT_PREFIX CONFIG
 
 Reads gpurun_out/prof/TAG/{trace_kernel_stats,pmc_fetch_counter_collection,
 pmc_write_counter_collection}.csv and writes
   profiles/OUT_PREFIX_kernel_stats.csv   (copy of the rocprofv3 --stats summary)
   profiles/OUT_PREFIX_pmc.json           (per-kernel mean FETCH/WRITE bytes per launch)
-  profiles/pmc_traffic.json              (the bench kernel's HBM bytes per launch)
+  profiles/pmc_traffic[_CONFIG].json     (the bench kernel's HBM bytes per launch; no suffix for c2)
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch; FETCH_SIZE is doubled (gfx950
 reports half the bytes of a wide streaming read, MI355X_MICROARCH.md §HBM).
@@ -33,6 +33,7 @@ def per_kernel(path, counter):
 
 def main():
     tag, kernel, events, prefix = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    cfg = sys.argv[5] if len(sys.argv) > 5 else "c2"
     d = os.path.join(ROOT, "gpurun_out", "prof", tag)
     prof = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(d, "trace_kernel_stats.csv"), os.path.join(prof, f"{prefix}_kernel_stats.csv"))
@@ -46,7 +47,7 @@ def main():
     out = {"kernel": kernel, "events": events, "source": f"profiles/{prefix}_pmc.json",
            "fetch_bytes_per_launch": k["fetch_bytes_corrected"], "write_bytes_per_launch": k["write_bytes"],
            "hbm_bytes_per_launch": k["fetch_bytes_corrected"] + k["write_bytes"]}
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+    with open(os.path.join(prof, "pmc_traffic.json" if cfg == "c2" else f"pmc_traffic_{cfg}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
 
