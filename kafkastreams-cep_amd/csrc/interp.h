@@ -23,6 +23,12 @@
 
 namespace kcep {
 
+// read-only program memory addressed wave-uniformly: constant address space,
+// so the compiler emits scalar loads (scalar cache) instead of vector loads
+typedef const int32_t __attribute__((address_space(4))) cint32_t;
+typedef const DevStage __attribute__((address_space(4))) cDevStage;
+typedef const DevProgram __attribute__((address_space(4))) cDevProgram;
+
 __device__ __forceinline__ double bc_f(int64_t b) { return __builtin_bit_cast(double, b); }
 __device__ __forceinline__ int64_t bc_b(double d) { return __builtin_bit_cast(int64_t, d); }
 __device__ __forceinline__ int64_t bc_sx32(int64_t x) { return int64_t(int32_t(uint32_t(uint64_t(x)))); }
@@ -162,8 +168,9 @@ __device__ __forceinline__ bool interp(const int32_t* __restrict__ code, int pc,
 // forward and nested, so a lane resumes exactly at its target instruction.
 // Returns false for a lane that raised (env.fail) -- only active lanes raise.
 template <class Env>
-__device__ __forceinline__ bool interp_ls(const int32_t* __restrict__ code, int pc0, Env& env, bool active,
+__device__ __forceinline__ bool interp_ls(const int32_t* __restrict__ code_flat, int pc0, Env& env, bool active,
                                           int64_t& result) {
+  const cint32_t* code = (const cint32_t*)code_flat;   // pc is wave-uniform: scalar fetches
   BcStack st;
 #pragma unroll
   for (int i = 0; i < NFA_STACK; i++) st.s[i] = 0;

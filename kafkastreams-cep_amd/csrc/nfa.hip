@@ -381,11 +381,12 @@ __device__ __forceinline__ void eval_event_only(Lane& l) {
   l.slm = 0;
   l.sle = 0;
   const int nsl = l.P->nsl;
-  for (int i = 0; i < nsl; i++) {
+  for (int i = 0; i < nsl; i++) {                  // uniform: lock-step interpreter, scalar code fetches
     const Ctx c{0, -1, -1, -1, false, 0, 0};
+    LaneEnv env{l, c, false, 0, 0};
     int64_t v = 0;
     const int e0 = l.err, o0 = l.overflow;
-    if (run_code(l, l.P->sl_pc[i], c, v)) {
+    if (interp_ls(l.P->code, l.P->sl_pc[i], env, true, v)) {
       if (v) l.slm |= 1ull << i;
     } else {
       l.sle |= 1ull << i;

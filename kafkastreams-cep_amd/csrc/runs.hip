@@ -40,6 +40,14 @@ struct RunState {
   int64_t val[RUNS_MAX_STATES];
 };
 
+constexpr int RUNS_COLCACHE = 4;   // columns of the current record held in registers
+
+__device__ __forceinline__ int64_t load_col(const RunsArgs& A, int col, int64_t g) {
+  const void* c = A.cols[col];
+  if (A.P->coltype[col] == T_I32) return static_cast<const int32_t*>(c)[g];
+  return static_cast<const int64_t*>(c)[g];
+}
+
 struct RunEnv {
   const RunsArgs& A;
   int64_t g;
@@ -48,7 +56,15 @@ struct RunEnv {
   bool in_fold;
   int32_t curr_tag;
   int64_t curr;
+  const int64_t* cv;               // the record's first RUNS_COLCACHE columns, loaded once per step
   __device__ __forceinline__ int64_t field(int col, int t) {
+    if (col < RUNS_COLCACHE) {
+      int64_t v = 0;
+#pragma unroll
+      for (int i = 0; i < RUNS_COLCACHE; i++)
+        if (i == col) v = cv[i];
+      return v;
+    }
     const void* c = A.cols[col];
     if (t == T_I32) return static_cast<const int32_t*>(c)[g];
     return static_cast<const int64_t*>(c)[g];
@@ -96,7 +112,7 @@ struct RunResult {
 template <class Item, class Done, class Consume>
 __device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_t i1, Item&& item, Done&& done,
                                            Consume&& on_consume) {
-  const DevProgram* P = A.P;
+  const cDevProgram* P = (const cDevProgram*)A.P;       // stage ids are wave-uniform: scalar reads
   RunState rs;
 #pragma unroll
   for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
@@ -107,6 +123,17 @@ __device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_
   int32_t k = 0;
   int64_t next = i0;                                          // wave-uniform: next unassigned item
   const int nst = P->nstages;
+  const int ncc = A.P->ncols < RUNS_COLCACHE ? A.P->ncols : RUNS_COLCACHE;
+  int64_t cv[RUNS_COLCACHE];
+#pragma unroll
+  for (int q = 0; q < RUNS_COLCACHE; q++) cv[q] = 0;
+  // the record's key and cached columns, issued together (one memory latency per step)
+  auto load_record = [&](int64_t g, int32_t* kk) {
+    *kk = A.key[g];
+#pragma unroll
+    for (int q = 0; q < RUNS_COLCACHE; q++)
+      if (q < ncc) cv[q] = load_col(A, q, g);
+  };
   for (;;) {
     // refill idle lanes from the chunk, in lane order
     const uint64_t idle = __builtin_amdgcn_ballot_w64(!alive);
@@ -121,7 +148,7 @@ __device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_
           r = j;
           ps = P->begin;                                      // the begin run's evaluation on record j
           cur = -1;
-          k = A.key[j];
+          load_record(j, &k);
           res = RunResult{-1, -1, 0};
 #pragma unroll
           for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
@@ -136,15 +163,15 @@ __device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_
     for (int s = nst - 1; s >= 1; s--) {
       const bool here = alive && ps == s;
       if (!wave_any(here)) continue;
-      const DevStage& st = P->st[s];
+      const cDevStage& st = P->st[s];
       uint32_t matched = 0;
       bool ok = true;
       for (int e = 0; e < st.nedges; e++) {
         if (st.pred[e] < 0) { matched |= 1u << e; continue; }
-        RunEnv env{A, r, rs, 0, false, 0, 0};
+        RunEnv env{A, r, rs, 0, false, 0, 0, cv};
         int64_t v;
         const bool act = here && ok;
-        if (!interp_ls(P->code, st.pred[e], env, act, v)) {
+        if (!interp_ls(A.P->code, st.pred[e], env, act, v)) {
           if (act) { ok = false; res.err = env.err; }
         } else if (act && v) {
           matched |= 1u << e;
@@ -162,14 +189,14 @@ __device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_
         if (!wave_any(consume && ok)) break;
         const int sidx = st.fold_state[f];
         int32_t ct = 0;
-        int64_t cv = 0;
+        int64_t cvv = 0;
 #pragma unroll
         for (int q = 0; q < RUNS_MAX_STATES; q++)
-          if (q == sidx) { ct = rs.tag[q]; cv = rs.val[q]; }
-        RunEnv env{A, r, rs, 0, true, ct, cv};
+          if (q == sidx) { ct = rs.tag[q]; cvv = rs.val[q]; }
+        RunEnv env{A, r, rs, 0, true, ct, cvv, cv};
         int64_t v;
         const bool act = consume && ok;
-        if (!interp_ls(P->code, st.fold_code[f], env, act, v)) {
+        if (!interp_ls(A.P->code, st.fold_code[f], env, act, v)) {
           if (act) { ok = false; res.err = env.err; }
         } else if (act) {
           const int32_t ft = st.fold_type[f];
@@ -197,8 +224,9 @@ __device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_
     if (alive) {
       if (ps == -1) {                                              // consumed: on to the next record
         r++;
-        if (r < A.n && r <= stop && A.key[r] == k) ps = cur;
-        else ps = -2;
+        int32_t kr = k + 1;
+        if (r < A.n && r <= stop) load_record(r, &kr);
+        ps = kr == k ? cur : -2;
       } else if (ps != -2) {
         ps = -2;                                                   // (a recursion that consumed nothing)
       }
@@ -248,7 +276,7 @@ struct WriteArgs {
 };
 
 __device__ __forceinline__ void put_entry(const WriteArgs& W, int64_t at, int stage, int64_t r) {
-  W.ent_name[at] = W.R.P->st[stage].name;
+  W.ent_name[at] = ((const cDevProgram*)W.R.P)->st[stage].name;
   W.ent_record[at] = W.R.base + r;
 }
 
