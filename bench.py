@@ -173,10 +173,12 @@ def main():
             "config": {"workload": C["desc"], "events_per_gpu": n, "keys_per_gpu": K,
                        "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
                        "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain", N.PATH_RUNS: "runs"}.get(sess.path, "general"),
-                       "parallelism": f"key-sharded x{world}"},
+                       "parallelism": f"key-sharded x{world}",
+                       "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
-                         "kernel": {N.PATH_GENERAL: "nfa_kernel", N.PATH_RUNS: "runs_sim"}.get(sess.path, "stencil_kernel"),
+                         "kernel": {N.PATH_GENERAL: "nfa_kernel",
+                                    N.PATH_RUNS: "kcep_runs_sim" if sess.jit else "runs_sim"}.get(sess.path, "stencil_kernel"),
                          "kernel_ms": avg_kernel_ms, "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",

@@ -20,7 +20,9 @@
  */
 #ifndef KCEP_H
 #define KCEP_H
+#ifndef __HIPCC_RTC__   /* per-pattern kernels (jit.cpp) include this header through hiprtc */
 #include <stddef.h>
+#endif
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -92,6 +94,10 @@ typedef struct {
                                 (records pushed before the batch + index in the batch).  Runs on the general
                                 path. */
 
+#define CEP_SESSION_INTERPRET 2  /* runs path: use the built-in kernels, which interpret the pattern's predicates
+                                    and folds, instead of kernels compiled for the pattern at cep_session_open
+                                    (hiprtc; also disabled by the environment variable KCEP_JIT=0) */
+
 #define CEP_MEM_HOST 0
 #define CEP_MEM_DEVICE 1
 
@@ -160,6 +166,13 @@ int32_t cep_pattern_stage(const cep_pattern* p, int32_t sid, int32_t* name_id, i
 int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** out);
 void cep_session_close(cep_session* s);
 int cep_session_path(const cep_session* s);
+/* 1 if the session runs kernels compiled for its pattern (see CEP_SESSION_INTERPRET), else 0 */
+int cep_session_jit(const cep_session* s);
+/* The HIP source of the pattern's compiled kernels for a path (CEP_PATH_RUNS), NUL-terminated;
+   with buf == NULL only *needed is set.  CEP_E_UNSUPPORTED if the path has none for this pattern. */
+int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t cap, size_t* needed);
+/* Generate and compile (gfx950 code object, no device needed) the pattern's kernels for a path. */
+int cep_pattern_build_kernels(const cep_pattern* p, int path);
 
 /* --- batch evaluation: replaces NFA.matchPattern per record (NFA.java:134-149) ---
  * Enqueues the match phase on `stream` (a hipStream_t, NULL = default stream)

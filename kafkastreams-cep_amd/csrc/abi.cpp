@@ -22,6 +22,7 @@
 
 #include "../../include/kcep.h"
 #include "kcep_internal.h"
+#include "jit.h"
 
 namespace kcep {
 hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
@@ -43,7 +44,7 @@ hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* 
                                const int32_t* res_err, int64_t* ctab, hipStream_t st);
 hipError_t carry_sizes_launch(const int64_t* ctab, int64_t nkeys, const int32_t* cpool, int64_t* words,
                               hipStream_t st);
-hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st);
+hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st, hipFunction_t jf);
 hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
                                unsigned long long* out, hipStream_t st);
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
@@ -51,7 +52,7 @@ hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int6
 hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,
                              int64_t* ent_off, int64_t* total, int64_t* scan_tmp, int64_t* match_record,
                              int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name, int64_t* ent_record,
-                             hipStream_t st, bool lengths_only);
+                             hipStream_t st, bool lengths_only, hipFunction_t jf);
 hipError_t carry_move_launch(int64_t* ctab, int64_t nkeys, const int32_t* src, const int64_t* off, int32_t* dst,
                              hipStream_t st);
 }  // namespace kcep
@@ -139,6 +140,8 @@ struct cep_session {
   int64_t cpool_words = 0, cpool_used = 0;
   // ---- deterministic runs workspace ----
   DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof;
+  std::shared_ptr<const JitModule> jit;   // kernels compiled for the pattern (jit.cpp), else interpreted
+  std::string jit_why;
   int32_t g_err = CEP_OK;
   int64_t g_err_rec = -1;
   // ---- host CSR of the last collect ----
@@ -292,7 +295,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.err_code = s->r_errcode.as<int32_t>();
   const unsigned long long init[2] = {0, ~0ull};
   HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
-  HIPCHECK(runs_sim_launch(A, s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), st));
+  HIPCHECK(runs_sim_launch(A, s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), st,
+                           s->jit ? s->jit->runs_sim : nullptr));
   HIPCHECK(hipEventRecord(s->ev1, st));
   int64_t* scal0 = s->scal.as<int64_t>();
   HIPCHECK(exclusive_scan(s->flag.as<int64_t>(), n, s->idx.as<int64_t>(), scal0 + 3, s->scan_tmp.as<int64_t>(), st));
@@ -325,7 +329,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   int64_t* scal = s->scal.as<int64_t>();
   HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
                              s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
-                             nullptr, nullptr, nullptr, st, true));
+                             nullptr, nullptr, nullptr, st, true,
+                             s->jit ? s->jit->runs_write : nullptr));
   const int64_t ne = read_i64(scal + 4, st, &rc);
   if (rc) return fail(rc, "entry count");
   const size_t nmb = size_t(std::max<int64_t>(nm, 1)), neb = size_t(std::max<int64_t>(ne, 1));
@@ -335,7 +340,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
                              s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), s->o_record.as<int64_t>(),
                              s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
-                             s->o_entrec.as<int64_t>(), st, false));
+                             s->o_entrec.as<int64_t>(), st, false,
+                             s->jit ? s->jit->runs_write : nullptr));
   HIPCHECK(hipEventRecord(s->eb1, st));
   s->g_matches = nm;
   s->g_entries = ne;
@@ -602,6 +608,9 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   }
   if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
     return cleanup(fail(CEP_E_HIP, "event create failed"));
+  const char* env_jit = getenv("KCEP_JIT");
+  if (path == CEP_PATH_RUNS && !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0")))
+    s->jit = jit_runs(P, s->jit_why);            // on failure the built-in (interpreting) kernels run
   *out = s;
   return CEP_OK;
 }
@@ -624,6 +633,29 @@ void cep_session_close(cep_session* s) {
 }
 
 int cep_session_path(const cep_session* s) { return s ? s->path : 0; }
+
+int cep_session_jit(const cep_session* s) { return s && s->jit ? 1 : 0; }
+
+int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t cap, size_t* needed) {
+  if (!p || !needed) return fail(CEP_E_ARG, "null argument");
+  if (path != CEP_PATH_RUNS || !p->prog.runs_ok) return fail(CEP_E_UNSUPPORTED, "no compiled kernels for this path");
+  std::string why;
+  const std::string src = jit_source_runs(p->prog, why);
+  if (src.empty()) return fail(CEP_E_UNSUPPORTED, "kernel generation failed: " + why);
+  *needed = src.size() + 1;
+  if (!buf) return CEP_OK;
+  if (cap < *needed) return fail(CEP_E_ARG, "buffer too small");
+  memcpy(buf, src.c_str(), src.size() + 1);
+  return CEP_OK;
+}
+
+int cep_pattern_build_kernels(const cep_pattern* p, int path) {
+  if (!p) return fail(CEP_E_ARG, "null argument");
+  if (path != CEP_PATH_RUNS || !p->prog.runs_ok) return fail(CEP_E_UNSUPPORTED, "no compiled kernels for this path");
+  std::string why;
+  if (!jit_check_runs(p->prog, why)) return fail(CEP_E_UNSUPPORTED, "kernel build failed: " + why);
+  return CEP_OK;
+}
 
 int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   if (!s || !b) return fail(CEP_E_ARG, "null argument");

@@ -15,11 +15,13 @@
 //   void fail(int code);
 //   bool in_fold; int32_t curr_tag; int64_t curr;        // Aggregator's current value
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 #include "../../include/kcep.h"
-#include "kcep_internal.h"
+#include "kcep_dev.h"
 
 namespace kcep {
 
@@ -32,6 +34,67 @@ typedef const DevProgram __attribute__((address_space(4))) cDevProgram;
 __device__ __forceinline__ double bc_f(int64_t b) { return __builtin_bit_cast(double, b); }
 __device__ __forceinline__ int64_t bc_b(double d) { return __builtin_bit_cast(int64_t, d); }
 __device__ __forceinline__ int64_t bc_sx32(int64_t x) { return int64_t(int32_t(uint32_t(uint64_t(x)))); }
+
+// One binary opcode with Java semantics: 0, or the exception it raises.  The
+// interpreters call it with a loaded opcode, the per-pattern kernels (jit.cpp)
+// with a constant one, so both evaluate every operator through this one body.
+__device__ __forceinline__ int bc_bin(int op, int64_t x, int64_t y, int64_t& z) {
+  z = 0;
+  switch (op) {
+    case BC_ADD_I32: z = bc_sx32(x + y); break;
+    case BC_SUB_I32: z = bc_sx32(x - y); break;
+    case BC_MUL_I32: z = bc_sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
+    case BC_DIV_I32: if (y == 0) return CEP_E_ARITHMETIC; z = (x == INT32_MIN && y == -1) ? INT32_MIN : x / y; break;
+    case BC_REM_I32: if (y == 0) return CEP_E_ARITHMETIC; z = y == -1 ? 0 : x % y; break;
+    case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
+    case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
+    case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
+    case BC_DIV_I64: if (y == 0) return CEP_E_ARITHMETIC; z = (x == INT64_MIN && y == -1) ? INT64_MIN : x / y; break;
+    case BC_REM_I64: if (y == 0) return CEP_E_ARITHMETIC; z = y == -1 ? 0 : x % y; break;
+    case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;
+    case BC_SUB_F64: z = bc_b(bc_f(x) - bc_f(y)); break;
+    case BC_MUL_F64: z = bc_b(bc_f(x) * bc_f(y)); break;
+    case BC_DIV_F64: z = bc_b(bc_f(x) / bc_f(y)); break;
+    case BC_REM_F64: z = bc_b(fmod(bc_f(x), bc_f(y))); break;
+    case BC_EQ_I: z = x == y; break;
+    case BC_NE_I: z = x != y; break;
+    case BC_LT_I: z = x < y; break;
+    case BC_LE_I: z = x <= y; break;
+    case BC_GT_I: z = x > y; break;
+    case BC_GE_I: z = x >= y; break;
+    case BC_EQ_F: z = bc_f(x) == bc_f(y); break;
+    case BC_NE_F: z = bc_f(x) != bc_f(y); break;
+    case BC_LT_F: z = bc_f(x) < bc_f(y); break;
+    case BC_LE_F: z = bc_f(x) <= bc_f(y); break;
+    case BC_GT_F: z = bc_f(x) > bc_f(y); break;
+    case BC_GE_F: z = bc_f(x) >= bc_f(y); break;
+    case BC_EQ_B: z = (x != 0) == (y != 0); break;
+    case BC_NE_B: z = (x != 0) != (y != 0); break;
+    default: return CEP_E_BAD_IR;
+  }
+  return 0;
+}
+
+// unary opcodes (none raises)
+__device__ __forceinline__ int64_t bc_un(int op, int64_t x) {
+  switch (op) {
+    case BC_NOT: return x ? 0 : 1;
+    case BC_NEG_I32: return bc_sx32(0 - x);
+    case BC_NEG_I64: return int64_t(0ull - uint64_t(x));
+    case BC_NEG_F64: return bc_b(-bc_f(x));
+    case BC_I64_TO_I32: return bc_sx32(x);
+    case BC_I_TO_F64: return bc_b(double(x));
+    case BC_F64_TO_I32: {
+      const double d = bc_f(x);
+      return d != d ? 0 : d >= 2147483647.0 ? INT32_MAX : d <= -2147483648.0 ? INT32_MIN : int64_t(int32_t(d));
+    }
+    case BC_F64_TO_I64: {
+      const double d = bc_f(x);
+      return d != d ? 0 : d >= 9223372036854775807.0 ? INT64_MAX : d <= -9223372036854775808.0 ? INT64_MIN : int64_t(d);
+    }
+  }
+  return 0;
+}
 
 struct BcStack {
   int64_t s[NFA_STACK];
@@ -88,72 +151,17 @@ __device__ __forceinline__ bool interp(const int32_t* __restrict__ code, int pc,
         st.push(v);
         break;
       }
-      case BC_NOT: st.s[0] = st.s[0] ? 0 : 1; break;
       case BC_JZ_KEEP: if (st.s[0] == 0) pc += 1 + code[pc]; else { st.pop(); pc++; } break;
       case BC_JNZ_KEEP: if (st.s[0] != 0) pc += 1 + code[pc]; else { st.pop(); pc++; } break;
       case BC_POP: st.pop(); break;
-      case BC_NEG_I32: st.s[0] = bc_sx32(0 - st.s[0]); break;
-      case BC_NEG_I64: st.s[0] = int64_t(0ull - uint64_t(st.s[0])); break;
-      case BC_NEG_F64: st.s[0] = bc_b(-bc_f(st.s[0])); break;
-      case BC_I64_TO_I32: st.s[0] = bc_sx32(st.s[0]); break;
-      case BC_I_TO_F64: st.s[0] = bc_b(double(st.s[0])); break;
-      case BC_F64_TO_I32: {
-        const double d = bc_f(st.s[0]);
-        st.s[0] = d != d ? 0 : d >= 2147483647.0 ? INT32_MAX : d <= -2147483648.0 ? INT32_MIN : int64_t(int32_t(d));
+      case BC_NOT: case BC_NEG_I32: case BC_NEG_I64: case BC_NEG_F64: case BC_I64_TO_I32: case BC_I_TO_F64:
+      case BC_F64_TO_I32: case BC_F64_TO_I64:
+        st.s[0] = bc_un(op, st.s[0]);
         break;
-      }
-      case BC_F64_TO_I64: {
-        const double d = bc_f(st.s[0]);
-        st.s[0] = d != d ? 0 : d >= 9223372036854775807.0 ? INT64_MAX : d <= -9223372036854775808.0 ? INT64_MIN : int64_t(d);
-        break;
-      }
       default: {
-        const int64_t y = st.s[0], x = st.s[1];
-        int64_t z = 0;
-        switch (op) {
-          case BC_ADD_I32: z = bc_sx32(x + y); break;
-          case BC_SUB_I32: z = bc_sx32(x - y); break;
-          case BC_MUL_I32: z = bc_sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
-          case BC_DIV_I32:
-            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
-            z = (x == INT32_MIN && y == -1) ? INT32_MIN : x / y;
-            break;
-          case BC_REM_I32:
-            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
-            z = y == -1 ? 0 : x % y;
-            break;
-          case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
-          case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
-          case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
-          case BC_DIV_I64:
-            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
-            z = (x == INT64_MIN && y == -1) ? INT64_MIN : x / y;
-            break;
-          case BC_REM_I64:
-            if (y == 0) { env.fail(CEP_E_ARITHMETIC); return false; }
-            z = y == -1 ? 0 : x % y;
-            break;
-          case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;
-          case BC_SUB_F64: z = bc_b(bc_f(x) - bc_f(y)); break;
-          case BC_MUL_F64: z = bc_b(bc_f(x) * bc_f(y)); break;
-          case BC_DIV_F64: z = bc_b(bc_f(x) / bc_f(y)); break;
-          case BC_REM_F64: z = bc_b(fmod(bc_f(x), bc_f(y))); break;
-          case BC_EQ_I: z = x == y; break;
-          case BC_NE_I: z = x != y; break;
-          case BC_LT_I: z = x < y; break;
-          case BC_LE_I: z = x <= y; break;
-          case BC_GT_I: z = x > y; break;
-          case BC_GE_I: z = x >= y; break;
-          case BC_EQ_F: z = bc_f(x) == bc_f(y); break;
-          case BC_NE_F: z = bc_f(x) != bc_f(y); break;
-          case BC_LT_F: z = bc_f(x) < bc_f(y); break;
-          case BC_LE_F: z = bc_f(x) <= bc_f(y); break;
-          case BC_GT_F: z = bc_f(x) > bc_f(y); break;
-          case BC_GE_F: z = bc_f(x) >= bc_f(y); break;
-          case BC_EQ_B: z = (x != 0) == (y != 0); break;
-          case BC_NE_B: z = (x != 0) != (y != 0); break;
-          default: env.fail(CEP_E_BAD_IR); return false;
-        }
+        int64_t z;
+        const int e = bc_bin(op, st.s[1], st.s[0], z);
+        if (e) { env.fail(e); return false; }
         st.pop();
         st.s[0] = z;
       }
@@ -233,7 +241,6 @@ __device__ __forceinline__ bool interp_ls(const int32_t* __restrict__ code_flat,
         }
         break;
       }
-      case BC_NOT: if (on) st.s[0] = st.s[0] ? 0 : 1; break;
       case BC_JZ_KEEP: case BC_JNZ_KEEP: {
         const int target = pc + 1 + code[pc];
         if (on) {
@@ -245,62 +252,30 @@ __device__ __forceinline__ bool interp_ls(const int32_t* __restrict__ code_flat,
         break;
       }
       case BC_POP: if (on) st.pop(); break;
-      case BC_NEG_I32: if (on) st.s[0] = bc_sx32(0 - st.s[0]); break;
-      case BC_NEG_I64: if (on) st.s[0] = int64_t(0ull - uint64_t(st.s[0])); break;
-      case BC_NEG_F64: if (on) st.s[0] = bc_b(-bc_f(st.s[0])); break;
-      case BC_I64_TO_I32: if (on) st.s[0] = bc_sx32(st.s[0]); break;
-      case BC_I_TO_F64: if (on) st.s[0] = bc_b(double(st.s[0])); break;
-      case BC_F64_TO_I32: {
-        const double d = bc_f(st.s[0]);
-        if (on) st.s[0] = d != d ? 0 : d >= 2147483647.0 ? INT32_MAX : d <= -2147483648.0 ? INT32_MIN : int64_t(int32_t(d));
+      case BC_NOT: case BC_NEG_I32: case BC_NEG_I64: case BC_NEG_F64: case BC_I64_TO_I32: case BC_I_TO_F64:
+      case BC_F64_TO_I32: case BC_F64_TO_I64:
+        if (on) st.s[0] = bc_un(op, st.s[0]);
         break;
-      }
-      case BC_F64_TO_I64: {
-        const double d = bc_f(st.s[0]);
-        if (on) st.s[0] = d != d ? 0 : d >= 9223372036854775807.0 ? INT64_MAX : d <= -9223372036854775808.0 ? INT64_MIN : int64_t(d);
-        break;
-      }
       default: {
-        const int64_t y = st.s[0], x = st.s[1];
-        int64_t z = 0;
-        bool bad = false;
-        switch (op) {
-          case BC_ADD_I32: z = bc_sx32(x + y); break;
-          case BC_SUB_I32: z = bc_sx32(x - y); break;
-          case BC_MUL_I32: z = bc_sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
-          case BC_DIV_I32: if (y == 0) bad = true; else z = (x == INT32_MIN && y == -1) ? INT32_MIN : x / y; break;
-          case BC_REM_I32: if (y == 0) bad = true; else z = y == -1 ? 0 : x % y; break;
-          case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
-          case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
-          case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
-          case BC_DIV_I64: if (y == 0) bad = true; else z = (x == INT64_MIN && y == -1) ? INT64_MIN : x / y; break;
-          case BC_REM_I64: if (y == 0) bad = true; else z = y == -1 ? 0 : x % y; break;
-          case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;
-          case BC_SUB_F64: z = bc_b(bc_f(x) - bc_f(y)); break;
-          case BC_MUL_F64: z = bc_b(bc_f(x) * bc_f(y)); break;
-          case BC_DIV_F64: z = bc_b(bc_f(x) / bc_f(y)); break;
-          case BC_REM_F64: z = bc_b(fmod(bc_f(x), bc_f(y))); break;
-          case BC_EQ_I: z = x == y; break;
-          case BC_NE_I: z = x != y; break;
-          case BC_LT_I: z = x < y; break;
-          case BC_LE_I: z = x <= y; break;
-          case BC_GT_I: z = x > y; break;
-          case BC_GE_I: z = x >= y; break;
-          case BC_EQ_F: z = bc_f(x) == bc_f(y); break;
-          case BC_NE_F: z = bc_f(x) != bc_f(y); break;
-          case BC_LT_F: z = bc_f(x) < bc_f(y); break;
-          case BC_LE_F: z = bc_f(x) <= bc_f(y); break;
-          case BC_GT_F: z = bc_f(x) > bc_f(y); break;
-          case BC_GE_F: z = bc_f(x) >= bc_f(y); break;
-          case BC_EQ_B: z = (x != 0) == (y != 0); break;
-          case BC_NE_B: z = (x != 0) != (y != 0); break;
-          default: if (on) { env.fail(CEP_E_BAD_IR); ok = false; } break;
-        }
-        if (on && bad) { env.fail(CEP_E_ARITHMETIC); ok = false; }
+        int64_t z;
+        const int e = bc_bin(op, st.s[1], st.s[0], z);
+        if (on && e) { env.fail(e); ok = false; }
         else if (on) { st.pop(); st.s[0] = z; }
       }
     }
   }
 }
+
+// The program table of the built-in kernels: the pattern's DevProgram in
+// device memory (wave-uniform reads through the scalar cache), predicates and
+// folds interpreted in lock-step.  jit.cpp's JitTab has the same interface.
+struct InterpTab {
+  const DevProgram* raw;
+  __device__ __forceinline__ const cDevProgram& prog() const { return *(const cDevProgram*)raw; }
+  template <class Env>
+  __device__ __forceinline__ bool eval(int pc, Env& env, bool active, int64_t& v) const {
+    return interp_ls(raw->code, pc, env, active, v);
+  }
+};
 
 }  // namespace kcep

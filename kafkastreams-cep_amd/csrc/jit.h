@@ -1,0 +1,32 @@
+// jit.h — per-pattern kernels (jit.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+
+#include "kcep_internal.h"
+
+namespace kcep {
+
+// One pattern's specialised kernels, loaded from a code object hiprtc built.
+// Shared by every session of the same program text (process-wide cache).
+struct JitModule {
+  hipModule_t mod = nullptr;
+  hipFunction_t runs_sim = nullptr;     // runs_dev.h runs_sim_body<JitTab>
+  hipFunction_t runs_write = nullptr;   // runs_dev.h runs_write_body<JitTab>
+  ~JitModule();
+};
+
+// The HIP source of the pattern's runs kernels: the DevProgram as a constexpr
+// table plus every predicate / fold as straight-line code (empty + why if some
+// bytecode cannot be translated).
+std::string jit_source_runs(const Program& P, std::string& why);
+
+// Compile (or fetch from the cache) and load the runs kernels; nullptr + why on failure.
+std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why);
+
+// Generate and compile only (no device needed): false + why if either fails.
+bool jit_check_runs(const Program& P, std::string& why);
+
+}  // namespace kcep

@@ -27,280 +27,23 @@
 #include "../../include/kcep.h"
 #include "kcep_internal.h"
 #include "interp.h"
+#include "runs_dev.h"
 
 namespace kcep {
 
 namespace {
 
-constexpr int RT = 256;
-
-// aggregates of one run: (boxed type, value bits) per state, 0 = null
-struct RunState {
-  int32_t tag[RUNS_MAX_STATES];
-  int64_t val[RUNS_MAX_STATES];
-};
-
-constexpr int RUNS_COLCACHE = 4;   // columns of the current record held in registers
-
-__device__ __forceinline__ int64_t load_col(const RunsArgs& A, int col, int64_t g) {
-  const void* c = A.cols[col];
-  if (A.P->coltype[col] == T_I32) return static_cast<const int32_t*>(c)[g];
-  return static_cast<const int64_t*>(c)[g];
-}
-
-struct RunEnv {
-  const RunsArgs& A;
-  int64_t g;
-  const RunState& rs;
-  int err;
-  bool in_fold;
-  int32_t curr_tag;
-  int64_t curr;
-  const int64_t* cv;               // the record's first RUNS_COLCACHE columns, loaded once per step
-  __device__ __forceinline__ int64_t field(int col, int t) {
-    if (col < RUNS_COLCACHE) {
-      int64_t v = 0;
-#pragma unroll
-      for (int i = 0; i < RUNS_COLCACHE; i++)
-        if (i == col) v = cv[i];
-      return v;
-    }
-    const void* c = A.cols[col];
-    if (t == T_I32) return static_cast<const int32_t*>(c)[g];
-    return static_cast<const int64_t*>(c)[g];
-  }
-  __device__ __forceinline__ int64_t key() { return A.key[g]; }
-  __device__ __forceinline__ int64_t ts() { return A.ts ? A.ts[g] : A.base + g; }
-  __device__ __forceinline__ int64_t off() { return A.offset ? A.offset[g] : A.base + g; }
-  __device__ __forceinline__ int64_t part() { return A.partition ? A.partition[g] : 0; }
-  __device__ __forceinline__ int32_t topic() { return A.topic ? A.topic[g] : 0; }
-  __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) {
-    tag = 0;
-    v = 0;
-#pragma unroll
-    for (int i = 0; i < RUNS_MAX_STATES; i++)                // registers: select, no dynamic index
-      if (i == idx) { tag = rs.tag[i]; v = rs.val[i]; }
-    return true;
-  }
-  __device__ __forceinline__ bool seq_avg(int, int64_t&) { err = CEP_E_UNSUPPORTED; return false; }
-  __device__ __forceinline__ void fail(int code) { err = code; }
-};
-
-__device__ __forceinline__ bool wave_any(bool x) { return __builtin_amdgcn_ballot_w64(x) != 0; }
-
-// Runs walked in lock-step by the whole wave: one record per step for every
-// live lane, and per record the stages in descending id (PROCEED /
-// SKIP_PROCEED always lead to a smaller id, so a recursion on the same record
-// is met later in the same sweep).  For each stage every edge predicate is
-// evaluated (matchEdgesAndGet, NFA.java:371-384) by the lanes waiting there,
-// then the one consuming edge (BEGIN / TAKE, with the stage's folds,
-// :319-321) or the one recursion edge applies.
-//
-// A wave owns a chunk of RUNS_CHUNK items (start records, or completed runs to
-// write); a lane whose run ends takes the next item of the chunk at the next
-// step, so the wave does not idle behind its longest run.
-constexpr int RUNS_CHUNK = 512;
-
-struct RunResult {
-  int64_t end;        // record where the run consumed its last stage, -1 none
-  int64_t fail_at;    // record whose evaluation raised, -1 none
-  int err;
-};
-
-// item(i, &j, &stop): start record and last record to walk of item i (false: skip)
-// done(i, RunResult); on_consume(i, record, stage)
-template <class Item, class Done, class Consume>
-__device__ __forceinline__ void run_engine(const RunsArgs& A, int64_t i0, int64_t i1, Item&& item, Done&& done,
-                                           Consume&& on_consume) {
-  const cDevProgram* P = (const cDevProgram*)A.P;       // stage ids are wave-uniform: scalar reads
-  RunState rs;
-#pragma unroll
-  for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
-  RunResult res{-1, -1, 0};
-  bool alive = false;
-  int64_t idx = -1, r = 0, stop = 0;
-  int ps = -1, cur = -1;
-  int32_t k = 0;
-  int64_t next = i0;                                          // wave-uniform: next unassigned item
-  const int nst = P->nstages;
-  const int ncc = A.P->ncols < RUNS_COLCACHE ? A.P->ncols : RUNS_COLCACHE;
-  int64_t cv[RUNS_COLCACHE];
-#pragma unroll
-  for (int q = 0; q < RUNS_COLCACHE; q++) cv[q] = 0;
-  // the record's key and cached columns, issued together (one memory latency per step)
-  auto load_record = [&](int64_t g, int32_t* kk) {
-    *kk = A.key[g];
-#pragma unroll
-    for (int q = 0; q < RUNS_COLCACHE; q++)
-      if (q < ncc) cv[q] = load_col(A, q, g);
-  };
-  for (;;) {
-    // refill idle lanes from the chunk, in lane order
-    const uint64_t idle = __builtin_amdgcn_ballot_w64(!alive);
-    if (idle && next < i1) {
-      const int rank = __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0));
-      if (!alive) {
-        const int64_t it = next + rank;
-        int64_t j = 0;
-        if (it < i1 && item(it, &j, &stop)) {
-          idx = it;
-          alive = true;
-          r = j;
-          ps = P->begin;                                      // the begin run's evaluation on record j
-          cur = -1;
-          load_record(j, &k);
-          res = RunResult{-1, -1, 0};
-#pragma unroll
-          for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
-        }
-      }
-      next += __popcll(idle);
-    }
-    if (!__builtin_amdgcn_ballot_w64(alive)) {
-      if (next >= i1) break;
-      continue;
-    }
-    for (int s = nst - 1; s >= 1; s--) {
-      const bool here = alive && ps == s;
-      if (!wave_any(here)) continue;
-      const cDevStage& st = P->st[s];
-      uint32_t matched = 0;
-      bool ok = true;
-      for (int e = 0; e < st.nedges; e++) {
-        if (st.pred[e] < 0) { matched |= 1u << e; continue; }
-        RunEnv env{A, r, rs, 0, false, 0, 0, cv};
-        int64_t v;
-        const bool act = here && ok;
-        if (!interp_ls(A.P->code, st.pred[e], env, act, v)) {
-          if (act) { ok = false; res.err = env.err; }
-        } else if (act && v) {
-          matched |= 1u << e;
-        }
-      }
-      int take = -1, rec = -1;
-      for (int e = 0; e < st.nedges; e++)
-        if ((matched >> e) & 1) {
-          const int op = st.op[e];
-          if (op == E_BEGIN || op == E_TAKE) take = e;
-          else if (op == E_PROCEED || op == E_SKIP_PROCEED) rec = e;
-        }
-      const bool consume = here && ok && take >= 0;
-      for (int f = 0; f < st.nfolds; f++) {                      // evaluateAggregates (:362-369)
-        if (!wave_any(consume && ok)) break;
-        const int sidx = st.fold_state[f];
-        int32_t ct = 0;
-        int64_t cvv = 0;
-#pragma unroll
-        for (int q = 0; q < RUNS_MAX_STATES; q++)
-          if (q == sidx) { ct = rs.tag[q]; cvv = rs.val[q]; }
-        RunEnv env{A, r, rs, 0, true, ct, cvv, cv};
-        int64_t v;
-        const bool act = consume && ok;
-        if (!interp_ls(A.P->code, st.fold_code[f], env, act, v)) {
-          if (act) { ok = false; res.err = env.err; }
-        } else if (act) {
-          const int32_t ft = st.fold_type[f];
-#pragma unroll
-          for (int q = 0; q < RUNS_MAX_STATES; q++)
-            if (q == sidx) { rs.tag[q] = ft; rs.val[q] = v; }
-        }
-      }
-      if (here) {
-        if (!ok) {
-          res.fail_at = r;
-          ps = -2;                                                 // finished
-        } else if (take >= 0) {
-          on_consume(idx, r, s);
-          cur = st.op[take] == E_TAKE ? s : st.target[take];
-          ps = -1;
-          if (cur == 0) { res.end = r; ps = -2; }                // forwarding to $final: emitted
-        } else if (rec >= 0) {
-          ps = st.target[rec];
-        } else {
-          ps = -2;                                                 // no edge: the run is removed
-        }
-      }
-    }
-    if (alive) {
-      if (ps == -1) {                                              // consumed: on to the next record
-        r++;
-        int32_t kr = k + 1;
-        if (r < A.n && r <= stop) load_record(r, &kr);
-        ps = kr == k ? cur : -2;
-      } else if (ps != -2) {
-        ps = -2;                                                   // (a recursion that consumed nothing)
-      }
-      if (ps == -2) {
-        done(idx, res);
-        alive = false;
-      }
-    }
-  }
-}
-
-// end_of[j] = completing record of the run started at record j (flag[j] = 1), else flag 0
 __global__ __launch_bounds__(RT) void runs_sim(RunsArgs A, int64_t* __restrict__ flag, int32_t* __restrict__ end_of) {
-  const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
-  const int64_t i0 = wave * RUNS_CHUNK, i1 = i0 + RUNS_CHUNK < A.n ? i0 + RUNS_CHUNK : A.n;
-  if (i0 >= A.n) return;
-  run_engine(
-      A, i0, i1, [&](int64_t i, int64_t* j, int64_t* stop) { *j = i; *stop = INT64_MAX; return true; },
-      [&](int64_t i, const RunResult& res) {
-        flag[i] = res.end >= 0 ? 1 : 0;
-        end_of[i] = int32_t(res.end);
-        if (res.fail_at >= 0) {
-          A.err_code[i] = res.err;
-          atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
-        }
-      },
-      [](int64_t, int64_t, int) {});
+  runs_sim_body(InterpTab{A.P}, A, flag, end_of);
 }
+
+__global__ __launch_bounds__(RT) void runs_write(WriteArgs W) { runs_write_body(InterpTab{W.R.P}, W); }
 
 // completed runs in start order: key (end << 31 | start)
 __global__ void runs_compact(const int64_t* __restrict__ flag, const int64_t* __restrict__ pos,
                              const int32_t* __restrict__ end_of, int64_t n, unsigned long long* __restrict__ out) {
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (j < n && flag[j]) out[pos[j]] = (unsigned long long)(int64_t(end_of[j]) << 31 | j);
-}
-
-struct WriteArgs {
-  RunsArgs R;
-  const unsigned long long* sorted;
-  int64_t nm;
-  const int64_t* ent_off;        // exclusive scan of lengths
-  int64_t* match_record;
-  int32_t* match_key;
-  int64_t* ent_off_out;
-  int32_t* ent_name;
-  int64_t* ent_record;
-};
-
-__device__ __forceinline__ void put_entry(const WriteArgs& W, int64_t at, int stage, int64_t r) {
-  W.ent_name[at] = ((const cDevProgram*)W.R.P)->st[stage].name;
-  W.ent_record[at] = W.R.base + r;
-}
-
-// re-walk each completed run: traversal order is final stage first (peek :176-201)
-__global__ __launch_bounds__(RT) void runs_write(WriteArgs W) {
-  const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
-  const int64_t i0 = wave * RUNS_CHUNK, i1 = i0 + RUNS_CHUNK < W.nm ? i0 + RUNS_CHUNK : W.nm;
-  if (i0 >= W.nm) return;
-  run_engine(
-      W.R, i0, i1,
-      [&](int64_t m, int64_t* j, int64_t* stop) {
-        const unsigned long long kv = W.sorted[m];
-        *j = int64_t(kv & 0x7FFFFFFFull);
-        *stop = int64_t(kv >> 31);
-        W.match_record[m] = W.R.base + *stop;
-        W.match_key[m] = W.R.key[*j];
-        W.ent_off_out[m] = W.ent_off[m];
-        return true;
-      },
-      [](int64_t, const RunResult&) {},
-      [&](int64_t m, int64_t r, int stage) {
-        const int64_t end = int64_t(W.sorted[m] >> 31);
-        put_entry(W, W.ent_off[m] + (end - r), stage, r);
-      });
 }
 
 __global__ void runs_lengths(const unsigned long long* __restrict__ sorted, int64_t nm, int64_t* __restrict__ len) {
@@ -317,8 +60,14 @@ static unsigned runs_blocks(int64_t items) {
   return unsigned((waves * 64 + RT - 1) / RT);
 }
 
-hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st) {
+// jf: the pattern's compiled runs_sim (jit.cpp), nullptr for the built-in interpreting kernel
+hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st, hipFunction_t jf) {
   if (A.n <= 0) return hipSuccess;
+  if (jf) {
+    RunsArgs a = A;
+    void* args[] = {&a, &flag, &end_of};
+    return hipModuleLaunchKernel(jf, runs_blocks(A.n), 1, 1, RT, 1, 1, 0, st, args, nullptr);
+  }
   hipLaunchKernelGGL(runs_sim, dim3(runs_blocks(A.n)), dim3(RT), 0, st, A, flag, end_of);
   return hipGetLastError();
 }
@@ -339,13 +88,17 @@ hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int6
 hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,
                              int64_t* ent_off, int64_t* total, int64_t* scan_tmp, int64_t* match_record,
                              int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name, int64_t* ent_record,
-                             hipStream_t st, bool lengths_only) {
+                             hipStream_t st, bool lengths_only, hipFunction_t jf) {
   if (nm <= 0) return hipMemsetAsync(total, 0, sizeof(int64_t), st);
   if (lengths_only) {
     hipLaunchKernelGGL(runs_lengths, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, sorted, nm, len);
     return exclusive_scan(len, nm, ent_off, total, scan_tmp, st);
   }
   WriteArgs W{R, sorted, nm, ent_off, match_record, match_key, ent_off_out, ent_name, ent_record};
+  if (jf) {
+    void* args[] = {&W};
+    return hipModuleLaunchKernel(jf, runs_blocks(nm), 1, 1, RT, 1, 1, 0, st, args, nullptr);
+  }
   hipLaunchKernelGGL(runs_write, dim3(runs_blocks(nm)), dim3(RT), 0, st, W);
   return hipGetLastError();
 }

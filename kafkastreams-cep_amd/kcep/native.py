@@ -26,6 +26,7 @@ PATH_STENCIL, PATH_GENERAL, PATH_CHAIN, PATH_RUNS = 1, 2, 3, 4
 MEM_HOST, MEM_DEVICE = 0, 1
 BATCH_OFFSETS_MONOTONE = 1
 SESSION_CARRY = 1
+SESSION_INTERPRET = 2
 
 
 class CepError(RuntimeError):
@@ -64,7 +65,8 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_session_open",
            "cep_session_close", "cep_session_path", "cep_push_batch", "cep_device_match_count", "cep_collect",
            "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version",
-           "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position"]
+           "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position",
+           "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels"]
 
 _lib = None
 
@@ -111,6 +113,9 @@ def lib():
     L.cep_key_state.argtypes = [P, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.cep_stream_position.argtypes = [P]
     L.cep_stream_position.restype = C.c_int64
+    L.cep_session_jit.argtypes = [P]
+    L.cep_pattern_kernel_source.argtypes = [P, C.c_int32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    L.cep_pattern_build_kernels.argtypes = [P, C.c_int32]
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -147,6 +152,18 @@ class CompiledPattern:
             out.append((self.names[nm.value], ty.value, w.value, [(ops[i], tg[i]) for i in range(ne)]))
         return out
 
+    def kernel_source(self, path=PATH_RUNS) -> str:
+        """HIP source of the kernels compiled for this pattern (cep_pattern_kernel_source)."""
+        n = C.c_size_t()
+        check(lib().cep_pattern_kernel_source(self.h, path, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        check(lib().cep_pattern_kernel_source(self.h, path, buf, n.value, C.byref(n)))
+        return buf.value.decode()
+
+    def build_kernels(self, path=PATH_RUNS):
+        """Generate and compile (hiprtc, gfx950) the pattern's kernels; raises CepError on failure."""
+        check(lib().cep_pattern_build_kernels(self.h, path))
+
     def close(self):
         if self.h:
             lib().cep_pattern_free(self.h)
@@ -163,14 +180,18 @@ class Session:
     """One ``cep_session`` (one stream task's processor on one GPU)."""
 
     def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0,
-                 carry=False, max_keys=0):
+                 carry=False, max_keys=0, interpret=False):
         """``carry=True``: every key's NFA state continues across batches (CEP_SESSION_CARRY);
-        key ids must then be dense in [0, max_keys) and record positions are stream positions."""
+        key ids must then be dense in [0, max_keys) and record positions are stream positions.
+        ``interpret=True``: the built-in interpreting kernels instead of kernels compiled for the
+        pattern (CEP_SESSION_INTERPRET); ``self.jit`` says which run."""
         self.pattern = pattern
         self.h = C.c_void_p()
-        o = Opts(device, mode, force_path, SESSION_CARRY if carry else 0, max_events, max_keys, 0.0)
+        flags = (SESSION_CARRY if carry else 0) | (SESSION_INTERPRET if interpret else 0)
+        o = Opts(device, mode, force_path, flags, max_events, max_keys, 0.0)
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)
+        self.jit = bool(lib().cep_session_jit(self.h))
         self._keep = None
 
     def close(self):

@@ -98,6 +98,29 @@ def test_null_strategy_is_npe():
     assert eo.value.code == 4
 
 
+def test_runs_kernels_build():
+    """Every runs-path pattern of the golden scenarios (and C3) gets kernels compiled for it
+    (jit.cpp): one straight-line function per predicate / fold entry, built by hiprtc for gfx950."""
+    import re
+    sch = Schema([("value", "i32")])
+    irs = [synth.c3_pattern().to_ir(sch)] + [bytes.fromhex(f["ir"]) for f in scenarios()]
+    built = 0
+    for ir in irs:
+        cp = N.CompiledPattern(ir)
+        if not cp.info.runs_ok:
+            with pytest.raises(N.CepError):
+                cp.kernel_source(N.PATH_RUNS)
+            continue
+        src = cp.kernel_source(N.PATH_RUNS)
+        fns = set(re.findall(r"bool jf_(\d+)\(", src))
+        cases = set(re.findall(r"case (\d+): return jf_", src))
+        assert fns and fns == cases
+        assert "kcep_runs_sim" in src and "kcep_runs_write" in src
+        cp.build_kernels(N.PATH_RUNS)
+        built += 1
+    assert built >= 8
+
+
 def test_runs_eligibility():
     """Deterministic strict patterns take the runs path (compile.cpp analyse_runs): C3's
     oneOrMore predicate and its successor's are complementary comparisons."""

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 I32 = Schema([("value", "i32")])
 
 
-def both(ir, key, cols, coltypes, mode=N.MODE_PROCESSOR, **kw):
+def both(ir, key, cols, coltypes, mode=N.MODE_PROCESSOR, interpret=False, **kw):
     omode = O.MODE_PROCESSOR if mode == N.MODE_PROCESSOR else O.MODE_NFA_PER_KEY
     p = O.OraclePattern(ir)
     r = O.OracleRun(p, omode)
@@ -30,7 +30,8 @@ def both(ir, key, cols, coltypes, mode=N.MODE_PROCESSOR, **kw):
         oerr = (e.code, e.record)
     want = [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)]
     cp = N.CompiledPattern(ir)
-    s = N.Session(cp, max(1, len(key)), mode=mode, force_path=N.PATH_RUNS)
+    s = N.Session(cp, max(1, len(key)), mode=mode, force_path=N.PATH_RUNS, interpret=interpret)
+    assert s.jit == (not interpret)           # compiled-for-the-pattern kernels unless asked otherwise
     s.push(len(key), np.ascontiguousarray(key, np.int32), [np.ascontiguousarray(c) for c in cols],
            flags=N.BATCH_OFFSETS_MONOTONE, **kw)
     out = s.collect(raise_on_error=False)
@@ -51,14 +52,16 @@ RUNS_FIXTURES = ["nfa_stateful_condition", "nfa_times3", "nfa_optional_times2_em
                  "nfa_optional_strict", "nfa_strict3", "nfa_one_or_more", "readme_letters"]
 
 
+@pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("name", RUNS_FIXTURES)
-def test_golden_runs(name):
+def test_golden_runs(name, interpret):
     fx = [f for f in scenarios() if f["name"] == name][0]
     a = event_arrays(fx)
     key = a["key"] if fx["mode"] == O.MODE_PROCESSOR else np.zeros_like(a["key"])
     mode = N.MODE_PROCESSOR if fx["mode"] == O.MODE_PROCESSOR else N.MODE_NFA
     kw = {f: a[f] for f in ("topic", "partition", "offset", "ts") if a[f] is not None}
-    want, got, oerr, gerr = both(bytes.fromhex(fx["ir"]), key, a["cols"], a["coltypes"], mode=mode, **kw)
+    want, got, oerr, gerr = both(bytes.fromhex(fx["ir"]), key, a["cols"], a["coltypes"], mode=mode,
+                                 interpret=interpret, **kw)
     assert oerr is None and gerr is None
     assert got == want and len(got) == len(fx["expected"]["sequences"])
 
@@ -109,9 +112,10 @@ def _shapes():
     }
 
 
+@pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("shape", ["interval_one_or_more", "times3_then_opt", "running_avg", "topics"])
 @pytest.mark.parametrize("mode", [N.MODE_PROCESSOR, N.MODE_NFA])
-def test_shapes(shape, mode):
+def test_shapes(shape, mode, interpret):
     rng = np.random.default_rng(len(shape))
     n = 30_000
     key = np.sort(rng.integers(0, 400, n)).astype(np.int32)
@@ -120,12 +124,14 @@ def test_shapes(shape, mode):
     pat = _shapes()[shape]
     assert N.CompiledPattern(pat.to_ir(sch)).info.runs_ok
     kw = dict(topic=rng.integers(0, 2, n).astype(np.int32)) if shape == "topics" else {}
-    want, got, oerr, gerr = both(pat.to_ir(sch), key, [val.astype(np.int32)], [1], mode=mode, **kw)
+    want, got, oerr, gerr = both(pat.to_ir(sch), key, [val.astype(np.int32)], [1], mode=mode, interpret=interpret,
+                                 **kw)
     assert oerr is None and gerr is None
     assert got == want and len(got) > 20
 
 
-def test_exceptions_match_the_reference():
+@pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
+def test_exceptions_match_the_reference(interpret):
     """The first exception of the batch (here: integer division by zero in a
     stage predicate, and an unset state) and its record are the reference's."""
     a = (QueryBuilder().select("a").where(v >= 0).fold("x", Event.value()).then()
@@ -134,7 +140,7 @@ def test_exceptions_match_the_reference():
     rng = np.random.default_rng(8)
     key = np.sort(rng.integers(0, 200, 5000)).astype(np.int32)
     val = rng.integers(0, 5, 5000).astype(np.int32)
-    want, got, oerr, gerr = both(a.to_ir(I32), key, [val], [1])
+    want, got, oerr, gerr = both(a.to_ir(I32), key, [val], [1], interpret=interpret)
     assert oerr is not None and gerr == oerr
     assert got == want
 
