@@ -177,7 +177,7 @@ def main():
                        "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
-                         "kernel": {N.PATH_GENERAL: "nfa_kernel",
+                         "kernel": {N.PATH_GENERAL: "kcep_nfa_kernel" if sess.jit else "nfa_kernel",
                                     N.PATH_RUNS: "kcep_runs_sim" if sess.jit else "runs_sim"}.get(sess.path, "stencil_kernel"),
                          "kernel_ms": avg_kernel_ms, "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": None,

@@ -30,7 +30,7 @@ int64_t stencil_tiles(int64_t n);
 hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t nm, int32_t* mkey,
                         const StencilProgram* P, unsigned long long* sum, hipStream_t st);
 
-hipError_t nfa_launch(const NfaArgs& A, hipStream_t st);
+hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
 hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
@@ -140,7 +140,11 @@ struct cep_session {
   int64_t cpool_words = 0, cpool_used = 0;
   // ---- deterministic runs workspace ----
   DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof;
-  std::shared_ptr<const JitModule> jit;   // kernels compiled for the pattern (jit.cpp), else interpreted
+  // kernels compiled for the pattern (jit.cpp); null: the built-in interpreting kernels run
+  bool jit_on = false;                     // allowed (not CEP_SESSION_INTERPRET / KCEP_JIT=0)
+  std::shared_ptr<const JitModule> jit;    // runs path
+  std::shared_ptr<const JitModule> jitg;   // general path (built at open, or at the first general batch)
+  bool jitg_tried = false;
   std::string jit_why;
   int32_t g_err = CEP_OK;
   int64_t g_err_rec = -1;
@@ -351,6 +355,10 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
 int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   const Program& P = s->pat->prog;
   const int64_t n = b->n;
+  if (s->jit_on && !s->jitg_tried) {           // a stencil / runs session's first batch that needs the NFA
+    s->jitg = jit_general(P, s->jit_why);
+    s->jitg_tried = true;
+  }
   NfaArgs A{};
   A.P = s->dprog.as<DevProgram>();
   A.n = n;
@@ -424,7 +432,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     unsigned long long init[4] = {0, (unsigned long long)s->cpool_used, 0, 0};
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
-    HIPCHECK(nfa_launch(A, st));
+    HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
     if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
     timed = true;
     unsigned long long res[4];
@@ -609,8 +617,12 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
     return cleanup(fail(CEP_E_HIP, "event create failed"));
   const char* env_jit = getenv("KCEP_JIT");
-  if (path == CEP_PATH_RUNS && !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0")))
-    s->jit = jit_runs(P, s->jit_why);            // on failure the built-in (interpreting) kernels run
+  s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
+  if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels
+  if (s->jit_on && path == CEP_PATH_GENERAL) {
+    s->jitg = jit_general(P, s->jit_why);
+    s->jitg_tried = true;
+  }
   *out = s;
   return CEP_OK;
 }
@@ -634,13 +646,17 @@ void cep_session_close(cep_session* s) {
 
 int cep_session_path(const cep_session* s) { return s ? s->path : 0; }
 
-int cep_session_jit(const cep_session* s) { return s && s->jit ? 1 : 0; }
+int cep_session_jit(const cep_session* s) {
+  if (!s) return 0;
+  return (s->path == CEP_PATH_RUNS && s->jit) || (s->path == CEP_PATH_GENERAL && s->jitg) ? 1 : 0;
+}
 
 int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t cap, size_t* needed) {
   if (!p || !needed) return fail(CEP_E_ARG, "null argument");
-  if (path != CEP_PATH_RUNS || !p->prog.runs_ok) return fail(CEP_E_UNSUPPORTED, "no compiled kernels for this path");
+  const bool runs = path == CEP_PATH_RUNS && p->prog.runs_ok, general = path == CEP_PATH_GENERAL && p->prog.general_ok;
+  if (!runs && !general) return fail(CEP_E_UNSUPPORTED, "no compiled kernels for this path");
   std::string why;
-  const std::string src = jit_source_runs(p->prog, why);
+  const std::string src = runs ? jit_source_runs(p->prog, why) : jit_source_general(p->prog, why);
   if (src.empty()) return fail(CEP_E_UNSUPPORTED, "kernel generation failed: " + why);
   *needed = src.size() + 1;
   if (!buf) return CEP_OK;
@@ -651,9 +667,11 @@ int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t 
 
 int cep_pattern_build_kernels(const cep_pattern* p, int path) {
   if (!p) return fail(CEP_E_ARG, "null argument");
-  if (path != CEP_PATH_RUNS || !p->prog.runs_ok) return fail(CEP_E_UNSUPPORTED, "no compiled kernels for this path");
+  const bool runs = path == CEP_PATH_RUNS && p->prog.runs_ok, general = path == CEP_PATH_GENERAL && p->prog.general_ok;
+  if (!runs && !general) return fail(CEP_E_UNSUPPORTED, "no compiled kernels for this path");
   std::string why;
-  if (!jit_check_runs(p->prog, why)) return fail(CEP_E_UNSUPPORTED, "kernel build failed: " + why);
+  if (!(runs ? jit_check_runs(p->prog, why) : jit_check_general(p->prog, why)))
+    return fail(CEP_E_UNSUPPORTED, "kernel build failed: " + why);
   return CEP_OK;
 }
 

@@ -329,6 +329,31 @@ std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why) {
   return build(src, names, slots, 2, why);
 }
 
+std::string jit_source_general(const Program& P, std::string& why) {
+  std::string o = "#include \"interp.h\"\n";
+  if (!gen_program(P, o, why)) return "";
+  o += R"(#include "nfa_dev.h"
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void kcep_nfa_kernel(kcep::NfaArgs A) {
+  kcep::nfa_kernel_body(A);
+}
+)";
+  return o;
+}
+
+std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why) {
+  const std::string src = jit_source_general(P, why);
+  if (src.empty()) return nullptr;
+  static const char* const names[] = {"kcep_nfa_kernel"};
+  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa};
+  return build(src, names, slots, 1, why);
+}
+
+bool jit_check_general(const Program& P, std::string& why) {
+  const std::string src = jit_source_general(P, why);
+  std::vector<char> code;
+  return !src.empty() && compile(src, code, why);
+}
+
 bool jit_check_runs(const Program& P, std::string& why) {
   const std::string src = jit_source_runs(P, why);
   std::vector<char> code;

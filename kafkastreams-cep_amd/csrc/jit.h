@@ -15,6 +15,7 @@ struct JitModule {
   hipModule_t mod = nullptr;
   hipFunction_t runs_sim = nullptr;     // runs_dev.h runs_sim_body<JitTab>
   hipFunction_t runs_write = nullptr;   // runs_dev.h runs_write_body<JitTab>
+  hipFunction_t nfa = nullptr;          // nfa_dev.h nfa_kernel_body (general path)
   ~JitModule();
 };
 
@@ -28,5 +29,10 @@ std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why);
 
 // Generate and compile only (no device needed): false + why if either fails.
 bool jit_check_runs(const Program& P, std::string& why);
+
+// the same for the general NFA path's kernel (nfa_dev.h)
+std::string jit_source_general(const Program& P, std::string& why);
+std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why);
+bool jit_check_general(const Program& P, std::string& why);
 
 }  // namespace kcep

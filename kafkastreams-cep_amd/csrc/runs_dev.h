@@ -7,10 +7,12 @@
 #pragma once
 #include "interp.h"
 
+#ifndef KCEP_UNROLL
 #ifdef KCEP_JIT
 #define KCEP_UNROLL _Pragma("unroll")
 #else
 #define KCEP_UNROLL
+#endif
 #endif
 
 namespace kcep {

@@ -26,7 +26,7 @@ def grouped(fx):
     return out, order
 
 
-def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, **kw):
+def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, interpret=False, **kw):
     p = O.OraclePattern(ir)
     r = O.OracleRun(p, mode)
     oerr = None
@@ -36,7 +36,9 @@ def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, **kw):
         oerr = (e.code, e.record)
     want = [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)]
     cp = N.CompiledPattern(ir)
-    s = N.Session(cp, max(1, len(key)), mode=mode, force_path=force)
+    s = N.Session(cp, max(1, len(key)), mode=mode, force_path=force, interpret=interpret)
+    if force == N.PATH_GENERAL:
+        assert s.jit == (not interpret)       # kernel compiled for the pattern unless asked otherwise
     s.push(len(key), np.ascontiguousarray(key, np.int32), [np.ascontiguousarray(c) for c in cols], **kw)
     gerr = None
     out = s.collect(raise_on_error=False)
@@ -60,11 +62,13 @@ def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, **kw):
 SC = scenarios()
 
 
+@pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("fx", SC, ids=[f["name"] for f in SC])
-def test_golden_general(fx):
+def test_golden_general(fx, interpret):
     g, order = grouped(fx)
     kw = {k: g[k] for k in ("topic", "partition", "offset", "ts", "valid") if g[k] is not None}
-    want, got, oerr, gerr = run_both(bytes.fromhex(fx["ir"]), fx["mode"], g["key"], g["cols"], g["coltypes"], **kw)
+    want, got, oerr, gerr = run_both(bytes.fromhex(fx["ir"]), fx["mode"], g["key"], g["cols"], g["coltypes"],
+                                     interpret=interpret, **kw)
     assert oerr is None and gerr is None
     assert got == want
     # and the reference's own expectation, mapped back to the fixture's record indices
@@ -89,9 +93,10 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("mode", [O.MODE_PROCESSOR, O.MODE_NFA_PER_KEY])
 @pytest.mark.parametrize("name,mk,vmax,gen", CASES, ids=[c[0] for c in CASES])
-def test_random_general(name, mk, vmax, gen, mode):
+def test_random_general(name, mk, vmax, gen, mode, interpret):
     per_key = 8 if name in ("c4_any", "any_any") else 30
     key, val = rand_stream(hash(name) % 1000, 300, per_key, vmax)
     if gen is not None:
@@ -103,7 +108,8 @@ def test_random_general(name, mk, vmax, gen, mode):
     r.process(O.BatchArrays(key, [val], [1]))
     want = [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)]
     cp = N.CompiledPattern(ir)
-    s = N.Session(cp, len(key), mode=gmode, force_path=N.PATH_GENERAL)
+    s = N.Session(cp, len(key), mode=gmode, force_path=N.PATH_GENERAL, interpret=interpret)
+    assert s.jit == (not interpret)
     s.push(len(key), key, [val])
     out = s.collect()
     got = []

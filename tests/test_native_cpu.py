@@ -121,6 +121,16 @@ def test_runs_kernels_build():
     assert built >= 8
 
 
+def test_general_kernels_build():
+    """The general path's kernel compiled for C4 and for a golden scenario with state,
+    getOrElse-free folds and topics (hiprtc, gfx950)."""
+    sch = Schema([("value", "i32")])
+    for ir in (synth.c4_pattern().to_ir(sch), bytes.fromhex([f for f in scenarios() if f["name"] == "stock_demo"][0]["ir"])):
+        cp = N.CompiledPattern(ir)
+        assert "kcep_nfa_kernel" in cp.kernel_source(N.PATH_GENERAL)
+        cp.build_kernels(N.PATH_GENERAL)
+
+
 def test_runs_eligibility():
     """Deterministic strict patterns take the runs path (compile.cpp analyse_runs): C3's
     oneOrMore predicate and its successor's are complementary comparisons."""
