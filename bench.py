@@ -185,6 +185,9 @@ def main():
         }
         if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):
             line["batch_ms"] = sess.last_batch_ms()
+        if sess.path == N.PATH_GENERAL:
+            line["config"]["live_run_hwm"] = sess.live_run_hwm()     # run-explosion high-water mark
+            line["config"]["keys_on_cpu"] = 0                        # no CPU fallback: every key runs on the GPU
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = _cpu_baseline(args.config, key, cols, ts, ir, args.cpu_threads, n_matches, csum,
                                                  sess, stream)

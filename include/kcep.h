@@ -98,6 +98,9 @@ typedef struct {
                                     and folds, instead of kernels compiled for the pattern at cep_session_open
                                     (hiprtc; also disabled by the environment variable KCEP_JIT=0) */
 
+#define CEP_SESSION_PROFILE 4    /* general path: record per key segment its live-run high-water mark, run
+                                    evaluations and kernel cycles (cep_key_profile) */
+
 #define CEP_MEM_HOST 0
 #define CEP_MEM_DEVICE 1
 
@@ -168,6 +171,18 @@ void cep_session_close(cep_session* s);
 int cep_session_path(const cep_session* s);
 /* 1 if the session runs kernels compiled for its pattern (see CEP_SESSION_INTERPRET), else 0 */
 int cep_session_jit(const cep_session* s);
+/* General path: the most live runs (NFA run queue length, NFAStates.java:33-37) any key held during the
+   last batch -- C4's run-explosion high-water mark.  -1 if the last batch ran on another path. */
+int cep_live_run_hwm(const cep_session* s, int64_t* hwm);
+/* CEP_SESSION_PROFILE sessions, after a general-path batch: per key segment {key id, live-run
+   high-water mark, run evaluations, kernel wall clock (100 MHz ticks), then shader clocks spent in
+   NFA.evaluate / edge predicates / buffer put+branch / removePattern / matchConstruction /
+   getPointerByVersion scans / predecessor appends / Dewey version copies, then counts of scans /
+   predecessor entries examined / digit-by-digit version checks (-1 each when the session runs the
+   built-in kernel), then 0 (reserved) and the workspace words the key took from the device pool};
+   17 int64 per key;
+   out == NULL sets only *n_keys. */
+int cep_key_profile(cep_session* s, int64_t* out, int64_t cap, int64_t* n_keys);
 /* The HIP source of the pattern's compiled kernels for a path (CEP_PATH_RUNS), NUL-terminated;
    with buf == NULL only *needed is set.  CEP_E_UNSUPPORTED if the path has none for this pattern. */
 int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t cap, size_t* needed);

@@ -145,6 +145,8 @@ struct cep_session {
   std::shared_ptr<const JitModule> jit;    // runs path
   std::shared_ptr<const JitModule> jitg;   // general path (built at open, or at the first general batch)
   bool jitg_tried = false;
+  int64_t live_hwm = 0;                    // general path: most live runs any key held in the last batch
+  DBuf r_prof;                             // CEP_SESSION_PROFILE: per key segment {live max, evaluations, cycles}
   std::string jit_why;
   int32_t g_err = CEP_OK;
   int64_t g_err_rec = -1;
@@ -356,7 +358,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   const Program& P = s->pat->prog;
   const int64_t n = b->n;
   if (s->jit_on && !s->jitg_tried) {           // a stencil / runs session's first batch that needs the NFA
-    s->jitg = jit_general(P, s->jit_why);
+    s->jitg = jit_general(P, s->jit_why, s->opts.flags & CEP_SESSION_PROFILE);
     s->jitg_tried = true;
   }
   NfaArgs A{};
@@ -418,6 +420,14 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.pool_top = ctl;
   A.cpool_top = ctl + 1;
   A.flags = reinterpret_cast<int32_t*>(ctl + 2);
+  // key segments per wave (KCEP_NFA_SPREAD: experiments; fewer keys per wave diverge less but leave
+  // the chip emptier -- tools/c4_profile.py)
+  const char* spread_env = getenv("KCEP_NFA_SPREAD");
+  A.spread = spread_env ? std::min(64, std::max(1, atoi(spread_env))) : 64;
+  if (s->opts.flags & CEP_SESSION_PROFILE) {
+    if (s->r_prof.ensure(sb * NFA_PROFILE_W)) return fail(CEP_E_HIP, "allocation failed");
+    A.profile = s->r_prof.as<int64_t>();
+  }
   bool timed = false;
   for (int attempt = 0;; attempt++) {
     if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
@@ -440,6 +450,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     HIPCHECK(hipStreamSynchronize(st));
     const int32_t* fl = reinterpret_cast<const int32_t*>(res + 2);
     if (fl[2]) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    s->live_hwm = fl[3];
     if (!fl[0] && !fl[1]) {
       if (s->carry) s->cpool_used = int64_t(res[1]);
       break;
@@ -620,7 +631,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
   if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels
   if (s->jit_on && path == CEP_PATH_GENERAL) {
-    s->jitg = jit_general(P, s->jit_why);
+    s->jitg = jit_general(P, s->jit_why, s->opts.flags & CEP_SESSION_PROFILE);
     s->jitg_tried = true;
   }
   *out = s;
@@ -634,7 +645,7 @@ void cep_session_close(cep_session* s) {
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
                   &s->o_entrec, &s->ctab, &s->cpool, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
-                  &s->r_errcode, &s->r_endof})
+                  &s->r_errcode, &s->r_endof, &s->r_prof})
     b->release();
   for (auto& c : s->h_cols) c.release();
   if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -645,6 +656,32 @@ void cep_session_close(cep_session* s) {
 }
 
 int cep_session_path(const cep_session* s) { return s ? s->path : 0; }
+
+int cep_live_run_hwm(const cep_session* s, int64_t* hwm) {
+  if (!s || !hwm) return fail(CEP_E_ARG, "null argument");
+  *hwm = s->last_path == CEP_PATH_GENERAL ? s->live_hwm : -1;
+  return CEP_OK;
+}
+
+int cep_key_profile(cep_session* s, int64_t* out, int64_t cap, int64_t* n_keys) {
+  if (!s || !n_keys) return fail(CEP_E_ARG, "null argument");
+  if (!(s->opts.flags & CEP_SESSION_PROFILE) || s->last_path != CEP_PATH_GENERAL)
+    return fail(CEP_E_UNSUPPORTED, "key profiles need CEP_SESSION_PROFILE and a general-path batch");
+  *n_keys = s->nseg;
+  if (!out) return CEP_OK;
+  constexpr int W = 1 + NFA_PROFILE_W;
+  if (cap < W * s->nseg) return fail(CEP_E_ARG, "buffer too small");
+  std::vector<int64_t> p(size_t(NFA_PROFILE_W * s->nseg)), start(size_t(s->nseg));
+  std::vector<int32_t> keys(size_t(std::max<int64_t>(s->n, 1)));
+  HIPCHECK(hipMemcpy(p.data(), s->r_prof.p, p.size() * 8, hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(start.data(), s->seg.p, start.size() * 8, hipMemcpyDeviceToHost));
+  if (s->n > 0) HIPCHECK(hipMemcpy(keys.data(), s->d_key, size_t(s->n) * 4, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < s->nseg; i++) {
+    out[W * i] = keys[size_t(start[size_t(i)])];
+    for (int j = 0; j < NFA_PROFILE_W; j++) out[W * i + 1 + j] = p[size_t(NFA_PROFILE_W * i + j)];
+  }
+  return CEP_OK;
+}
 
 int cep_session_jit(const cep_session* s) {
   if (!s) return 0;

@@ -329,8 +329,8 @@ std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why) {
   return build(src, names, slots, 2, why);
 }
 
-std::string jit_source_general(const Program& P, std::string& why) {
-  std::string o = "#include \"interp.h\"\n";
+std::string jit_source_general(const Program& P, std::string& why, bool phases) {
+  std::string o = phases ? "#define KCEP_PHASES 1\n#include \"interp.h\"\n" : "#include \"interp.h\"\n";
   if (!gen_program(P, o, why)) return "";
   o += R"(#include "nfa_dev.h"
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void kcep_nfa_kernel(kcep::NfaArgs A) {
@@ -340,8 +340,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
   return o;
 }
 
-std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why) {
-  const std::string src = jit_source_general(P, why);
+std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why, bool phases) {
+  const std::string src = jit_source_general(P, why, phases);
   if (src.empty()) return nullptr;
   static const char* const names[] = {"kcep_nfa_kernel"};
   static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa};

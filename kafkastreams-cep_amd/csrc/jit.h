@@ -31,8 +31,9 @@ std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why);
 bool jit_check_runs(const Program& P, std::string& why);
 
 // the same for the general NFA path's kernel (nfa_dev.h)
-std::string jit_source_general(const Program& P, std::string& why);
-std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why);
+std::string jit_source_general(const Program& P, std::string& why, bool phases = false);
+// phases: the profiling build (KCEP_PHASES clocks, CEP_SESSION_PROFILE sessions)
+std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why, bool phases = false);
 bool jit_check_general(const Program& P, std::string& why);
 
 }  // namespace kcep

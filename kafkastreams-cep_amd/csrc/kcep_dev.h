@@ -58,6 +58,11 @@ constexpr int NFA_MAX_SL = 64;     // event-only edge predicates evaluated once 
 constexpr int NFA_STACK = 8;       // operand stack of the device interpreter (registers)
 constexpr int NFA_MAX_FRAMES = 16; // NFA.evaluate recursion depth of the device kernel
 constexpr int RUNS_MAX_STATES = 8; // aggregate registers of one deterministic run
+// per key segment: live-run max, run evaluations, wall clock (100 MHz), then (profiling kernels; -1
+// otherwise) shader clocks in evaluate / predicates / buffer put+branch / removePattern /
+// matchConstruction / first_compatible / add_pred / version copies, and counts of first_compatible
+// calls / pred entries examined / digit-by-digit checks
+constexpr int NFA_PROFILE_W = 16;   // + reserved (0) / workspace words taken from the pool
 
 struct DevStage {
   int32_t name, type, slot, nedges, nfolds;
@@ -135,7 +140,10 @@ struct NfaArgs {
   int64_t* res_out;               // device address of the key's output region
   int32_t* res_err;
   int64_t* res_err_rec;
-  int32_t* flags;                 // [0] pool overflow lanes, [1] carry-pool overflow lanes, [2] bad key ids
+  int32_t* flags;                 // [0] pool overflow lanes, [1] carry-pool overflow lanes, [2] bad key ids,
+                                  // [3] live-run high-water mark over the batch's keys
+  int64_t* profile;               // CEP_SESSION_PROFILE: NFA_PROFILE_W words per segment (nfa_dev.h)
+  int32_t spread;                 // key segments per wave (1..64)
 };
 
 // deterministic-runs path (runs.hip)

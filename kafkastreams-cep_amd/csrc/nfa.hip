@@ -126,15 +126,17 @@ __global__ void scan_final(const int64_t* __restrict__ in, int64_t n, const int6
   }
 }
 
-// jf: the pattern's compiled nfa kernel (jit.cpp), nullptr for the built-in interpreting one
+// jf: the pattern's compiled nfa kernel (jit.cpp), nullptr for the built-in interpreting one.
+// One wave per workgroup, A.spread key segments per wave.
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf) {
   if (A.nseg <= 0) return hipSuccess;
+  const unsigned grid = unsigned((A.nseg + A.spread - 1) / A.spread);
   if (jf) {
     NfaArgs a = A;
     void* args[] = {&a};
-    return hipModuleLaunchKernel(jf, unsigned((A.nseg + 63) / 64), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+    return hipModuleLaunchKernel(jf, grid, 1, 1, 64, 1, 1, 0, st, args, nullptr);
   }
-  hipLaunchKernelGGL(nfa_kernel, dim3(unsigned((A.nseg + 63) / 64)), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(nfa_kernel, dim3(grid), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 

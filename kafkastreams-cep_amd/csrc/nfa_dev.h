@@ -69,12 +69,32 @@ struct Lane {
   int64_t g;                   // its batch record index
   int64_t nmatch;
   uint64_t slm, sle;           // event-only edge predicates on record r: values / deferred errors
+  int64_t pool_words;          // taken from the pool (profile)
+#ifdef KCEP_PHASES
+  uint64_t ph[11];             // profiling kernels only: clocks in evaluate / predicates / buffer puts+branch /
+                               // removePattern / matchConstruction / first_compatible / add_pred / versions,
+                               // then counts: first_compatible calls / entries examined / digit-by-digit checks
+#endif
 };
 
+// phase timers of the profiling kernels (jit.cpp builds them for CEP_SESSION_PROFILE sessions)
+#ifdef KCEP_PHASES
+#define KPH_BEGIN(l, i) const uint64_t kph_t##i = clock64()
+#define KPH_END(l, i) const_cast<Lane&>(l).ph[i] += clock64() - kph_t##i
+#define KPH_COUNT(l, i, n) const_cast<Lane&>(l).ph[i] += (n)
+#else
+#define KPH_BEGIN(l, i)
+#define KPH_END(l, i)
+#define KPH_COUNT(l, i, n)
+#endif
+
 // ---- pool ----
+// every allocation is a multiple of 16 bytes (queues are read as int4)
 __device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words) {
-  const unsigned long long at = atomicAdd(l.A->pool_top, (unsigned long long)words);
-  if (at + (unsigned long long)words > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
+  const int64_t w = (words + 3) & ~int64_t(3);
+  const unsigned long long at = atomicAdd(l.A->pool_top, (unsigned long long)w);
+  if (at + (unsigned long long)w > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
+  l.pool_words += w;
   return l.A->pool + at;
 }
 // re-allocate `*a` (cap words used up to `used`) at >= need words
@@ -114,7 +134,7 @@ __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
   l.heap_top += words;
   return at;
 }
-__device__ __forceinline__ int dw_add_stage(Lane& l, int v) {             // DeweyVersion.addStage :95-97
+__device__ __forceinline__ int dw_add_stage_(Lane& l, int v) {            // DeweyVersion.addStage :95-97
   const int len = l.heap[v];
   const int n = heap_alloc(l, len + 2);
   if (n < 0) return -1;
@@ -123,7 +143,7 @@ __device__ __forceinline__ int dw_add_stage(Lane& l, int v) {             // Dew
   l.heap[n + 1 + len] = 0;
   return n;
 }
-__device__ __forceinline__ int dw_add_run(Lane& l, int v, int off) {      // DeweyVersion.addRun :62-67
+__device__ __forceinline__ int dw_add_run_(Lane& l, int v, int off) {     // DeweyVersion.addRun :62-67
   const int len = l.heap[v];
   const int idx = len - off;
   if (idx < 0 || idx >= len) { l.err = CEP_E_INDEX; return -1; }
@@ -134,6 +154,19 @@ __device__ __forceinline__ int dw_add_run(Lane& l, int v, int off) {      // Dew
   l.heap[n + 1 + idx] = int32_t(uint32_t(l.heap[n + 1 + idx]) + 1u);
   return n;
 }
+__device__ __forceinline__ int dw_add_stage(Lane& l, int v) {
+  KPH_BEGIN(l, 7);
+  const int n = dw_add_stage_(l, v);
+  KPH_END(l, 7);
+  return n;
+}
+__device__ __forceinline__ int dw_add_run(Lane& l, int v, int off) {
+  KPH_BEGIN(l, 7);
+  const int n = dw_add_run_(l, v, off);
+  KPH_END(l, 7);
+  return n;
+}
+
 // a.isCompatible(b) (:73-93), with b's length and first digit known up front
 __device__ __forceinline__ bool dw_compatible(const Lane& l, int a, int b, int lb, int b0) {
   const int la = l.heap[a];
@@ -157,7 +190,7 @@ __device__ __forceinline__ int32_t* node(Lane& l, int slot, int ev) {
 __device__ __forceinline__ int slot_of(const Lane& l, int sid) { return stg(l, sid).slot; }
 __device__ __forceinline__ bool exists(const int32_t* nd) { return nd[3] & NF_EXISTS; }
 
-__device__ __forceinline__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslot, int pev) {   // MatchedEvent.addPredecessor
+__device__ __forceinline__ bool add_pred_(Lane& l, int32_t* nd, int ver, int pslot, int pev) {   // MatchedEvent.addPredecessor
   const int p = heap_alloc(l, PW);
   if (p < 0) return false;
   l.heap[p] = ver; l.heap[p + 1] = pslot; l.heap[p + 2] = pev; l.heap[p + 3] = -1;
@@ -166,6 +199,12 @@ __device__ __forceinline__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslo
   else l.heap[nd[2] + 3] = p;
   nd[2] = p;
   return true;
+}
+__device__ __forceinline__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslot, int pev) {
+  KPH_BEGIN(l, 6);
+  const bool ok = add_pred_(l, nd, ver, pslot, pev);
+  KPH_END(l, 6);
+  return ok;
 }
 // put 5-arg (SharedVersionedBufferStoreImpl.java:101-126)
 __device__ __forceinline__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_sid, int pev, int ver) {
@@ -182,13 +221,21 @@ __device__ __forceinline__ void buf_put3(Lane& l, int cur_sid, int ev, int ver) 
   c[0] = 1; c[1] = -1; c[2] = -1; c[3] = NF_EXISTS;
   add_pred(l, c, ver, -1, 0);
 }
-__device__ __forceinline__ int first_compatible(const Lane& l, const int32_t* nd, int ver, int* prevp) {   // getPointerByVersion
+__device__ __forceinline__ int first_compatible_(const Lane& l, const int32_t* nd, int ver, int* prevp) {   // getPointerByVersion
   int pp = -1;
   for (int p = nd[1]; p >= 0; p = l.heap[p + 3]) {
+    KPH_COUNT(l, 9, 1);
     if (dw_compatible(l, ver, l.heap[p], l.heap[p + 4], l.heap[p + 5])) { if (prevp) *prevp = pp; return p; }
     pp = p;
   }
   return -1;
+}
+__device__ __forceinline__ int first_compatible(const Lane& l, const int32_t* nd, int ver, int* prevp) {
+  KPH_BEGIN(l, 5);
+  const int p = first_compatible_(l, nd, ver, prevp);
+  KPH_END(l, 5);
+  KPH_COUNT(l, 8, 1);
+  return p;
 }
 // branch (:132-142)
 __device__ __forceinline__ void buf_branch(Lane& l, int sid, int ev, int ver) {
@@ -420,7 +467,10 @@ __device__ __forceinline__ bool frame_enter(Lane& l, Frame& f) {
       } else {
         Ctx c{f.cs.seq, f.prev_sid >= 0 ? int(f.prev_sid) : -1, f.cs.ev, f.cs.ver, false, 0, 0};
         int64_t v;
-        if (!run_code(l, pc, c, v)) return false;
+        KPH_BEGIN(l, 1);
+        const bool good = run_code(l, pc, c, v);
+        KPH_END(l, 1);
+        if (!good) return false;
         ok = v != 0;
       }
     }
@@ -435,15 +485,16 @@ __device__ __forceinline__ bool frame_enter(Lane& l, Frame& f) {
 
 // NFA.evaluate (NFA.java:190-341) for one run; results appended to tq
 __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
+  // the current frame lives in registers; fr[] (scratch) holds only the suspended parents
   int d = 0;
-  fr[0].cs = run;
-  fr[0].cur_sid = int16_t(r_sid(run));
-  fr[0].cur_eps = int16_t(r_eps(run));
-  fr[0].prev_sid = -1;
-  fr[0].prev_eps = EPS_NONE;
-  if (!frame_enter(l, fr[0])) return false;
+  Frame f;
+  f.cs = run;
+  f.cur_sid = int16_t(r_sid(run));
+  f.cur_eps = int16_t(r_eps(run));
+  f.prev_sid = -1;
+  f.prev_eps = EPS_NONE;
+  if (!frame_enter(l, f)) return false;
   for (;;) {
-    Frame& f = fr[d];
     if (f.i < f.nm) {
       const int e = f.medge[f.i++];
       const bool eps = f.cur_eps != EPS_NONE;
@@ -453,7 +504,7 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
       const int ver = f.cs.ver, seq = f.cs.seq;
       if (op == E_PROCEED || op == E_SKIP_PROCEED) {                 // :222-237
         if (d + 1 >= MAXD) { l.overflow = 1; return false; }
-        Frame& g = fr[d + 1];
+        Frame g;
         g.cs = f.cs;
         if (stg(l, target).name != s.name && !r_br(f.cs) && !r_ig(f.cs)) {   // isForwardingToNextStage :343-349
           const int nv = dw_add_stage(l, ver);
@@ -466,21 +517,26 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
         g.cur_eps = EPS_NONE;
         f.before = l.tlen;
         f.pending = 1;
-        d++;
-        if (!frame_enter(l, fr[d])) return false;
+        fr[d++] = f;                                                  // suspend the parent
+        f = g;
+        if (!frame_enter(l, f)) return false;
         continue;
       }
       if (op == E_TAKE) {                                            // :238-255
         if (!push_t(l, mk_run(f.cur_sid, f.cur_sid, ver, l.r, seq, false, false))) return false;
         int pv = ver;
         if (!(!f.branching || f.ignored)) { pv = dw_add_run(l, ver, 1); if (pv < 0) return false; }
+        KPH_BEGIN(l, 2);
         if (f.prev_sid >= 0) buf_put5(l, f.cur_sid, l.r, f.prev_sid, f.cs.ev, pv);
         else buf_put3(l, f.cur_sid, l.r, pv);
+        KPH_END(l, 2);
         if (l.err || l.overflow) return false;
         f.consumed = 1;
       } else if (op == E_BEGIN) {                                    // :256-271
+        KPH_BEGIN(l, 2);
         if (f.prev_sid >= 0) buf_put5(l, f.cur_sid, l.r, f.prev_sid, f.cs.ev, ver);
         else buf_put3(l, f.cur_sid, l.r, ver);
+        KPH_END(l, 2);
         if (l.err || l.overflow) return false;
         if (!push_t(l, mk_run(f.cur_sid, target, ver, l.r, seq, false, false))) return false;
         f.consumed = 1;
@@ -510,7 +566,12 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
           if (!dst) return false;
           if (s0) { dst[0] = s0; dst[1] = s1; dst[2] = s2; }
         }
-        if (!pb) { buf_branch(l, f.prev_sid, pev, ver); if (l.err) return false; }
+        if (!pb) {
+          KPH_BEGIN(l, 2);
+          buf_branch(l, f.prev_sid, pev, ver);
+          KPH_END(l, 2);
+          if (l.err) return false;
+        }
       } else if (!f.proceed) {
         if (!push_t(l, f.cs)) return false;
       }
@@ -541,11 +602,10 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
       }
     }
     if (d == 0) return true;
-    d--;
-    Frame& p = fr[d];
-    if (p.pending) {
-      if (l.tlen > p.before) p.proceed = 1;
-      p.pending = 0;
+    f = fr[--d];                                                      // resume the parent
+    if (f.pending) {
+      if (l.tlen > f.before) f.proceed = 1;
+      f.pending = 0;
     }
   }
 }
@@ -598,9 +658,15 @@ __device__ __forceinline__ bool step(Lane& l, Frame* fr) {
     l.tlen = 0;
     // window check (:179-188): every non-begin run sits on an epsilon stage
     // whose window is -1, so it never prunes; nothing to evaluate.
-    if (!evaluate(l, run, fr)) return false;
+    KPH_BEGIN(l, 0);
+    const bool good = evaluate(l, run, fr);
+    KPH_END(l, 0);
+    if (!good) return false;
     if (l.tlen == 0) {                                               // removePattern :160-163
-      if (buf_peek(l, r_sid(run), run.ev, run.ver, true, nullptr, 0) < 0) return false;
+      KPH_BEGIN(l, 3);
+      const int rm = buf_peek(l, r_sid(run), run.ev, run.ver, true, nullptr, 0);
+      KPH_END(l, 3);
+      if (rm < 0) return false;
     }
     for (int t = 0; t < l.tlen; t++) {
       const int4 y = reinterpret_cast<int4*>(l.tq)[t];
@@ -621,7 +687,10 @@ __device__ __forceinline__ bool step(Lane& l, Frame* fr) {
   l.qlen = qn;
   for (int k = 0; k < l.flen; k++) {                                // matchConstruction :151-158
     const int4 y = reinterpret_cast<int4*>(l.fq)[k];
-    if (!emit_match(l, Run{y.x, y.y, y.z, y.w})) return false;
+    KPH_BEGIN(l, 4);
+    const bool good = emit_match(l, Run{y.x, y.y, y.z, y.w});
+    KPH_END(l, 4);
+    if (!good) return false;
   }
   return true;
 }
@@ -845,11 +914,13 @@ __device__ __forceinline__ int64_t export_state(Lane& l) {
 }
 
 __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
-  const int seg = blockIdx.x * blockDim.x + threadIdx.x;
-  if (seg >= A.nseg) return;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int seg = (gid >> 6) * A.spread + (gid & 63);
+  if ((gid & 63) >= A.spread || seg >= A.nseg) return;
   Lane l;
   l.A = &A;
   l.P = A.P;
+  l.pool_words = 0;
   const auto& P = KCEP_PROG(l);
   l.seg0 = A.seg_start[seg];
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
@@ -918,6 +989,12 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   Frame fr[MAXD];
   int64_t err_rec = -1;
   const bool proc = A.mode == CEP_MODE_PROCESSOR;
+#ifdef KCEP_PHASES
+  for (int i = 0; i < 11; i++) l.ph[i] = 0;
+#endif
+  int32_t live_max = l.qlen;                                         // live-run high-water mark of the key
+  int64_t evals = 0;
+  const uint64_t t0 = A.profile ? wall_clock64() : 0;
   for (int i = 0; i < l.L && !l.err && !l.overflow; i++) {
     const int r = l.C + i;
     const int64_t g = l.seg0 + i;
@@ -934,10 +1011,12 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
       }
     }
     eval_event_only(l);
+    evals += l.qlen;
     if (!step(l, fr)) {
       if (l.err) err_rec = A.base + g;
       break;
     }
+    live_max = l.qlen > live_max ? l.qlen : live_max;
     if (proc) {
       const int h = hwm_find(l, b_topic(l, g));
       if (h == l.nhwm) {
@@ -953,6 +1032,20 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   if (A.carry && !l.err && !l.overflow) {                              // NFAStoreImpl.put (:144-147)
     const int64_t at = export_state(l);
     if (at >= 0) A.res_carry[seg] = at;
+  }
+  atomicMax(&A.flags[3], live_max);
+  if (A.profile) {
+    int64_t* pr = A.profile + NFA_PROFILE_W * int64_t(seg);
+    pr[0] = live_max;
+    pr[1] = evals;
+    pr[2] = int64_t(wall_clock64() - t0);
+#ifdef KCEP_PHASES
+    for (int i = 0; i < 11; i++) pr[3 + i] = int64_t(l.ph[i]);
+#else
+    for (int i = 0; i < 11; i++) pr[3 + i] = -1;
+#endif
+    pr[14] = 0;                                                        // (no LDS workspace)
+    pr[15] = l.pool_words;
   }
   A.res_matches[seg] = l.nmatch;
   A.res_words[seg] = l.out_top;

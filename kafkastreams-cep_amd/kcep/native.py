@@ -27,6 +27,7 @@ MEM_HOST, MEM_DEVICE = 0, 1
 BATCH_OFFSETS_MONOTONE = 1
 SESSION_CARRY = 1
 SESSION_INTERPRET = 2
+SESSION_PROFILE = 4
 
 
 class CepError(RuntimeError):
@@ -66,7 +67,8 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_session_close", "cep_session_path", "cep_push_batch", "cep_device_match_count", "cep_collect",
            "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version",
            "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position",
-           "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels"]
+           "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels", "cep_live_run_hwm",
+           "cep_key_profile"]
 
 _lib = None
 
@@ -114,6 +116,8 @@ def lib():
     L.cep_stream_position.argtypes = [P]
     L.cep_stream_position.restype = C.c_int64
     L.cep_session_jit.argtypes = [P]
+    L.cep_live_run_hwm.argtypes = [P, C.POINTER(C.c_int64)]
+    L.cep_key_profile.argtypes = [P, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
     L.cep_pattern_kernel_source.argtypes = [P, C.c_int32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
     L.cep_pattern_build_kernels.argtypes = [P, C.c_int32]
     L.cep_last_error.restype = C.c_char_p
@@ -180,14 +184,15 @@ class Session:
     """One ``cep_session`` (one stream task's processor on one GPU)."""
 
     def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0,
-                 carry=False, max_keys=0, interpret=False):
+                 carry=False, max_keys=0, interpret=False, profile=False):
         """``carry=True``: every key's NFA state continues across batches (CEP_SESSION_CARRY);
         key ids must then be dense in [0, max_keys) and record positions are stream positions.
         ``interpret=True``: the built-in interpreting kernels instead of kernels compiled for the
         pattern (CEP_SESSION_INTERPRET); ``self.jit`` says which run."""
         self.pattern = pattern
         self.h = C.c_void_p()
-        flags = (SESSION_CARRY if carry else 0) | (SESSION_INTERPRET if interpret else 0)
+        flags = ((SESSION_CARRY if carry else 0) | (SESSION_INTERPRET if interpret else 0) |
+                 (SESSION_PROFILE if profile else 0))
         o = Opts(device, mode, force_path, flags, max_events, max_keys, 0.0)
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)
@@ -248,6 +253,22 @@ class Session:
         n = C.c_int64()
         check(lib().cep_checksum(self.h, C.byref(s), C.byref(n)))
         return n.value, s.value
+
+    def live_run_hwm(self) -> int:
+        """General path: the most live runs any key held during the last batch (-1: other path)."""
+        v = C.c_int64()
+        check(lib().cep_live_run_hwm(self.h, C.byref(v)))
+        return v.value
+
+    def key_profile(self):
+        """``profile=True`` sessions: int64 array [n_keys, 17] (cep_key_profile): key, live-run max, run
+        evaluations, wall clock (100 MHz), 8 phase clocks, 3 scan counters, 0, pool words."""
+        import numpy as np
+        n = C.c_int64()
+        check(lib().cep_key_profile(self.h, None, 0, C.byref(n)))
+        out = np.zeros((n.value, 17), np.int64)
+        check(lib().cep_key_profile(self.h, out.ctypes.data, out.size, C.byref(n)))
+        return out
 
     # ---- carried state (CEP_SESSION_CARRY) ----
     def state_export(self, key_lo=0, key_hi=2**31 - 1) -> bytes:

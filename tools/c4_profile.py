@@ -1,0 +1,52 @@
+"""Per-key cost profile of the general path on C4 (CEP_SESSION_PROFILE): where the kernel's time goes.
+
+Prints the kernel time, the distribution of per-key cycles / live runs / run evaluations, and the
+heaviest keys.  Usage (GPU box): python tools/c4_profile.py [n_keys] [--interpret]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kafkastreams-cep_amd"))
+import torch  # noqa: E402
+from kcep import native as N, synth, Schema  # noqa: E402
+
+K = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 100_000
+interp = "--interpret" in sys.argv
+key, val, ts = synth.c4_stream_torch(K, "cuda")
+n = key.numel()
+cp = N.CompiledPattern(synth.c4_pattern().to_ir(Schema([("value", "i32")])))
+s = N.Session(cp, n, force_path=N.PATH_GENERAL, profile=True, interpret=interp)
+st = torch.cuda.current_stream().cuda_stream
+for i in range(3):
+    s.push(n, key.data_ptr(), [val.data_ptr()], ts=ts.data_ptr(), mem=N.MEM_DEVICE, stream=st)
+    kms = s.last_kernel_ms()
+prof = s.key_profile()
+cyc = prof[:, 3].astype(np.float64) / 100.0   # wall clock 100 MHz -> us
+live, ev = prof[:, 1], prof[:, 2]
+print(f"jit={s.jit} kernel {kms:.2f} ms  keys {len(prof)}  live-run hwm {s.live_run_hwm()}")
+for nm, a in (("key us", cyc), ("live runs", live), ("evaluations", ev)):
+    print(f"{nm:12s} mean {a.mean():9.2f} p50 {np.median(a):9.2f} p99 {np.percentile(a, 99):9.2f} "
+          f"p99.9 {np.percentile(a, 99.9):9.2f} max {a.max():9.2f} sum {a.sum():.3e}")
+o = np.argsort(-cyc)[:10]
+print("heaviest keys (key, live max, evals, us):")
+for i in o:
+    print("  ", int(prof[i, 0]), int(live[i]), int(ev[i]), round(float(cyc[i]), 1))
+print("us per evaluation (top 100 keys):", float(cyc[o[:100]].sum() / max(1, ev[np.argsort(-cyc)[:100]].sum())))
+print("corr(evals, us)", float(np.corrcoef(ev, cyc)[0, 1]))
+ws = prof[:, 15] + prof[:, 16]
+print("workspace words: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %d; heaviest key %d" %
+      (ws.mean(), np.median(ws), np.percentile(ws, 90), np.percentile(ws, 99), ws.max(), ws[o[0]]))
+ph = prof[:, 4:15].astype(np.float64)
+if (ph >= 0).all():
+    names = ["evaluate", "predicates", "buffer put+branch", "removePattern", "matchConstruction", "scans",
+             "add_pred", "versions"]
+    for sel, nm in ((slice(None), "all keys"), (o[:100], "top-100 keys")):
+        tot = ph[sel].sum(axis=0)
+        print(nm, "clock share of evaluate+remove+emit:",
+              {n: round(float(t / (tot[0] + tot[3] + tot[4])), 3) for n, t in zip(names, tot[:8])})
+        print(nm, "scans", int(tot[8]), "entries/scan", round(float(tot[9] / max(1, tot[8])), 2),
+              "digit checks/scan", round(float(tot[10] / max(1, tot[8])), 2),
+              "clocks/scan", round(float(tot[5] / max(1, tot[8])), 1))
