@@ -12,12 +12,14 @@ key, val, _ = synth.c2_stream_torch(n, K, "cuda")
 torch.cuda.synchronize()
 s = N.Session(N.CompiledPattern(synth.c2_pattern().to_ir(Schema([("value", "i32")]))), n)
 st = torch.cuda.current_stream().cuda_stream
-ms = []
+ms, bms = [], []
 for i in range(25):
     s.push(n, key.data_ptr(), [val.data_ptr()], mem=N.MEM_DEVICE, stream=st)
     ms.append(s.last_kernel_ms())
+    bms.append(s.last_batch_ms())
 nm, cs = s.checksum()
-print(json.dumps({"lib": os.environ["KCEP_LIB"], "ms": statistics.median(ms[5:]), "matches": nm, "csum": "%%016x" %% cs}))
+print(json.dumps({"lib": os.environ["KCEP_LIB"], "ms": statistics.median(ms[5:]), "batch_ms": statistics.median(bms[5:]),
+                  "matches": nm, "csum": "%%016x" %% cs}))
 ''' % ROOT
 for lib in sorted(glob.glob(os.path.join(ROOT, "build_variants", "*", "libkcep.so"))):
     env = dict(os.environ, KCEP_LIB=lib)

@@ -11,7 +11,9 @@ rm -rf build_variants
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   mkdir -p build_variants/$name
-  /opt/rocm/bin/hipcc $F $flags -x hip -c kafkastreams-cep_amd/csrc/stencil.hip -o build_variants/$name/stencil.o
-  /opt/rocm/bin/hipcc $F -shared -o build_variants/$name/libkcep.so $B/compile.cpp.o $B/abi.cpp.o $B/nfa.hip.o $B/runs.hip.o build_variants/$name/stencil.o
-  rm build_variants/$name/stencil.o
+  O=build_variants/$name/stencil.o
+  /opt/rocm/bin/hipcc $F $flags -x hip -c kafkastreams-cep_amd/csrc/stencil.hip -o $O
+  /opt/rocm/bin/hipcc $F -shared -o build_variants/$name/libkcep.so $B/compile.cpp.o $B/abi.cpp.o $B/jit.cpp.o \
+    $B/nfa.hip.o $B/runs.hip.o $O -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
+  rm $O
 done
