@@ -332,8 +332,11 @@ std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why) {
 std::string jit_source_general(const Program& P, std::string& why, bool phases) {
   std::string o = phases ? "#define KCEP_PHASES 1\n#include \"interp.h\"\n" : "#include \"interp.h\"\n";
   if (!gen_program(P, o, why)) return "";
-  o += R"(#include "nfa_dev.h"
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void kcep_nfa_kernel(kcep::NfaArgs A) {
+  // waves per SIMD the register budget is cut for (KCEP_NFA_WAVES, tuning only)
+  const char* wenv = getenv("KCEP_NFA_WAVES");
+  const int waves = wenv ? std::min(8, std::max(1, atoi(wenv))) : 2;
+  o += "#include \"nfa_dev.h\"\nextern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(" +
+       std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
   kcep::nfa_kernel_body(A);
 }
 )";
