@@ -7,9 +7,10 @@ matching itself runs in hand-written HIP kernels behind the C-ABI of
 from .expr import (Event, States, Curr, SequenceAgg, Int, Long, Double, T_I32, T_I64, T_F64)  # noqa: F401
 from .pattern import (QueryBuilder, Pattern, PatternBuilder, StageBuilder, PredicateBuilder,  # noqa: F401
                       Selected, Strategy, Cardinality, TimeUnit, Schema)
+from .serde import JsonSequenceSerde  # noqa: F401
 
 __all__ = [
     "Event", "States", "Curr", "SequenceAgg", "Int", "Long", "Double",
     "QueryBuilder", "Pattern", "PatternBuilder", "StageBuilder", "PredicateBuilder",
-    "Selected", "Strategy", "Cardinality", "TimeUnit", "Schema",
+    "Selected", "Strategy", "Cardinality", "TimeUnit", "Schema", "JsonSequenceSerde",
 ]
