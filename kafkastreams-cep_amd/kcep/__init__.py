@@ -8,9 +8,12 @@ from .expr import (Event, States, Curr, SequenceAgg, Int, Long, Double, T_I32, T
 from .pattern import (QueryBuilder, Pattern, PatternBuilder, StageBuilder, PredicateBuilder,  # noqa: F401
                       Selected, Strategy, Cardinality, TimeUnit, Schema)
 from .serde import JsonSequenceSerde  # noqa: F401
+from .ingest import StockEvent, StockEventSerde, ColumnDecoder  # noqa: F401
+from .processor import GpuCEPProcessor  # noqa: F401
 
 __all__ = [
     "Event", "States", "Curr", "SequenceAgg", "Int", "Long", "Double",
     "QueryBuilder", "Pattern", "PatternBuilder", "StageBuilder", "PredicateBuilder",
     "Selected", "Strategy", "Cardinality", "TimeUnit", "Schema", "JsonSequenceSerde",
+    "StockEvent", "StockEventSerde", "ColumnDecoder", "GpuCEPProcessor",
 ]

@@ -1,0 +1,178 @@
+"""GpuCEPProcessor: batching host mirror of the reference ``CEPProcessor``.
+
+Reference: ``cep/processor/CEPProcessor.java:46-171``.  The reference steps one
+key's NFA per ``process(key, value)`` call, loading and saving the key's state in
+its stores around each record (``loadNFA`` ``:111-124``, ``nfaStore.put``
+``:144-147``) and forwarding the completed ``Sequence``s at once (``:148``).
+
+This processor keeps the same contract but hands the records to the device in
+batches: ``process`` appends the record to a host buffer and a
+flush -- on ``batch_size`` records, ``punctuate`` or ``close`` -- does one
+``cep_push_batch`` on a carry session (``CEP_SESSION_CARRY``), whose device-side
+per-key state (run queue, runs counter, high-water marks, buffer nodes, fold
+registers) plays the role of the reference's three stores.
+
+* **Null filter** (``:135-138``): a record with a null key or value is dropped
+  before anything else, so it neither touches state nor moves the high-water
+  mark.
+* **High-water mark** (``:140, 152-160``): evaluated on the device per key and
+  topic, across batches.
+* **Keys and topics** are interned to dense ids (``key_id`` for the carry
+  session, topic ids from the pattern's ``Schema`` so that ``withTopic`` filters
+  keep their ids).
+* **Values** are decoded into the schema's typed columns by a
+  ``kcep.ingest.ColumnDecoder``.
+* **Forward order.**  Each batch is stable-sorted by key for the device; the
+  matches are then put back into arrival order of their completing record
+  (stable, so one record's matches keep ``matchPattern``'s order).  The forwarded
+  stream is therefore exactly the reference's, record for record -- only delayed
+  to the flush.
+* **Errors.**  Where the reference throws out of ``process()`` (user-predicate
+  exceptions, ``UnknownAggregateException``, the buffer's ``IllegalStateException``)
+  the flush forwards the matches of the records that arrived before the failing
+  one and raises ``CepError``; the processor is then failed, as the reference's
+  stream task is.
+* **Query name** normalisation copies ``:83``: ``toLowerCase()`` then
+  ``String.replace("\\\\s+", "")``, which is a *literal* replace in Java (no regex).
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from . import native as N
+from .ingest import ColumnDecoder
+from .pattern import Pattern, Schema
+from .sequence import Event, Sequence, sequence_from_traversal
+
+
+class ProcessorFailed(RuntimeError):
+    pass
+
+
+class GpuCEPProcessor:
+    """One stream task's processor for one query (``CEPProcessor`` equivalent)."""
+
+    def __init__(self, queryName: str, pattern: Union[Pattern, bytes], schema: Schema, decoder: ColumnDecoder,
+                 batch_size: int = 1 << 16, max_keys: int = 1 << 20, device: int = 0,
+                 mode: int = N.MODE_PROCESSOR):
+        if decoder.schema is not schema and decoder.schema.columns != schema.columns:
+            raise ValueError("decoder and pattern use different schemas")
+        self.queryName = queryName.lower().replace("\\s+", "")
+        self.schema = schema
+        self.decoder = decoder
+        self.batch_size = int(batch_size)
+        self.max_keys = int(max_keys)
+        self.device = device
+        self.mode = mode
+        ir = pattern if isinstance(pattern, (bytes, bytearray)) else pattern.to_ir(schema)
+        self.compiled = N.CompiledPattern(bytes(ir))
+        self.session: Optional[N.Session] = None
+        self._forward: Optional[Callable[[Any, Sequence], None]] = None
+        self._keys: Dict[Any, int] = {}
+        self._pending: List[Tuple[int, tuple, int, int, int, int, Event]] = []
+        self._log: Dict[int, Event] = {}          # stream position -> Event (carried runs point back here)
+        self._failed: Optional[Exception] = None
+
+    # ---- Processor API (CEPProcessor.init/process/punctuate/close, :88-170) ----
+    def init(self, forward: Callable[[Any, Sequence], None], session=None):
+        """``forward(key, sequence)`` is ``ProcessorContext.forward`` (``:148``).  ``session``
+        defaults to a carry ``kcep.native.Session`` on ``device`` (tests pass a stand-in to
+        check the host logic without a GPU)."""
+        self._forward = forward
+        self.session = session or N.Session(self.compiled, self.batch_size, mode=self.mode, device=self.device,
+                                            carry=True, max_keys=self.max_keys)
+
+    def process(self, key, value, topic: str, partition: int, offset: int, timestamp: int):
+        """One record with its ``ProcessorContext`` metadata."""
+        self._check()
+        if key is None or value is None:                  # :135-138
+            return
+        kid = self._keys.get(key)
+        if kid is None:
+            if len(self._keys) >= self.max_keys:
+                raise N.CepError(11, f"more than max_keys={self.max_keys} distinct keys")
+            kid = self._keys[key] = len(self._keys)
+        row = self.decoder.row(value)
+        ev = Event(key, value, int(timestamp), topic, int(partition), int(offset))
+        self._pending.append((kid, row, self.schema.topic_id(topic), int(partition), int(offset), int(timestamp), ev))
+        if len(self._pending) >= self.batch_size:
+            self.flush()
+
+    def punctuate(self, timestamp: int):
+        self.flush()
+
+    def close(self):
+        try:
+            if self._failed is None and self.session is not None:
+                self.flush()
+        finally:
+            if self.session is not None:
+                self.session.close()
+                self.session = None
+
+    # ---- batching ----
+    def flush(self) -> int:
+        """Push the buffered records as one batch and forward its matches; returns how many."""
+        self._check()
+        if not self._pending:
+            return 0
+        recs, self._pending = self._pending, []
+        n = len(recs)
+        kid = np.fromiter((r[0] for r in recs), np.int32, n)
+        perm = np.argsort(kid, kind="stable")             # the device wants the batch grouped by key
+        sorted_recs = [recs[i] for i in perm]
+        cols = self.decoder.columns([r[1] for r in sorted_recs])
+        topic = np.fromiter((r[2] for r in sorted_recs), np.int32, n)
+        part = np.fromiter((r[3] for r in sorted_recs), np.int32, n)
+        off = np.fromiter((r[4] for r in sorted_recs), np.int64, n)
+        ts = np.fromiter((r[5] for r in sorted_recs), np.int64, n)
+        base = self.session.stream_position()
+        for i, r in enumerate(sorted_recs):
+            self._log[base + i] = r[6]
+        self.session.push(n, kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts)
+        out = self.session.collect(raise_on_error=False)
+
+        mrec = out["match_record"] - base                 # stream position -> batch position
+        m_arrival = perm[mrec] if len(mrec) else np.zeros(0, np.int64)
+        order = np.argsort(m_arrival, kind="stable")
+        limit = None
+        if out["err"]:
+            limit = int(perm[int(out["err_record"]) - base])
+        names = self.compiled.names
+        sent = 0
+        for m in order:
+            if limit is not None and m_arrival[m] >= limit:
+                break
+            a, b = int(out["ent_off"][m]), int(out["ent_off"][m + 1])
+            ents = [(int(out["ent_name"][i]), int(out["ent_record"][i])) for i in range(a, b)]
+            seq = sequence_from_traversal(ents, names, self._log.__getitem__)
+            self._forward(recs[m_arrival[m]][6].key, seq)
+            sent += 1
+        if out["err"]:
+            self._failed = N.CepError(int(out["err"]), out.get("msg") or N.lib().cep_last_error().decode(), limit)
+            raise self._failed
+        return sent
+
+    # ---- checkpoint / restore (the NFAStore / buffer / aggregates stores) ----
+    def checkpoint(self) -> dict:
+        """Flushes, then returns the device state (``cep_state_export``) with the host's key table
+        and the records carried runs may still reference."""
+        self.flush()
+        return {"state": self.session.state_export(), "keys": dict(self._keys), "log": dict(self._log)}
+
+    def restore(self, snap: dict):
+        self._check()
+        if self._pending:
+            raise ProcessorFailed("restore() with buffered records")
+        self.session.state_clear()
+        self.session.state_import(snap["state"])
+        self._keys = dict(snap["keys"])
+        self._log = dict(snap["log"])
+
+    def _check(self):
+        if self._failed is not None:
+            raise ProcessorFailed(f"processor failed earlier: {self._failed}")
+        if self.session is None:
+            raise ProcessorFailed("processor not initialised (call init())")

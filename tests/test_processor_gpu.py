@@ -1,0 +1,200 @@
+"""GpuCEPProcessor (kcep/processor.py) end to end on the device.
+
+The processor is the batching equivalent of the reference's CEPProcessor
+(CEPProcessor.java:111-160): records go in one at a time with their context
+(topic, partition, offset, timestamp), values are decoded into SoA columns, and
+forwarded (key, Sequence) pairs come out.  Its forwarded stream must equal the
+reference's record for record, whatever the batch size:
+
+* the reference's own processor-mode fixtures (CEPStockDemoTest with values as
+  StockEventSerde JSON bytes, CEPStreamIntegrationTest multiple keys),
+* random interleaved streams with nulls and re-delivered offsets against the
+  oracle run over the same arrival-order stream,
+* a checkpoint/restore into a fresh processor mid-stream,
+* the reference's exception, raised after forwarding what came before it.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from kcep import Schema
+from kcep import native as N
+from kcep.ingest import StockEvent, StockEventSerde, stock_columns, scalar_column, STOCK_SCHEMA
+from kcep.processor import GpuCEPProcessor, ProcessorFailed
+from kcep.sequence import Event as Ev, sequence_from_traversal
+from golden_util import scenarios
+import patterns_lib as PL
+
+pytestmark = pytest.mark.gpu
+
+
+def seq_view(seq):
+    return [(s.getStage(), [e.offset for e in s.getEvents()]) for s in seq.matched()]
+
+
+def run_proc(proc, records, flush_every=None):
+    got = []
+    proc.init(lambda k, s: got.append((k, seq_view(s))))
+    for i, r in enumerate(records):
+        proc.process(*r)
+        if flush_every and (i + 1) % flush_every == 0:
+            proc.punctuate(0)
+    proc.close()
+    return got
+
+
+def fixture(name):
+    return [f for f in scenarios() if f["name"] == name][0]
+
+
+@pytest.mark.parametrize("batch", [1, 3, 8, 1000])
+def test_stock_demo_from_json_bytes(batch):
+    """CEPStockDemoTest.java:97-138: quotes serialized by StockEventSerde, decoded by the
+    processor's ingest path, matched on the device, forwarded as Sequences."""
+    fx = fixture("stock_demo")
+    ev = fx["events"]
+    recs = []
+    for i in range(len(ev["key"])):
+        data = StockEventSerde.serialize("stock-events", StockEvent("ALXN", ev["cols"][0][i], ev["cols"][1][i]))
+        val = StockEventSerde.deserialize("stock-events", data)
+        recs.append(("ALXN", val, "stock-events", 0, ev["offset"][i], ev["ts"][i]))
+    proc = GpuCEPProcessor("Stocks", bytes.fromhex(fx["ir"]), STOCK_SCHEMA, stock_columns(), batch_size=batch)
+    got = run_proc(proc, recs)
+    want = [("ALXN", [(g["stage"], g["events"]) for g in s]) for s in fx["expected"]["sequences"]]
+    assert got == want
+
+
+@pytest.mark.parametrize("batch", [1, 4, 100])
+def test_integration_multiple_keys(batch):
+    """CEPStreamIntegrationTest.java:117-168 through the processor."""
+    fx = fixture("integration_multiple_keys")
+    ev = fx["events"]
+    sch = Schema([("value", "i32")], topics=list(fx["topics"]))
+    ir = bytes.fromhex(fx["ir"])
+    recs = [(f"K{ev['key'][i]}", ev["cols"][0][i], "input_topic_1", 0, ev["offset"][i], ev["ts"][i])
+            for i in range(len(ev["key"]))]
+    proc = GpuCEPProcessor("Integration", ir, sch, scalar_column(sch), batch_size=batch)
+    got = run_proc(proc, recs)
+    want = [(f"K{k}", [(g["stage"], g["events"]) for g in s])
+            for k, s in zip(fx["expected"]["match_keys"], fx["expected"]["sequences"])]
+    assert got == want
+
+
+def random_records(seed, n_keys, n, vmax, null_frac=0.05, redeliver_frac=0.05):
+    """Interleaved keys, offsets increasing per partition, some nulls, some re-deliveries."""
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        k = int(rng.integers(0, n_keys))
+        v = int(rng.integers(0, vmax))
+        recs.append([f"user-{k}", v, "events", 0, i, 1000 + i])
+    for _ in range(int(n * redeliver_frac)):            # the same record delivered again later
+        i = int(rng.integers(0, n))
+        j = int(rng.integers(i + 1, len(recs) + 1))
+        recs.insert(j, list(recs[i]))
+    for i in rng.choice(len(recs), int(len(recs) * null_frac), replace=False):
+        if rng.random() < 0.5:
+            recs[i][0] = None
+        else:
+            recs[i][1] = None
+    return [tuple(r) for r in recs]
+
+
+def oracle_forward(pattern, sch, recs):
+    """The oracle over the arrival-order stream (processor mode), as (key, sequence view)."""
+    keys = {}
+    kid, val, valid, off, ts = [], [], [], [], []
+    for k, v, _t, _p, o, t in recs:
+        kid.append(keys.setdefault(k, len(keys)) if k is not None else 0)
+        val.append(0 if v is None else v)
+        valid.append(0 if (k is None or v is None) else 1)
+        off.append(o)
+        ts.append(t)
+    p = O.OraclePattern(pattern.to_ir(sch))
+    r = O.OracleRun(p, O.MODE_PROCESSOR)
+    r.process(O.BatchArrays(np.asarray(kid, np.int32), [np.asarray(val, np.int32)], [1],
+                            valid=np.asarray(valid, np.uint8), offset=np.asarray(off, np.int64),
+                            ts=np.asarray(ts, np.int64)))
+
+    def event_of(i):
+        k, v, t, pa, o, ts_ = recs[i]
+        return Ev(k, v, ts_, t, pa, o)
+    out = []
+    for m in r.matches(with_groups=False):
+        seq = sequence_from_traversal(m.traversal, p.names, event_of)
+        out.append((recs[m.record][0], seq_view(seq)))
+    return out
+
+
+@pytest.mark.parametrize("name,mk,vmax", [("any_any", PL.any_any, 4), ("next_one_or_more", PL.next_one_or_more, 4),
+                                          ("c3_stock", PL.c3_stock, 7)])
+@pytest.mark.parametrize("batch", [7, 256])
+def test_random_streams_vs_oracle(name, mk, vmax, batch):
+    recs = random_records(sum(map(ord, name)) * 31 + batch, 40, 1500, vmax)
+    if name == "c3_stock":                              # a price walk, so the averages move
+        walk = 100 + np.cumsum(np.random.default_rng(3).integers(-5, 6, len(recs)))
+        recs = [(k, None if v is None else int(walk[i]), t, p, o, ts) for i, (k, v, t, p, o, ts) in enumerate(recs)]
+    sch = Schema([("value", "i32")])
+    want = oracle_forward(mk(), sch, recs)
+    proc = GpuCEPProcessor(name, mk(), sch, scalar_column(sch), batch_size=batch)
+    got = run_proc(proc, recs)
+    assert len(want) > 0
+    assert got == want
+
+
+def test_checkpoint_restore_mid_stream():
+    """Checkpoint (cep_state_export + key table + carried records) half way, restore into a
+    fresh processor, continue: the same forwarded stream as one uninterrupted processor."""
+    recs = random_records(77, 30, 1200, 4)
+    sch = Schema([("value", "i32")])
+    whole = run_proc(GpuCEPProcessor("q", PL.next_one_or_more(), sch, scalar_column(sch), batch_size=64), recs)
+
+    got = []
+    fwd = lambda k, s: got.append((k, seq_view(s)))   # noqa: E731
+    p1 = GpuCEPProcessor("q", PL.next_one_or_more(), sch, scalar_column(sch), batch_size=64)
+    p1.init(fwd)
+    half = len(recs) // 2
+    for r in recs[:half]:
+        p1.process(*r)
+    snap = p1.checkpoint()
+    p1.close()
+    p2 = GpuCEPProcessor("q", PL.next_one_or_more(), sch, scalar_column(sch), batch_size=64)
+    p2.init(fwd)
+    p2.restore(snap)
+    for r in recs[half:]:
+        p2.process(*r)
+    p2.close()
+    assert got == whole and len(whole) > 0
+
+
+def test_reference_exception_surfaces():
+    """test_stock_demo_minimal_npe's input through the processor: the matches before the
+    failing record are forwarded, then the reference's NullPointerException is raised and
+    the processor stays failed."""
+    quotes = [(100, 1001), (102, 1001), (102, 700), (100, 500)]
+    recs = [("S", StockEvent("S", p, v), "stock-events", 0, i, i) for i, (p, v) in enumerate(quotes)]
+    got = []
+    proc = GpuCEPProcessor("Stocks", PL.stock_demo(), STOCK_SCHEMA, stock_columns(), batch_size=16)
+    proc.init(lambda k, s: got.append((k, seq_view(s))))
+    for r in recs:
+        proc.process(*r)
+    with pytest.raises(N.CepError) as ei:
+        proc.flush()
+    assert ei.value.code == 4 and ei.value.record == 3
+    want = oracle_forward_stock(quotes)
+    assert got == want
+    with pytest.raises(ProcessorFailed):
+        proc.process(*recs[0])
+
+
+def oracle_forward_stock(quotes):
+    p = O.OraclePattern(PL.stock_demo().to_ir(STOCK_SCHEMA))
+    r = O.OracleRun(p, O.MODE_PROCESSOR)
+    n = len(quotes)
+    with pytest.raises(O.OracleError) as ei:
+        r.process(O.BatchArrays(np.zeros(n, np.int32), [np.array([q[0] for q in quotes], np.int64),
+                                                         np.array([q[1] for q in quotes], np.int64)], [2, 2]))
+    return [("S", seq_view(sequence_from_traversal(m.traversal, p.names,
+                                                   lambda i: Ev("S", None, i, "stock-events", 0, i))))
+            for m in r.matches(with_groups=False) if m.record < ei.value.record]   # forward() runs after
+                                                                                 # matchPattern returns (:142-148)
