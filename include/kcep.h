@@ -174,6 +174,12 @@ int cep_session_jit(const cep_session* s);
 /* General path: the most live runs (NFA run queue length, NFAStates.java:33-37) any key held during the
    last batch -- C4's run-explosion high-water mark.  -1 if the last batch ran on another path. */
 int cep_live_run_hwm(const cep_session* s, int64_t* hwm);
+/* Every exception of the last batch, one per failing key: (stream position, CEP_E_* code), in
+   ascending position.  cep_collect reports only the earliest in the batch's key-grouped order; a
+   host that re-orders a batch by key (GpuCEPProcessor) uses this list to find the first failure in
+   arrival order, which is where the reference's process() throws (CEPProcessor.java:134-149).
+   Call with records = codes = NULL for the count.  The runs path reports its first exception only. */
+int cep_batch_errors(const cep_session* s, int64_t* records, int32_t* codes, int64_t cap, int64_t* n);
 /* CEP_SESSION_PROFILE sessions, after a general-path batch: per key segment {key id, live-run
    high-water mark, run evaluations, kernel wall clock (100 MHz ticks), then shader clocks spent in
    NFA.evaluate / edge predicates / buffer put+branch / removePattern / matchConstruction /

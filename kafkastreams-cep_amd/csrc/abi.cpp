@@ -150,6 +150,8 @@ struct cep_session {
   std::string jit_why;
   int32_t g_err = CEP_OK;
   int64_t g_err_rec = -1;
+  std::vector<int64_t> e_rec;              // every failing key's (record, code) of the last batch
+  std::vector<int32_t> e_code;
   // ---- host CSR of the last collect ----
   std::vector<int64_t> match_record, ent_off, ent_record;
   std::vector<int32_t> match_key, ent_name, out_host;
@@ -276,6 +278,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->d_key = in.key;
   s->g_err = CEP_OK;
   s->g_err_rec = -1;
+  s->e_rec.clear();
+  s->e_code.clear();
   s->g_matches = s->g_entries = 0;
   HIPCHECK(hipEventRecord(s->ev0, st));
   if (n == 0) {
@@ -321,6 +325,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     if (code == CEP_E_UNSUPPORTED) return fail(CEP_E_UNSUPPORTED, "sequence condition on the runs path");
     s->g_err = code;
     s->g_err_rec = at;
+    s->e_rec.push_back(at);                        // the runs path keeps only the first exception
+    s->e_code.push_back(code);
   }
   int bits = 31;
   while ((int64_t(1) << (bits - 31)) <= n) bits++;
@@ -370,6 +376,8 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->d_key = A.key;
   s->g_err = CEP_OK;
   s->g_err_rec = -1;
+  s->e_rec.clear();
+  s->e_code.clear();
   s->g_matches = s->g_entries = 0;
   s->nseg = 0;
   A.base = s->carry ? s->base : 0;
@@ -494,9 +502,13 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   HIPCHECK(hipMemcpyAsync(erec.data(), s->r_errrec.p, size_t(nseg) * 8, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
   for (int64_t i = 0; i < nseg; i++)
-    if (err[size_t(i)] && (s->g_err_rec < 0 || erec[size_t(i)] < s->g_err_rec)) {
-      s->g_err = err[size_t(i)];
-      s->g_err_rec = erec[size_t(i)];
+    if (err[size_t(i)]) {
+      if (s->g_err_rec < 0 || erec[size_t(i)] < s->g_err_rec) {
+        s->g_err = err[size_t(i)];
+        s->g_err_rec = erec[size_t(i)];
+      }
+      s->e_rec.push_back(erec[size_t(i)]);         // segments are in stream order, so e_rec ascends
+      s->e_code.push_back(err[size_t(i)]);
     }
   if (s->carry && s->cpool_used > s->cpool_words / 4 * 3) {   // keep room for the next batch
     if ((rc = carry_gc(s, 0, st))) return rc;
@@ -663,6 +675,18 @@ int cep_live_run_hwm(const cep_session* s, int64_t* hwm) {
   return CEP_OK;
 }
 
+int cep_batch_errors(const cep_session* s, int64_t* records, int32_t* codes, int64_t cap, int64_t* n) {
+  if (!s || !n) return fail(CEP_E_ARG, "null argument");
+  *n = int64_t(s->e_rec.size());
+  if (!records && !codes) return CEP_OK;
+  if (cap < *n) return fail(CEP_E_ARG, "capacity below the error count");
+  for (size_t i = 0; i < s->e_rec.size(); i++) {
+    if (records) records[i] = s->e_rec[i];
+    if (codes) codes[i] = s->e_code[i];
+  }
+  return CEP_OK;
+}
+
 int cep_key_profile(cep_session* s, int64_t* out, int64_t cap, int64_t* n_keys) {
   if (!s || !n_keys) return fail(CEP_E_ARG, "null argument");
   if (!(s->opts.flags & CEP_SESSION_PROFILE) || s->last_path != CEP_PATH_GENERAL)
@@ -725,6 +749,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   s->stream = st;
   s->n = b->n;
   s->pending = true;
+  s->e_rec.clear();
+  s->e_code.clear();
   HIPCHECK(hipEventRecord(s->eb0, st));
   // records the processor would drop (null key/value, re-delivered offsets)
   // break contiguity: the stencil only takes batches without them

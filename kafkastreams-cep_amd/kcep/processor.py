@@ -31,7 +31,9 @@ registers) plays the role of the reference's three stores.
   exceptions, ``UnknownAggregateException``, the buffer's ``IllegalStateException``)
   the flush forwards the matches of the records that arrived before the failing
   one and raises ``CepError``; the processor is then failed, as the reference's
-  stream task is.
+  stream task is.  The device reports every failing key of the batch
+  (``cep_batch_errors``), so the failure picked is the first in arrival order,
+  where the reference's ``process()`` throws.
 * **Query name** normalisation copies ``:83``: ``toLowerCase()`` then
   ``String.replace("\\\\s+", "")``, which is a *literal* replace in Java (no regex).
 """
@@ -137,9 +139,12 @@ class GpuCEPProcessor:
         mrec = out["match_record"] - base                 # stream position -> batch position
         m_arrival = perm[mrec] if len(mrec) else np.zeros(0, np.int64)
         order = np.argsort(m_arrival, kind="stable")
-        limit = None
-        if out["err"]:
-            limit = int(perm[int(out["err_record"]) - base])
+        limit = err_code = None
+        if out["err"]:                                    # the first failure in ARRIVAL order (cep_batch_errors)
+            erec, ecode = self.session.batch_errors()
+            arr = perm[erec - base]
+            j = int(np.argmin(arr))
+            limit, err_code = int(arr[j]), int(ecode[j])
         names = self.compiled.names
         sent = 0
         for m in order:
@@ -151,7 +156,7 @@ class GpuCEPProcessor:
             self._forward(recs[m_arrival[m]][6].key, seq)
             sent += 1
         if out["err"]:
-            self._failed = N.CepError(int(out["err"]), out.get("msg") or N.lib().cep_last_error().decode(), limit)
+            self._failed = N.CepError(err_code, N.ERRORS.get(err_code, "exception") + " in process()", limit)
             raise self._failed
         return sent
 

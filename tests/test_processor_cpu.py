@@ -70,10 +70,14 @@ class StubSession:
         self.pushes.append(dict(key=key.copy(), val=cols[0].copy(), offset=offset.copy(), topic=topic.copy()))
         rec, ents = [], []
         err, err_rec = 0, -1
+        self.errs, seen = [], set()
         for i in range(n):
             v = int(cols[0][i])
-            if v == self.err_value and err == 0:
-                err, err_rec = 4, self.pos + i
+            if v == self.err_value and int(key[i]) not in seen:   # a key stops at its first exception
+                seen.add(int(key[i]))
+                self.errs.append(self.pos + i)
+                if err == 0:
+                    err, err_rec = 4, self.pos + i
             if v in self.complete:
                 rec.append(self.pos + i)
                 ents.append([(0, self.pos + i)])
@@ -86,6 +90,9 @@ class StubSession:
 
     def collect(self, raise_on_error=True):
         return self.out
+
+    def batch_errors(self):
+        return np.asarray(self.errs, np.int64), np.full(len(self.errs), 4, np.int32)
 
     def close(self):
         self.closed = True
@@ -129,3 +136,17 @@ def test_processor_error_truncates_and_fails():
     assert got == [("a", [("$final", [0])])]              # only what arrived before it
     with pytest.raises(ProcessorFailed):
         p.process("a", 1, "events", 0, 9, 9)
+
+
+def test_processor_error_is_first_in_arrival_order():
+    """Two keys fail in one batch; the key-grouped batch puts the later-arriving failure first.
+    The processor must fail where the reference does: at the earliest arrival."""
+    stub = StubSession(complete={7}, err_value=9)
+    p, got = make(100, stub)
+    for k, v, o in [("a", 7, 0), ("b", 9, 1), ("a", 9, 2), ("a", 7, 3)]:
+        p.process(k, v, "events", 0, o, o)
+    with pytest.raises(N.CepError) as ei:
+        p.flush()
+    assert stub.out["err_record"] == 1                  # grouped order: a0 a2 a3 b1 -> a2 reported first
+    assert ei.value.record == 1 and ei.value.code == 4  # but b1 arrived first
+    assert got == [("a", [("$final", [0])])]

@@ -198,3 +198,34 @@ def oracle_forward_stock(quotes):
                                                    lambda i: Ev("S", None, i, "stock-events", 0, i))))
             for m in r.matches(with_groups=False) if m.record < ei.value.record]   # forward() runs after
                                                                                  # matchPattern returns (:142-148)
+
+
+@pytest.mark.parametrize("seed", [11, 17, 28])
+def test_stock_demo_random_keys_fail_where_the_reference_fails(seed):
+    """The example pattern on random interleaved quotes of 200 keys throws inside the
+    reference (test_stock_demo_random); several keys fail within one batch.  The processor
+    must forward exactly what the reference forwarded before its first exception in
+    arrival order, and raise that exception at that record."""
+    rng = np.random.default_rng(seed)
+    n = 5000
+    kid = rng.integers(0, 200, n).astype(np.int32)
+    price = (120 + rng.integers(-6, 7, n)).astype(np.int64)
+    vol = rng.integers(600, 1200, n).astype(np.int64)
+    p = O.OraclePattern(PL.stock_demo().to_ir(STOCK_SCHEMA))
+    r = O.OracleRun(p, O.MODE_PROCESSOR)
+    with pytest.raises(O.OracleError) as oe:
+        r.process(O.BatchArrays(kid, [price, vol], [2, 2]))
+    recs = [(f"S{kid[i]}", StockEvent(f"S{kid[i]}", int(price[i]), int(vol[i])), "stock-events", 0, i, i)
+            for i in range(n)]
+    want = [(recs[m.record][0], seq_view(sequence_from_traversal(
+        m.traversal, p.names, lambda i: Ev(recs[i][0], recs[i][1], i, "stock-events", 0, i))))
+        for m in r.matches(with_groups=False) if m.record < oe.value.record]
+    got = []
+    proc = GpuCEPProcessor("Stocks", PL.stock_demo(), STOCK_SCHEMA, stock_columns(), batch_size=n)
+    proc.init(lambda k, s: got.append((k, seq_view(s))))
+    with pytest.raises(N.CepError) as ge:
+        for rr in recs:
+            proc.process(*rr)
+    assert (ge.value.code, ge.value.record) == (oe.value.code, oe.value.record)
+    assert len(proc.session.batch_errors()[0]) > 1        # several keys failed in the batch
+    assert got == want and len(want) > 0
