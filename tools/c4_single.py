@@ -1,7 +1,7 @@
 """Is the C4 general-path kernel bound by one key's serial chain, or by contention?
 
 Profiles the full C4 batch, then re-runs only the heaviest keys (by run evaluations) on an
-otherwise idle GPU and prints their kernel time.  Usage (GPU box): python tools/c4_single.py"""
+otherwise idle GPU and prints their kernel time.  Usage (GPU box): python tools/c4_single.py [--top1]"""
 import os
 import sys
 
@@ -32,7 +32,7 @@ prof = s.key_profile()
 ev = prof[:, 2]
 print(f"full batch: kernel {ms:.2f} ms, max evals {ev.max()}, live hwm {s.live_run_hwm()}", flush=True)
 order = np.argsort(-ev)
-for top in (1, 8, 64, 1024):
+for top in ((1,) if "--top1" in sys.argv else (1, 8, 64, 1024)):
     ks = np.sort(prof[order[:top], 0])
     idx = torch.as_tensor((ks[:, None] * L + np.arange(L)[None, :]).reshape(-1), device="cuda")
     k2, v2, t2 = key[idx].contiguous(), val[idx].contiguous(), ts[idx].contiguous()
