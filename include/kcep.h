@@ -174,6 +174,10 @@ int cep_session_jit(const cep_session* s);
 /* General path: the most live runs (NFA run queue length, NFAStates.java:33-37) any key held during the
    last batch -- C4's run-explosion high-water mark.  -1 if the last batch ran on another path. */
 int cep_live_run_hwm(const cep_session* s, int64_t* hwm);
+/* Per-batch HIP event timing (cep_last_kernel_ms / cep_last_batch_ms), on by default.  Off, the
+   stencil and chain paths put no event packets into the stream; the two timing calls then fail
+   with CEP_E_UNSUPPORTED.  A serving host that does not read the timings turns it off. */
+int cep_session_set_timing(cep_session* s, int on);
 /* Every exception of the last batch, one per failing key: (stream position, CEP_E_* code), in
    ascending position.  cep_collect reports only the earliest in the batch's key-grouped order; a
    host that re-orders a batch by key (GpuCEPProcessor) uses this list to find the first failure in

@@ -121,6 +121,7 @@ struct cep_session {
   int64_t n = 0;
   bool pending = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, eb0 = nullptr, eb1 = nullptr;
+  bool timing = true;                      // cep_session_set_timing: stencil/chain batches record events
   // ---- stencil workspace ----
   DBuf prog, out, status, counter, total, sum, mkey, slots;   // status: tile counts + prefixes; counter: scan scratch
   int64_t out_cap = 0;
@@ -191,8 +192,8 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic, SP.chain,
                   s->slots.as<int32_t>(), tc, tc + ntiles + 1, s->counter.as<int64_t>(), s->out.as<int32_t>(),
                   s->out_cap, s->total.as<int64_t>()};
-  HIPCHECK(stencil_launch(L, s->ev0, s->ev1, st));
-  HIPCHECK(hipEventRecord(s->eb1, st));
+  HIPCHECK(stencil_launch(L, s->timing ? s->ev0 : nullptr, s->timing ? s->ev1 : nullptr, st));
+  if (s->timing) HIPCHECK(hipEventRecord(s->eb1, st));
   return CEP_OK;
 }
 
@@ -751,7 +752,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   s->pending = true;
   s->e_rec.clear();
   s->e_code.clear();
-  HIPCHECK(hipEventRecord(s->eb0, st));
+  if (s->timing) HIPCHECK(hipEventRecord(s->eb0, st));
   // records the processor would drop (null key/value, re-delivered offsets)
   // break contiguity: the stencil only takes batches without them
   const bool stencil_batch = !b->valid && !(s->opts.mode == CEP_MODE_PROCESSOR && b->offset &&
@@ -772,8 +773,15 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
 
 const int64_t* cep_device_match_count(const cep_session* s) { return s ? s->total.as<int64_t>() : nullptr; }
 
+int cep_session_set_timing(cep_session* s, int on) {
+  if (!s) return fail(CEP_E_ARG, "null argument");
+  s->timing = on != 0;
+  return CEP_OK;
+}
+
 int cep_last_kernel_ms(cep_session* s, float* ms) {
   if (!s || !ms) return fail(CEP_E_ARG, "null argument");
+  if (!s->timing) return fail(CEP_E_UNSUPPORTED, "timing is off (cep_session_set_timing)");
   HIPCHECK(hipEventSynchronize(s->ev1));
   HIPCHECK(hipEventElapsedTime(ms, s->ev0, s->ev1));
   return CEP_OK;
@@ -781,6 +789,7 @@ int cep_last_kernel_ms(cep_session* s, float* ms) {
 
 int cep_last_batch_ms(cep_session* s, float* ms) {
   if (!s || !ms) return fail(CEP_E_ARG, "null argument");
+  if (!s->timing) return fail(CEP_E_UNSUPPORTED, "timing is off (cep_session_set_timing)");
   HIPCHECK(hipEventSynchronize(s->eb1));
   HIPCHECK(hipEventElapsedTime(ms, s->eb0, s->eb1));
   return CEP_OK;

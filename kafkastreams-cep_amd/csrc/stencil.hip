@@ -540,16 +540,17 @@ static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
 // stencil_kernel (timed as the dominant kernel between ev0 and ev1), then the
 // tile-count scan and the gather into the contiguous output
 hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
+  // null events: timing off (cep_session_set_timing), no event packets in the stream
   if (L.n <= 0) {
-    hipError_t e = hipEventRecord(ev0, st);
-    if (e == hipSuccess) e = hipEventRecord(ev1, st);
+    hipError_t e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
+    if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
     return e == hipSuccess ? hipMemsetAsync(L.total, 0, sizeof(int64_t), st) : e;
   }
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
   const int64_t nsuper = (ntiles + ST_SUB - 1) / ST_SUB;
-  hipError_t e = hipEventRecord(ev0, st);
+  hipError_t e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
   if (e == hipSuccess) e = stencil_count(L, st);
-  if (e == hipSuccess) e = hipEventRecord(ev1, st);
+  if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total);
   hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre, L.k,

@@ -68,7 +68,7 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version",
            "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position",
            "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels", "cep_live_run_hwm",
-           "cep_batch_errors",
+           "cep_batch_errors", "cep_session_set_timing",
            "cep_key_profile"]
 
 _lib = None
@@ -118,6 +118,7 @@ def lib():
     L.cep_stream_position.restype = C.c_int64
     L.cep_session_jit.argtypes = [P]
     L.cep_live_run_hwm.argtypes = [P, C.POINTER(C.c_int64)]
+    L.cep_session_set_timing.argtypes = [P, C.c_int32]
     L.cep_batch_errors.argtypes = [P, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
     L.cep_key_profile.argtypes = [P, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
     L.cep_pattern_kernel_source.argtypes = [P, C.c_int32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
@@ -261,6 +262,10 @@ class Session:
         v = C.c_int64()
         check(lib().cep_live_run_hwm(self.h, C.byref(v)))
         return v.value
+
+    def set_timing(self, on: bool):
+        """cep_session_set_timing: per-batch HIP event timing on/off."""
+        check(lib().cep_session_set_timing(self.h, 1 if on else 0))
 
     def batch_errors(self):
         """Every failing key's (stream position, code) of the last batch, ascending (cep_batch_errors)."""
