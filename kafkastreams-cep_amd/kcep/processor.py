@@ -53,12 +53,38 @@ class ProcessorFailed(RuntimeError):
     pass
 
 
+# carry blob layout (csrc/kcep_dev.h CB_*, nfa_dev.h export_state): per key a header of CB_HDR
+# words, then 3 words per high-water mark, 4 per queued run, then the carried events, each
+# carry_evw(ncols) = 8 + 2*ncols words starting with its stream position (int64)
+_CB_HDR, _CB_NHWM, _CB_QLEN, _CB_NEV, _CB_NCOLS = 12, 3, 4, 5, 10
+
+
+def carried_positions(blob: bytes) -> set:
+    """Stream positions of every event a ``cep_state_export`` blob carries."""
+    hdr = np.frombuffer(blob, np.int32, 5, 0)
+    nkeys = int(hdr[4])
+    out = set()
+    at = 20
+    for _ in range(nkeys):
+        w = int(np.frombuffer(blob, np.int32, 1, at + 4)[0])
+        words = np.frombuffer(blob, np.int32, w, at + 8)
+        nev = int(words[_CB_NEV])
+        if nev:
+            evw = 8 + 2 * int(words[_CB_NCOLS])
+            e0 = _CB_HDR + 3 * int(words[_CB_NHWM]) + 4 * int(words[_CB_QLEN])
+            ev = words[e0:e0 + nev * evw].reshape(nev, evw)
+            pos = ev[:, 0].astype(np.uint32).astype(np.int64) | (ev[:, 1].astype(np.int64) << 32)
+            out.update(int(x) for x in pos)
+        at += 8 + 4 * w
+    return out
+
+
 class GpuCEPProcessor:
     """One stream task's processor for one query (``CEPProcessor`` equivalent)."""
 
     def __init__(self, queryName: str, pattern: Union[Pattern, bytes], schema: Schema, decoder: ColumnDecoder,
                  batch_size: int = 1 << 16, max_keys: int = 1 << 20, device: int = 0,
-                 mode: int = N.MODE_PROCESSOR):
+                 mode: int = N.MODE_PROCESSOR, prune_at: int = 1 << 20):
         if decoder.schema is not schema and decoder.schema.columns != schema.columns:
             raise ValueError("decoder and pattern use different schemas")
         self.queryName = queryName.lower().replace("\\s+", "")
@@ -76,6 +102,8 @@ class GpuCEPProcessor:
         self._pending: List[Tuple[int, tuple, int, int, int, int, Event]] = []
         self._log: Dict[int, Event] = {}          # stream position -> Event (carried runs point back here)
         self._failed: Optional[Exception] = None
+        self._prune_at = max(int(prune_at), 2 * self.batch_size)   # _log size that triggers a prune
+        self._prune_min = self._prune_at
 
     # ---- Processor API (CEPProcessor.init/process/punctuate/close, :88-170) ----
     def init(self, forward: Callable[[Any, Sequence], None], session=None):
@@ -155,10 +183,20 @@ class GpuCEPProcessor:
             seq = sequence_from_traversal(ents, names, self._log.__getitem__)
             self._forward(recs[m_arrival[m]][6].key, seq)
             sent += 1
+        if not out["err"] and len(self._log) >= self._prune_at:
+            self._prune()
         if out["err"]:
             self._failed = N.CepError(err_code, N.ERRORS.get(err_code, "exception") + " in process()", limit)
             raise self._failed
         return sent
+
+    def _prune(self):
+        """Drop the records no live run can reach any more: the device's carried state lists, per
+        key, the events its runs and buffer nodes still reference (``cep_state_export``), each with
+        its stream position.  Runs only when the log has doubled since the last prune."""
+        keep = carried_positions(self.session.state_export())
+        self._log = {p: ev for p, ev in self._log.items() if p in keep}
+        self._prune_at = max(self._prune_min, 2 * len(self._log))
 
     # ---- checkpoint / restore (the NFAStore / buffer / aggregates stores) ----
     def checkpoint(self) -> dict:

@@ -150,3 +150,28 @@ def test_processor_error_is_first_in_arrival_order():
     assert stub.out["err_record"] == 1                  # grouped order: a0 a2 a3 b1 -> a2 reported first
     assert ei.value.record == 1 and ei.value.code == 4  # but b1 arrived first
     assert got == [("a", [("$final", [0])])]
+
+
+def test_carried_positions_parses_export_blob():
+    """kcep.processor.carried_positions on a hand-built cep_state_export blob: two keys, the
+    first with 1 high-water mark, 2 queued runs and 2 carried events of 1 column."""
+    from kcep.processor import carried_positions
+    import struct
+
+    def key_words(nhwm, qlen, positions, ncols=1):
+        evw = 8 + 2 * ncols
+        hdr = [0] * 12
+        hdr[3], hdr[4], hdr[5], hdr[10] = nhwm, qlen, len(positions), ncols
+        body = [7] * (3 * nhwm + 4 * qlen)
+        for p in positions:
+            ev = [0] * evw
+            ev[0], ev[1] = p & 0xFFFFFFFF, p >> 32
+            body += ev
+        w = hdr + body
+        w[0] = len(w)
+        return w
+
+    blob = struct.pack("<IIqi", 0x4B434550, 1, 0, 2)
+    for k, ws in ((3, key_words(1, 2, [5, (1 << 33) + 9])), (8, key_words(0, 0, []))):
+        blob += struct.pack("<ii", k, len(ws)) + struct.pack(f"<{len(ws)}I", *ws)
+    assert carried_positions(blob) == {5, (1 << 33) + 9}

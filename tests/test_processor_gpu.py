@@ -229,3 +229,21 @@ def test_stock_demo_random_keys_fail_where_the_reference_fails(seed):
     assert (ge.value.code, ge.value.record) == (oe.value.code, oe.value.record)
     assert len(proc.session.batch_errors()[0]) > 1        # several keys failed in the batch
     assert got == want and len(want) > 0
+
+
+def test_record_log_is_pruned_to_carried_events():
+    """The host keeps a record only while a carried run can still reach it (positions listed in
+    the exported state); pruning must not change the forwarded stream."""
+    recs = random_records(99, 25, 3000, 4, null_frac=0.0, redeliver_frac=0.0)
+    sch = Schema([("value", "i32")])
+    want = oracle_forward(PL.next_one_or_more(), sch, recs)
+    proc = GpuCEPProcessor("q", PL.next_one_or_more(), sch, scalar_column(sch), batch_size=32, prune_at=64)
+    got = []
+    proc.init(lambda k, s: got.append((k, seq_view(s))))
+    peak = 0
+    for r in recs:
+        proc.process(*r)
+        peak = max(peak, len(proc._log))
+    proc.close()
+    assert got == want and len(want) > 0
+    assert peak < 600                                     # without pruning it would reach 3000
