@@ -49,6 +49,7 @@ def parse(argv=None):
     ap.add_argument("--keys", type=int, default=None, help="keys per GPU")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-input", action="store_true", help="skip the PCIe-inclusive (host buffer) figure")
     return ap.parse_args(argv)
 
 
@@ -191,12 +192,38 @@ def main():
         if sess.path == N.PATH_GENERAL:
             line["config"]["live_run_hwm"] = sess.live_run_hwm()     # run-explosion high-water mark
             line["config"]["keys_on_cpu"] = 0                        # no CPU fallback: every key runs on the GPU
+        if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and not args.no_host_input:
+            line["pcie_inclusive"] = _pcie_inclusive(sess, n, key, cols, stream, csum)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = _cpu_baseline(args.config, key, cols, ts, ir, args.cpu_threads, n_matches, csum,
                                                  sess, stream)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _pcie_inclusive(sess, n, key, cols, stream, csum, steps=3):
+    """The same batch handed over in (pinned) host memory, as the JNI boundary would: each push
+    stages the columns over PCIe before the kernels.  Reported beside `value`, never as it."""
+    from kcep import native as N
+    hk = key.cpu().pin_memory()
+    hc = [c.cpu().pin_memory() for c in cols]
+    sess.set_timing(False)
+
+    def push():
+        sess.push(n, hk.data_ptr(), [c.data_ptr() for c in hc], mem=N.MEM_HOST, stream=stream.cuda_stream)
+    push()
+    stream.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        push()
+    stream.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    sess.set_timing(True)
+    _, c2 = sess.checksum()
+    return {"value": n / dt, "unit": "events/s", "ms_per_step": dt * 1e3, "host_memory": "pinned",
+            "bytes_per_step": int(hk.numel() * hk.element_size() + sum(c.numel() * c.element_size() for c in hc)),
+            "parity": c2 == csum}
 
 
 def _pmc_traffic(cfg, n):
