@@ -19,7 +19,7 @@ import pytest
 import oracle as O
 from kcep import Schema
 from kcep import native as N
-from kcep.ingest import StockEvent, StockEventSerde, stock_columns, scalar_column, STOCK_SCHEMA
+from kcep.ingest import StockEvent, StockEventSerde, ColumnDecoder, stock_columns, scalar_column, STOCK_SCHEMA
 from kcep.processor import GpuCEPProcessor, ProcessorFailed
 from kcep.sequence import Event as Ev, sequence_from_traversal
 from golden_util import scenarios
@@ -247,3 +247,34 @@ def test_record_log_is_pruned_to_carried_events():
     proc.close()
     assert got == want and len(want) > 0
     assert peak < 600                                     # without pruning it would reach 3000
+
+
+PROC_FIXTURES = ["proc_high_water_mark", "proc_null_key_value", "integration_multiple_keys",
+                 "integration_multiple_topics", "readme_letters", "stock_demo"]
+
+
+@pytest.mark.parametrize("batch", [1, 100])
+@pytest.mark.parametrize("name", PROC_FIXTURES)
+def test_every_processor_fixture(name, batch):
+    """Every processor-mode golden fixture (CEPProcessorTest, CEPStreamIntegrationTest, README,
+    CEPStockDemoTest) through GpuCEPProcessor, records carrying their topic names; sequences
+    compared as (stage, [(topic, offset)]) since offsets repeat across topics."""
+    fx = fixture(name)
+    ev = fx["events"]
+    tname = {v: k for k, v in fx["topics"].items()}
+    sch = Schema([(c, {1: "i32", 2: "i64", 3: "f64"}[t]) for c, t in fx["columns"]], topics=list(fx["topics"]))
+    dec = ColumnDecoder(sch, [lambda v, i=i: v[i] for i in range(len(fx["columns"]))])
+    n = len(ev["key"])
+    valid = ev.get("valid", [1] * n)
+    recs = [(f"k{ev['key'][i]}", tuple(c[i] for c in ev["cols"]) if valid[i] else None, tname[ev["topic"][i]],
+             ev["partition"][i], ev["offset"][i], ev["ts"][i]) for i in range(n)]
+    got = []
+    proc = GpuCEPProcessor(name, bytes.fromhex(fx["ir"]), sch, dec, batch_size=batch)
+    proc.init(lambda k, s: got.append([(g.getStage(), [(e.topic, e.offset) for e in g.getEvents()])
+                                       for g in s.matched()]))
+    for r in recs:
+        proc.process(*r)
+    proc.close()
+    want = [[(g["stage"], [(tname[ev["topic"][i]], ev["offset"][i]) for i in g["events"]]) for g in s]
+            for s in fx["expected"]["sequences"]]
+    assert got == want
