@@ -488,12 +488,19 @@ __global__ __launch_bounds__(1024) void tile_scan(const int64_t* __restrict__ cn
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t per = (nt + 1023) / 1024, a = tid * per, b = a + per < nt ? a + per : nt;
   int64_t sum = 0;
-  for (int64_t c = a; c < b; c += 8) {
-    int64_t v[8];
+  int64_t r8[8];                                  // per <= 8 (<= 8192 super-tiles): one pass over global memory
+  const bool one_pass = per <= 8;
+  if (one_pass) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = c + i < b ? cnt[c + i] : 0;
+    for (int i = 0; i < 8; i++) { r8[i] = a + i < b ? cnt[a + i] : 0; sum += r8[i]; }
+  } else {
+    for (int64_t c = a; c < b; c += 8) {
+      int64_t v[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) sum += v[i];
+      for (int i = 0; i < 8; i++) v[i] = c + i < b ? cnt[c + i] : 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) sum += v[i];
+    }
   }
   int64_t incl = sum;
 #pragma unroll
@@ -505,14 +512,20 @@ __global__ __launch_bounds__(1024) void tile_scan(const int64_t* __restrict__ cn
   __syncthreads();
   int64_t run = incl - sum;
   for (int w = 0; w < wid; w++) run += s_w[w];
-  for (int64_t c = a; c < b; c += 8) {
-    int64_t v[8];
+  if (one_pass) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = c + i < b ? cnt[c + i] : 0;
+    for (int i = 0; i < 8; i++)
+      if (a + i < b) { pre[a + i] = run; run += r8[i]; }
+  } else {
+    for (int64_t c = a; c < b; c += 8) {
+      int64_t v[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if (c + i < b) pre[c + i] = run;
-      run += v[i];
+      for (int i = 0; i < 8; i++) v[i] = c + i < b ? cnt[c + i] : 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        if (c + i < b) pre[c + i] = run;
+        run += v[i];
+      }
     }
   }
   if (tid == 1023) *total = run;
