@@ -187,22 +187,29 @@ struct ChainWin {
   uint32_t same;      // record w has the key of record w-1
 };
 
+// bit i of each of the 8 bytes of m -> 8 contiguous bits (byte b -> bit b): the
+// byte-LSB gather by one multiply (0x0102040810204080 lands byte b's bit at 56+b;
+// the cross terms stay below bit 56 or overflow past 63)
+__device__ __forceinline__ uint32_t byte_bits(uint64_t m, int i) {
+  return uint32_t((((m >> i) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+}
+
 template <int K>
-__device__ __forceinline__ ChainWin<K> chain_window(const int32_t (&wk)[24], const uint8_t (&wm)[24], uint32_t opt) {
+__device__ __forceinline__ ChainWin<K> chain_window(const int32_t (&wk)[24], const uint64_t (&m8)[3], uint32_t opt) {
   ChainWin<K> c;
 #pragma unroll
   for (int i = 0; i < K; i++) { c.b[i] = 0; c.s[i] = 0; }
   c.same = 0;
 #pragma unroll
-  for (int w = 0; w < 24; w++) {
-    const uint32_t m = wm[w];
+  for (int q = 0; q < 3; q++) {
 #pragma unroll
     for (int i = 0; i < K; i++) {
-      c.b[i] |= ((m >> i) & 1u) << w;
-      c.s[i] |= ((m >> (CHAIN_MAX_K + i)) & 1u) << w;
+      c.b[i] |= byte_bits(m8[q], i) << (8 * q);
+      c.s[i] |= byte_bits(m8[q], CHAIN_MAX_K + i) << (8 * q);
     }
-    if (w) c.same |= uint32_t(wk[w] == wk[w - 1]) << w;
   }
+#pragma unroll
+  for (int w = 1; w < 24; w++) c.same |= uint32_t(wk[w] == wk[w - 1]) << w;
 #pragma unroll
   for (int i = 0; i < K; i++)
     if (!((opt >> i) & 1)) c.s[i] = 0;
@@ -316,6 +323,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
       const int lb = ST_EPT * tid + 8;            // 16 records of this thread + 8 of history
       int32_t wk[24];
       uint8_t wm[24];
+      uint64_t m8s[3];
 #pragma unroll
       for (int q = 0; q < 6; q++) {
         const v4i k4 = *reinterpret_cast<const v4i*>(&s_key[kpos(lb + 4 * q)]);
@@ -324,13 +332,14 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 #pragma unroll
       for (int q = 0; q < 3; q++) {
         const uint64_t m8 = *reinterpret_cast<const uint64_t*>(&s_mask[lb + 8 * q]);
+        m8s[q] = m8;
 #pragma unroll
         for (int b = 0; b < 8; b++) wm[8 * q + b] = uint8_t(m8 >> (8 * b));
       }
       uint32_t hit = 0;
       int cnt = 0;
       if constexpr (CHAIN) {
-        const ChainWin<K> cw = chain_window<K>(wk, wm, opt);
+        const ChainWin<K> cw = chain_window<K>(wk, m8s, opt);
         ChainEnds<K> ce;
         ce.run(cw, 0, 0, nullptr);
 #pragma unroll
