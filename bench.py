@@ -47,7 +47,8 @@ def parse(argv=None):
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--events", type=int, default=None, help="events per GPU (c2)")
     ap.add_argument("--keys", type=int, default=None, help="keys per GPU")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle threads for cpu_baseline (default: nproc, every CPU this process may run on)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-input", action="store_true", help="skip the PCIe-inclusive (host buffer) figure")
     return ap.parse_args(argv)
@@ -126,7 +127,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    kernel_ms = []
+    kernel_ms, batch_ms = [], []
     if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
         sess.set_timing(False)        # no event packets in the timed steps; kernel time is a separate pass
     t0 = time.perf_counter()
@@ -134,6 +135,7 @@ def main():
         step()
         if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):   # these pushes sync internally; read the kernel time
             kernel_ms.append(sess.last_kernel_ms())
+            batch_ms.append(sess.last_batch_ms())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -159,7 +161,15 @@ def main():
             n_ent = len(out["ent_record"])
             # 8 B/event in (key + i32 value); CSR out: 20 B/match + 12 B/entry
             algo_bytes = 8.0 * n + 20.0 * n_matches + 12.0 * n_ent
-        achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
+            roof_ms, roof_kernel = avg_kernel_ms, "stencil_kernel"
+        else:
+            # these paths write their CSR in later launches (runs_write / nfa_compact), so the bytes
+            # are divided by the whole step's device time (HIP events around cep_push_batch)
+            roof_ms = sum(batch_ms) / len(batch_ms)
+            roof_kernel = "whole cep_push_batch (" + ("runs_sim + sort + runs_write" if sess.path == N.PATH_RUNS
+                                                       else "nfa_kernel + compaction") + ")"
+        achieved = algo_bytes / (roof_ms * 1e-3) / 1e9
         value = tot_events * args.steps / t_max
         line = {
             "metric": METRIC if args.config == "c2" else f"events/sec (whole node), {C['desc']}",
@@ -181,14 +191,15 @@ def main():
                        "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
-                         "kernel": {N.PATH_GENERAL: "kcep_nfa_kernel" if sess.jit else "nfa_kernel",
-                                    N.PATH_RUNS: "kcep_runs_sim" if sess.jit else "runs_sim"}.get(sess.path, "stencil_kernel"),
-                         "kernel_ms": avg_kernel_ms, "algo_bytes_per_launch": algo_bytes},
+                         "kernel": roof_kernel, "kernel_ms": roof_ms, "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",
         }
         if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):
-            line["batch_ms"] = sess.last_batch_ms()
+            line["batch_ms"] = roof_ms
+            line["first_kernel"] = {"name": {N.PATH_GENERAL: "kcep_nfa_kernel" if sess.jit else "nfa_kernel",
+                                             N.PATH_RUNS: "kcep_runs_sim" if sess.jit else "runs_sim"}[sess.path],
+                                    "ms": avg_kernel_ms}
         if sess.path == N.PATH_GENERAL:
             line["config"]["live_run_hwm"] = sess.live_run_hwm()     # run-explosion high-water mark
             line["config"]["keys_on_cpu"] = 0                        # no CPU fallback: every key runs on the GPU
@@ -240,6 +251,38 @@ def _pmc_traffic(cfg, n):
         return None
 
 
+def host_cpu():
+    """The host the CPU baseline runs on: CPU model, logical CPUs, physical cores (distinct
+    (package, core) pairs of /proc/cpuinfo), the CPUs this process may run on (nproc) and the
+    cgroup CPU quota, if any (a GPU box may grant a share of a larger machine)."""
+    model, phys, cur = None, set(), {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k in ("physical id", "core id"):
+                    cur[k] = v
+                elif not k and cur:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count(), "physical_cores": len(phys) or None,
+            "nproc": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota}
+
+
 def _cpu_baseline(cfg, key, cols, ts, ir, threads, gpu_matches, gpu_csum, sess, stream):
     """The oracle (C restatement of the reference NFA) on the host cores.
 
@@ -254,7 +297,8 @@ def _cpu_baseline(cfg, key, cols, ts, ir, threads, gpu_matches, gpu_csum, sess, 
     hc = [c.cpu().numpy() for c in cols]
     ho = ts.cpu().numpy()
     p = O.OraclePattern(ir)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    cpu = host_cpu()
+    threads = max(1, threads or cpu["nproc"])
 
     def prefix(m):
         m = min(len(hk), m)
@@ -280,7 +324,9 @@ def _cpu_baseline(cfg, key, cols, ts, ir, threads, gpu_matches, gpu_csum, sess, 
     dt1 = time.perf_counter() - t1
     return {"value": m_all / dt, "unit": "events/s", "cores": threads, "kind": "port",
             "sample": f"{'full workload' if cfg == 'c2' else 'whole-key prefix'} ({m_all} events) on {threads} "
-                      f"threads; 1-core figure on a {m1}-event whole-key prefix",
+                      f"threads (key-sharded, one per CPU of nproc); 1-core figure on a {m1}-event whole-key "
+                      f"prefix",
+            "model": cpu["model"], "host": cpu, "seconds": dt,
             "value_1core": m1 / dt1, "parity": bool(nm == gpu_matches and cs == gpu_csum),
             "oracle_matches": int(nm)}
 

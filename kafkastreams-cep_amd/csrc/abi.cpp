@@ -42,6 +42,9 @@ hipError_t nfa_compact_launch(int64_t nseg, const int32_t* key, const int64_t* s
                               int64_t* ent_record, hipStream_t st);
 hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_carry,
                                const int32_t* res_err, int64_t* ctab, hipStream_t st);
+hipError_t carry_keycheck_launch(int64_t max_seg, const int64_t* nseg, const int32_t* key, const int64_t* seg_start,
+                                int32_t max_keys, int32_t* stamp, int32_t batch_no, unsigned long long* flags,
+                                hipStream_t st);
 hipError_t carry_sizes_launch(const int64_t* ctab, int64_t nkeys, const int32_t* cpool, int64_t* words,
                               hipStream_t st);
 hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st, hipFunction_t jf);
@@ -138,6 +141,8 @@ struct cep_session {
   bool carry = false;
   int64_t base = 0;             // stream position of the next batch's record 0
   DBuf ctab, cpool;             // per key id: blob offset (-1 none); blobs (int32 words)
+  DBuf kstamp;                  // per key id: number of the last batch that had a segment of it
+  int32_t batch_no = 0;
   int64_t cpool_words = 0, cpool_used = 0;
   // ---- deterministic runs workspace ----
   DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof;
@@ -396,8 +401,18 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   int64_t* scal = s->scal.as<int64_t>();
   HIPCHECK(nfa_segments(A.key, n, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
                         s->scan_tmp.as<int64_t>(), st));
-  const int64_t nseg = read_i64(scal, st, &rc);
-  if (rc) return fail(rc, "segment count");
+  int64_t segs[2] = {0, 0};                       // segment count, carry key-check flags
+  if (s->carry) {
+    HIPCHECK(hipMemsetAsync(scal + 1, 0, 8, st));
+    HIPCHECK(carry_keycheck_launch(n, scal, A.key, s->seg.as<int64_t>(), int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
+                                   s->kstamp.as<int32_t>(), ++s->batch_no, reinterpret_cast<unsigned long long*>(scal + 1),
+                                   st));
+  }
+  HIPCHECK(hipMemcpyAsync(segs, scal, sizeof segs, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const int64_t nseg = segs[0];
+  if (segs[1] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+  if (segs[1] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
   if (nseg >= (int64_t(1) << 31)) return fail(CEP_E_ARG, "too many keys in one batch");
   s->nseg = nseg;
   A.nseg = int32_t(nseg);
@@ -635,7 +650,8 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
     s->carry = true;
     s->cpool_words = std::max<int64_t>(int64_t(1) << 20, opts->max_keys * 64);
     if (s->ctab.ensure(size_t(opts->max_keys) * 8) || s->cpool.ensure(size_t(s->cpool_words) * 4) ||
-        hipMemset(s->ctab.p, 0xFF, size_t(opts->max_keys) * 8))
+        hipMemset(s->ctab.p, 0xFF, size_t(opts->max_keys) * 8) || s->kstamp.ensure(size_t(opts->max_keys) * 4) ||
+        hipMemset(s->kstamp.p, 0, size_t(opts->max_keys) * 4))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   }
   if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
@@ -657,7 +673,7 @@ void cep_session_close(cep_session* s) {
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
-                  &s->o_entrec, &s->ctab, &s->cpool, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
+                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
                   &s->r_errcode, &s->r_endof, &s->r_prof})
     b->release();
   for (auto& c : s->h_cols) c.release();

@@ -191,6 +191,19 @@ __global__ void carry_commit(int64_t nseg, const int32_t* __restrict__ key, cons
   if (s >= nseg || res_err[s] || res_carry[s] < 0) return;
   ctab[key[seg_start[s]]] = res_carry[s];
 }
+// Carry sessions need each key in one contiguous segment (the batch contract of kcep.h): a key
+// met in two segments would load its blob twice and lose one segment's update.  Every segment
+// stamps its key with the batch number; a stamp that is already there means a second segment.
+// flags: bit 0 a key id outside [0, max_keys), bit 1 a key owning two segments.
+__global__ void carry_keycheck(const int64_t* __restrict__ nseg, const int32_t* __restrict__ key,
+                               const int64_t* __restrict__ seg_start, int32_t max_keys, int32_t* __restrict__ stamp,
+                               int32_t batch_no, unsigned long long* __restrict__ flags) {
+  const int64_t s = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= *nseg) return;
+  const int32_t k = key[seg_start[s]];
+  if (k < 0 || k >= max_keys) { atomicOr(flags, 1ull); return; }
+  if (atomicExch(stamp + k, batch_no) == batch_no) atomicOr(flags, 2ull);
+}
 // carry-pool compaction: live blob sizes, then a copy to the fresh pool
 __global__ void carry_sizes(const int64_t* __restrict__ ctab, int64_t nkeys, const int32_t* __restrict__ cpool,
                             int64_t* __restrict__ words) {
@@ -241,6 +254,16 @@ hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* 
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(carry_commit, dim3(unsigned((nseg + 255) / 256)), dim3(256), 0, st, nseg, key, seg_start,
                      res_carry, res_err, ctab);
+  return hipGetLastError();
+}
+
+// max_seg: a host bound on the segment count (the batch size); the count itself is on the device
+hipError_t carry_keycheck_launch(int64_t max_seg, const int64_t* nseg, const int32_t* key, const int64_t* seg_start,
+                                int32_t max_keys, int32_t* stamp, int32_t batch_no, unsigned long long* flags,
+                                hipStream_t st) {
+  if (max_seg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(carry_keycheck, dim3(unsigned((max_seg + 255) / 256)), dim3(256), 0, st, nseg, key, seg_start,
+                     max_keys, stamp, batch_no, flags);
   return hipGetLastError();
 }
 

@@ -237,7 +237,7 @@ class Schema:
 
     def topic_id(self, topic: str) -> int:
         if topic not in self.topics:
-            self.topics[topic] = len(self.topics)
+            self.topics[topic] = max(self.topics.values(), default=-1) + 1
         return self.topics[topic]
 
 

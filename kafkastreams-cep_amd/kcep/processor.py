@@ -161,8 +161,12 @@ class GpuCEPProcessor:
         base = self.session.stream_position()
         for i, r in enumerate(sorted_recs):
             self._log[base + i] = r[6]
-        self.session.push(n, kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts)
-        out = self.session.collect(raise_on_error=False)
+        try:
+            self.session.push(n, kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts)
+            out = self.session.collect(raise_on_error=False)
+        except N.CepError as e:                           # no state was committed for this batch:
+            self._failed = e                              # the task fails, as the reference's does
+            raise
 
         mrec = out["match_record"] - base                 # stream position -> batch position
         m_arrival = perm[mrec] if len(mrec) else np.zeros(0, np.int64)
@@ -203,12 +207,22 @@ class GpuCEPProcessor:
         """Flushes, then returns the device state (``cep_state_export``) with the host's key table
         and the records carried runs may still reference."""
         self.flush()
-        return {"state": self.session.state_export(), "keys": dict(self._keys), "log": dict(self._log)}
+        return {"state": self.session.state_export(), "keys": dict(self._keys), "log": dict(self._log),
+                "topics": dict(self.schema.topics)}
 
     def restore(self, snap: dict):
         self._check()
         if self._pending:
             raise ProcessorFailed("restore() with buffered records")
+        # carried high-water marks are (interned topic id, offset) pairs (NFAStates.latestOffsets,
+        # NFAStates.java:37): the topic ids must mean the same topics as when the snapshot was taken
+        topics = dict(snap.get("topics", {}))
+        ids = {i: t for t, i in self.schema.topics.items()}
+        for t, i in topics.items():
+            if self.schema.topics.get(t, i) != i or ids.get(i, t) != t:
+                raise ProcessorFailed(f"snapshot topic ids conflict with this processor's schema: {t!r} -> {i}")
+        for t, i in sorted(topics.items(), key=lambda x: x[1]):
+            self.schema.topics[t] = i
         self.session.state_clear()
         self.session.state_import(snap["state"])
         self._keys = dict(snap["keys"])

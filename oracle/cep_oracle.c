@@ -1271,6 +1271,31 @@ int orc_queue_entry(const orc_run* R, int32_t key, int64_t idx, int32_t* sid, in
 }
 
 /* ------------------------------------------------------------------------- */
+/* direct buffer access for SharedVersionedBufferTest.java:50-87: puts and a  */
+/* get (peek without remove, :164-175) on the events of a bound batch         */
+/* ------------------------------------------------------------------------- */
+void orc_svb_bind(orc_run* R, const orc_batch* b) { R->b = b; }
+/* psid < 0: the 3-arg put (:149-157), else the 5-arg put (:101-126) */
+int orc_svb_put(orc_run* R, int sid, int64_t ev, int psid, int64_t pev, const char* version) {
+  SRef cur = {sid, -1};
+  Dewey* v = dw_parse(&R->arena, version);
+  if (psid < 0) return buf_put3(R, cur, ev, v);
+  SRef prev = {psid, -1};
+  return buf_put5(R, cur, ev, prev, pev, v);
+}
+/* buffer.get(Matched.from(stage, ev), version): appended to the run's matches */
+int orc_svb_get(orc_run* R, int sid, int64_t ev, const char* version, int remove) {
+  SRef cur = {sid, -1};
+  Match m; memset(&m, 0, sizeof m);
+  m.record = ev; m.key = R->b->key[ev];
+  int rc = buf_peek(R, cur, ev, dw_parse(&R->arena, version), remove, &m.eb, &m.ee);
+  if (rc) return rc;
+  materialise(R, m.eb, m.ee, &m.gb, &m.ge);
+  VPUSH(R->m, m);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------- */
 /* CPU baseline: key-sharded threads over a key-grouped batch                */
 /* ------------------------------------------------------------------------- */
 typedef struct {

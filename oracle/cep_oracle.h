@@ -98,6 +98,13 @@ int orc_queue_entry(const orc_run* r, int32_t key, int64_t idx, int32_t* stage_i
 int64_t orc_baseline(const orc_pattern* p, const orc_batch* b, int mode, int nthreads,
                      uint64_t* checksum, int* err);
 
+/* SharedVersionedBufferTest (SharedVersionedBufferTest.java:50-87): buffer puts and gets on the
+ * events of a bound batch.  psid < 0 selects the 3-arg put.  orc_svb_get appends the traversal
+ * (and its materialised Sequence) to the run's matches. */
+void orc_svb_bind(orc_run* r, const orc_batch* b);
+int orc_svb_put(orc_run* r, int stage_id, int64_t ev, int prev_stage_id, int64_t prev_ev, const char* version);
+int orc_svb_get(orc_run* r, int stage_id, int64_t ev, const char* version, int remove);
+
 /* DeweyVersion helpers exposed for DeweyVersionTest */
 int orc_dewey_compatible(const char* a, const char* b);
 int orc_dewey_add_run(const char* v, int offset, char* out, size_t cap);

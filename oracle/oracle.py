@@ -68,6 +68,10 @@ def lib():
                                       C.POINTER(I64), C.c_char_p, C.c_size_t]
         L.orc_baseline.argtypes = [P, P, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]
         L.orc_baseline.restype = I64
+        L.orc_svb_bind.argtypes = [P, P]
+        L.orc_svb_bind.restype = None
+        L.orc_svb_put.argtypes = [P, C.c_int, I64, C.c_int, I64, C.c_char_p]
+        L.orc_svb_get.argtypes = [P, C.c_int, I64, C.c_char_p, C.c_int]
         L.orc_dewey_compatible.argtypes = [C.c_char_p, C.c_char_p]
         L.orc_dewey_add_run.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_size_t]
         L.orc_dewey_add_stage.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
@@ -196,6 +200,23 @@ class OracleRun:
                     k += cnts[g]
             out.append(mt)
         return out
+
+    # ---- SharedVersionedBufferTest: direct buffer operations on a bound batch ----
+    def svb_bind(self, batch: BatchArrays):
+        self._keep.append(batch)
+        lib().orc_svb_bind(self.h, C.byref(batch.s))
+
+    def svb_put(self, sid, ev, psid, pev, version):
+        rc = lib().orc_svb_put(self.h, sid, ev, -1 if psid is None else psid, -1 if pev is None else pev,
+                               version.encode())
+        if rc:
+            raise OracleError(rc, lib().orc_err_msg(self.h).decode())
+
+    def svb_get(self, sid, ev, version, remove=False):
+        rc = lib().orc_svb_get(self.h, sid, ev, version.encode(), 1 if remove else 0)
+        if rc:
+            raise OracleError(rc, lib().orc_err_msg(self.h).decode())
+        return self.matches()[-1]
 
     def state(self, key=0):
         runs, qs = C.c_int64(), C.c_int64()

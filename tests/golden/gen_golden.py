@@ -329,7 +329,7 @@ def processor_fixtures():
 
 
 def dewey_fixtures():
-    """DeweyVersionTest.java:24-60 and SharedVersionedBufferTest.java:50-87."""
+    """DeweyVersionTest.java:24-60 (SharedVersionedBufferTest: svb_fixtures)."""
     return dict(
         name="dewey", source="DeweyVersionTest.java:24-60",
         to_string=[["1", "1"], ["1.0.1", "1.0.1"]],
@@ -340,6 +340,25 @@ def dewey_fixtures():
     )
 
 
+def svb_fixtures():
+    """SharedVersionedBufferTest.java:50-87: puts on stages first/second/latest over ev1..ev5
+    (keys k1..k5, topic-test partition 0, offsets 0..4, ts 1000000001..5, :38-42) and the
+    Sequences the test reads back with buffer.get(Matched.from(stage, ev), version).  A get
+    asserts the total size and, per stage name, either the event list or only its size,
+    exactly as the Java test does."""
+    events = dict(key=[1, 2, 3, 4, 5], offset=[0, 1, 2, 3, 4], ts=[1000000001 + i for i in range(5)])
+    one = [["first", 0, None, None, "1"], ["second", 1, "first", 0, "1.0"], ["latest", 2, "second", 1, "1.0.0"]]
+    get1 = dict(stage="latest", event=2, version="1.0.0", size=3,
+                events={"latest": [2], "second": [1], "first": [0]})
+    branch = one + [["second", 2, "second", 1, "1.1"], ["second", 3, "second", 2, "1.1"],
+                    ["latest", 4, "second", 3, "1.1.0"]]
+    get2 = dict(stage="latest", event=4, version="1.1.0", size=5, counts={"latest": 1, "second": 3, "first": 1})
+    return [dict(name="svb_one_run", source="SharedVersionedBufferTest.java:50-62", events=events, puts=one,
+                 gets=[get1]),
+            dict(name="svb_branching_run", source="SharedVersionedBufferTest.java:64-87", events=events,
+                 puts=branch, gets=[get1, get2])]
+
+
 def main():
     fx = nfa_fixtures() + processor_fixtures()
     with open(os.path.join(HERE, "scenarios.json"), "w") as f:
@@ -348,6 +367,8 @@ def main():
         json.dump(stages_factory_fixtures(), f, indent=1)
     with open(os.path.join(HERE, "dewey.json"), "w") as f:
         json.dump(dewey_fixtures(), f, indent=1)
+    with open(os.path.join(HERE, "svb.json"), "w") as f:
+        json.dump(svb_fixtures(), f, indent=1)
     print(f"wrote {len(fx)} scenarios")
 
 

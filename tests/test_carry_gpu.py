@@ -185,3 +185,20 @@ def test_key_id_out_of_range_is_rejected():
     with pytest.raises(N.CepError) as e:
         s.push(2, np.array([1, 9], np.int32), [np.zeros(2, np.int32)])
     assert e.value.code == 11
+
+
+def test_interleaved_carry_batch_is_rejected():
+    """A carry batch must hold each key in one contiguous segment (kcep.h batch contract): a key
+    in two segments would load its carried state twice and lose one segment's update, so the
+    push fails with CEP_E_ARG before the NFA runs, and the carried state is untouched."""
+    ir = PL.any_any().to_ir(PL.I32)
+    s = N.Session(N.CompiledPattern(ir), 10, carry=True, max_keys=4)
+    s.push(3, np.array([0, 0, 1], np.int32), [np.array([0, 1, 2], np.int32)])
+    s.collect()
+    before = [s.key_state(k) for k in range(4)]
+    with pytest.raises(N.CepError) as e:
+        s.push(3, np.array([0, 1, 0], np.int32), [np.array([1, 2, 3], np.int32)])
+    assert e.value.code == 11
+    assert [s.key_state(k) for k in range(4)] == before
+    s.push(2, np.array([1, 1], np.int32), [np.array([1, 2], np.int32)])   # the session still works
+    s.collect()

@@ -71,3 +71,34 @@ def test_dewey():
         assert O.dewey_add_run(O.dewey_add_stage(v)) == want
     for a, b, want in d["compatible"]:
         assert O.dewey_compatible(a, b) == want
+
+
+SVB = load("svb.json")
+
+
+@pytest.mark.parametrize("fx", SVB, ids=[f["name"] for f in SVB])
+def test_shared_versioned_buffer(fx):
+    """SharedVersionedBufferTest.java:50-87 on the oracle's buffer (put 3/5-arg, get)."""
+    from kcep import Schema, QueryBuilder
+    from kcep.expr import Event
+    # a pattern only to name the stages first / second / latest
+    p = O.OraclePattern((QueryBuilder().select("first").where(Event.value() == 0).then()
+                         .select("second").where(Event.value() == 1).then()
+                         .select("latest").where(Event.value() == 2).build()).to_ir(Schema([("value", "i32")])))
+    sid = {name: i for i, (name, _t, _w, _e) in enumerate(p.stages())}
+    ev = fx["events"]
+    n = len(ev["key"])
+    import numpy as np
+    b = O.BatchArrays(ev["key"], [np.zeros(n, np.int32)], [1], offset=ev["offset"], ts=ev["ts"])
+    run = O.OracleRun(p, O.MODE_NFA_SINGLE)
+    run.svb_bind(b)
+    for stage, e, prev, pe, ver in fx["puts"]:
+        run.svb_put(sid[stage], e, None if prev is None else sid[prev], pe, ver)
+    for g in fx["gets"]:
+        m = run.svb_get(sid[g["stage"]], g["event"], g["version"])
+        groups = dict(m.groups)
+        assert sum(len(v) for v in groups.values()) == g["size"]
+        for name, evs in g.get("events", {}).items():
+            assert groups[name] == evs
+        for name, cnt in g.get("counts", {}).items():
+            assert len(groups[name]) == cnt

@@ -152,6 +152,47 @@ def test_processor_error_is_first_in_arrival_order():
     assert got == [("a", [("$final", [0])])]
 
 
+def test_push_failure_fails_the_processor():
+    """A push that raises (e.g. CEP_E_RUN_CAPACITY) leaves the batch uncommitted on the device:
+    the processor must be failed, not silently drop the batch and carry on."""
+    class Boom(StubSession):
+        def push(self, *a, **kw):
+            raise N.CepError(9, "a key exceeded the largest NFA workspace")
+    p, got = make(2, Boom())
+    p.process("a", 1, "events", 0, 0, 0)
+    with pytest.raises(N.CepError):
+        p.process("a", 2, "events", 0, 1, 1)
+    with pytest.raises(ProcessorFailed):
+        p.process("a", 3, "events", 0, 2, 2)
+
+
+def test_restore_reseeds_topic_ids():
+    """checkpoint() carries the Schema's topic ids; restore() into a fresh schema adopts them and
+    refuses a schema whose ids already mean other topics (hwm per interned topic id)."""
+    class Carry(StubSession):
+        def state_export(self, *a):
+            return b"KCST"
+        def state_clear(self):
+            pass
+        def state_import(self, blob):
+            self.imported = blob
+    p, _ = make(100, Carry())
+    for t in ("x", "y"):
+        p.process("a", 1, t, 0, 0, 0)
+    snap = p.checkpoint()
+    assert snap["topics"] == {"x": 0, "y": 1}
+    sch = Schema([("value", "i32")])
+    q = GpuCEPProcessor("q", PL.any_any(), sch, scalar_column(sch))
+    q.init(lambda k, s: None, session=Carry())
+    q.restore(snap)
+    assert sch.topic_id("y") == 1 and sch.topic_id("z") == 2
+    sch2 = Schema([("value", "i32")], topics=["y"])
+    r = GpuCEPProcessor("q", PL.any_any(), sch2, scalar_column(sch2))
+    r.init(lambda k, s: None, session=Carry())
+    with pytest.raises(ProcessorFailed):
+        r.restore(snap)
+
+
 def test_carried_positions_parses_export_blob():
     """kcep.processor.carried_positions on a hand-built cep_state_export blob: two keys, the
     first with 1 high-water mark, 2 queued runs and 2 carried events of 1 column."""

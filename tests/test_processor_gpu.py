@@ -167,6 +167,46 @@ def test_checkpoint_restore_mid_stream():
     assert got == whole and len(whole) > 0
 
 
+def test_checkpoint_restore_fresh_schema_two_topics():
+    """High-water marks are carried per interned topic id (NFAStates.java:37): a restore into a
+    processor with a freshly built Schema that meets the topics in the other order must keep
+    the snapshot's ids, or re-delivered records are judged against the wrong topic's mark."""
+    rng = np.random.default_rng(5)
+    recs, off = [], {"ta": 1000, "tb": 0}
+    for i in range(1600):
+        t = "ta" if i < 400 else ("tb" if i < 900 or rng.random() < 0.5 else "ta")
+        recs.append((f"user-{int(rng.integers(0, 20))}", int(rng.integers(0, 4)), t, 0, off[t], i))
+        off[t] += 1
+    half = 1000                                         # the second half starts with topic tb
+    recs = recs[:half] + [recs[i] for i in rng.choice(half, 60)] + recs[half:]   # re-deliveries
+    whole = run_proc(GpuCEPProcessor("q", PL.any_any(), Schema([("value", "i32")]),
+                                     scalar_column(Schema([("value", "i32")])), batch_size=64), recs)
+    got = []
+    fwd = lambda k, s: got.append((k, seq_view(s)))   # noqa: E731
+    s1 = Schema([("value", "i32")])
+    p1 = GpuCEPProcessor("q", PL.any_any(), s1, scalar_column(s1), batch_size=64)
+    p1.init(fwd)
+    for r in recs[:half]:
+        p1.process(*r)
+    snap = p1.checkpoint()
+    p1.close()
+    s2 = Schema([("value", "i32")])                     # fresh: no topic seen yet
+    p2 = GpuCEPProcessor("q", PL.any_any(), s2, scalar_column(s2), batch_size=64)
+    p2.init(fwd)
+    p2.restore(snap)
+    assert s2.topics == {"ta": 0, "tb": 1}
+    for r in recs[half:]:
+        p2.process(*r)
+    p2.close()
+    assert got == whole and len(whole) > 0
+    s3 = Schema([("value", "i32")], topics=["tb"])      # an id already taken by another topic
+    p3 = GpuCEPProcessor("q", PL.any_any(), s3, scalar_column(s3), batch_size=64)
+    p3.init(fwd)
+    with pytest.raises(ProcessorFailed):
+        p3.restore(snap)
+    p3.close()
+
+
 def test_reference_exception_surfaces():
     """test_stock_demo_minimal_npe's input through the processor: the matches before the
     failing record are forwarded, then the reference's NullPointerException is raised and
