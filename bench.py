@@ -6,12 +6,19 @@
   the dominant kernel.
 
 One process per GPU (torch.distributed over RCCL when launched with
-torch.distributed.run).  Keys are sharded across ranks (weak scaling: every
-rank owns its own keys and events); the only collective is the all-gather of
-per-rank (events, matches, seconds) after the timed region.
+torch.distributed.run).  With N > 1 every rank generates the node-wide stream
+(counter RNG, identical on every rank), splits it with the product partitioner
+(kcep/shard.py: cep_shard_plan + cep_partition on the device, keys by hash
+rebalanced to equal events) and matches only its shard.  C2/C3/C4 keep the
+per-GPU shape (weak scaling: N x 1M keys x 100M events for C2); C5 is the
+node-wide 10M keys x 100 events split over N GPUs (strong scaling).  The one
+collective is kcep/shard.py's CountExchange: after every step the rank's
+device-resident match count is all-gathered over RCCL with its event count and
+scanned into the rank's global match offset, on a side stream that overlaps the
+next step.
 
-``--config c3|c4|c5`` measures the other BASELINE configs on the general NFA
-kernel (not the headline line; DESIGN.md reports them).
+``--config c3|c4|c5`` measures the other BASELINE configs (not the headline
+line; DESIGN.md reports them).
 
 Prints ONE JSON line on rank 0.
 """
@@ -35,7 +42,8 @@ CONFIGS = {
     "c2": dict(keys=1_000_000, events=100_000_000, desc="C2: 3-stage strict A->B->C, processor mode"),
     "c3": dict(keys=100_000, per_key=100, desc="C3: stock oneOrMore + sum/count state + within(60s)"),
     "c4": dict(keys=100_000, per_key=12, desc="C4: skip-till-any times(3) + zeroOrMore"),
-    "c5": dict(keys=1_250_000, per_key=100, desc="C5: AND/OR + optional(), strict (1/8 of the 10M-key node)"),
+    "c5": dict(keys=10_000_000, per_key=100, node_wide=True,
+               desc="C5: AND/OR + optional(), strict, 10M keys x 100 events node-wide, key-hash sharded"),
 }
 
 
@@ -51,18 +59,15 @@ def parse(argv=None):
                     help="oracle threads for cpu_baseline (default: nproc, every CPU this process may run on)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-input", action="store_true", help="skip the PCIe-inclusive (host buffer) figure")
+    ap.add_argument("--gather-matches", action="store_true",
+                    help="N > 1: after the timed steps, gather every rank's matches to rank 0 (12 B/match) and "
+                         "time it")
     return ap.parse_args(argv)
 
 
-def shard(rank: int, n: int, K: int):
-    """Rank r owns keys [r*K, (r+1)*K) and the counter range [r*n, (r+1)*n) of the
-    generator: disjoint key sets, so per-key NFAs never cross ranks."""
-    return rank * K, rank * n
-
-
 def gather_stats(stats, world: int):
-    """The path's one exchange step: all-gather per-rank (events, matches, seconds);
-    returns (total events, total matches, max seconds over ranks)."""
+    """All-gather per-rank (events, matches, seconds) after the timed region; returns (total
+    events, total matches, max seconds over ranks)."""
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -72,22 +77,48 @@ def gather_stats(stats, world: int):
     return float(stats[0]), float(stats[1]), float(stats[2])
 
 
-def workload(cfg: str, rank: int, K: int, n: int | None, dev):
-    """Device-resident batch of one rank: (key, [cols], ts, ir, schema_types, stream_np_fn)."""
+def node_stream(cfg: str, K: int, n: int | None, dev):
+    """The stream one GPU (world 1) or the whole node (world > 1) matches, device-resident:
+    (key, [cols], ts, ir)."""
     from kcep import synth, Schema
     I32 = Schema([("value", "i32")])
     if cfg == "c2":
-        ko, lo = shard(rank, n, K)
-        key, val, order = synth.c2_stream_torch(n, K, dev, key_offset=ko, lo=lo)
-        return key, [val], order, synth.c2_pattern().to_ir(I32), \
-            lambda m: synth.c2_stream_np(n, K, key_offset=ko, lo=lo)
+        key, val, order = synth.c2_stream_torch(n, K, dev)
+        return key, [val], order, synth.c2_pattern().to_ir(I32)
     L = CONFIGS[cfg]["per_key"]
     gen_t = {"c3": synth.c3_stream_torch, "c4": synth.c4_stream_torch, "c5": synth.c5_stream_torch}[cfg]
-    gen_n = {"c3": synth.c3_stream_np, "c4": synth.c4_stream_np, "c5": synth.c5_stream_np}[cfg]
     pat = {"c3": synth.c3_pattern, "c4": synth.c4_pattern, "c5": synth.c5_pattern}[cfg]()
-    ko, lo = rank * K, rank * K
-    key, val, ts = gen_t(K, dev, L=L, key_offset=ko, lo=lo)
-    return key, [val], ts, pat.to_ir(I32), lambda kk: gen_n(kk, L=L, key_offset=ko, lo=lo)
+    key, val, ts = gen_t(K, dev, L=L)
+    return key, [val], ts, pat.to_ir(I32)
+
+
+def workload(cfg: str, rank: int, world: int, K: int, n: int | None, dev, stream):
+    """This rank's device-resident batch: (key, [cols], ts, ir, shard info).  World 1: the
+    per-GPU config.  World > 1: the node-wide stream split by the product partitioner -- keys
+    planned by hash, rebalanced to equal events (cep_shard_plan), split on the device
+    (cep_partition + cep_gather)."""
+    import torch
+    from kcep import shard as S
+    node_wide = CONFIGS[cfg].get("node_wide", False)
+    if world == 1:
+        key, cols, ts, ir = node_stream(cfg, K, n, dev)
+        return key, cols, ts, ir, None
+    NK = K if node_wide else K * world
+    NN = None if n is None else (n if node_wide else n * world)
+    key, cols, ts, ir = node_stream(cfg, NK, NN, dev)
+    t0 = time.perf_counter()
+    counts = torch.bincount(key, minlength=NK).cpu().numpy()
+    table, loads = S.shard_plan(counts, world, rebalance=True)
+    sh = S.split(rank, world, key, cols, table=torch.from_numpy(table).to(dev),
+                 stream=stream.cuda_stream if stream is not None else None, ts=ts)
+    if key.is_cuda:
+        torch.cuda.synchronize(dev)
+    info = {"node_events": int(key.numel()), "node_keys": NK, "planned_events": loads.tolist(),
+            "partition_s": time.perf_counter() - t0, "partitioner": "cep_shard_plan(rebalance) + cep_partition"}
+    del key, cols, ts
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    return sh.key, sh.cols, sh.extra["ts"], ir, (sh, info)
 
 
 def main():
@@ -109,9 +140,13 @@ def main():
     C = CONFIGS[args.config]
     K = args.keys or C["keys"]
     n_req = args.events or C.get("events")
-    key, cols, ts, ir, gen_np = workload(args.config, rank, K, n_req, dev)
+    key, cols, ts, ir, shard_info = workload(args.config, rank, world, K, n_req, dev, stream)
     n = int(key.numel())
     torch.cuda.synchronize(dev)
+    exchange = None
+    if world > 1:
+        from kcep import shard as S
+        exchange = S.CountExchange(dev)
 
     pat = N.CompiledPattern(ir)
     sess = N.Session(pat, n, mode=N.MODE_PROCESSOR, device=local)
@@ -120,6 +155,8 @@ def main():
 
     def step():
         sess.push(n, key.data_ptr(), [c.data_ptr() for c in cols], mem=N.MEM_DEVICE, stream=stream.cuda_stream)
+        if exchange is not None:             # the path's one exchange: counts -> global match offsets
+            exchange.post(sess, n, stream)
 
     for _ in range(args.warmup):
         step()
@@ -151,6 +188,22 @@ def main():
     n_matches, csum = sess.checksum()
     stats = torch.tensor([float(n), float(n_matches), elapsed], dtype=torch.float64, device=dev)
     tot_events, tot_matches, t_max = gather_stats(stats, world)
+    exch = None
+    if exchange is not None:
+        off, node_ev, node_m = exchange.result((exchange.posted - 1) % exchange.slots)
+        exch = {"collective": "RCCL all_gather of (events, matches) + exclusive scan, per step, side stream",
+                "rank0_match_offset": off, "node_events": node_ev, "node_matches": node_m,
+                "consistent": bool(node_ev == int(tot_events) and node_m == int(tot_matches))}
+        if args.gather_matches:
+            from kcep import shard as S
+            out = sess.collect()
+            dist.barrier()
+            tg = time.perf_counter()
+            merged = S.gather_matches(out, shard_info[0].perm, dst=0)
+            dist.barrier()
+            exch["gather_s"] = time.perf_counter() - tg
+            if rank == 0:
+                exch["gathered_matches"] = int(len(merged["match_record"]))
 
     if rank == 0:
         if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
@@ -180,14 +233,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": t_max * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if C.get("node_wide") and world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (splitmix64 counter RNG, BASELINE.md §3)",
             "config": {"workload": C["desc"], "events_per_gpu": n, "keys_per_gpu": K,
                        "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
                        "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain", N.PATH_RUNS: "runs"}.get(sess.path, "general"),
-                       "parallelism": f"key-sharded x{world}",
+                       "parallelism": f"key-hash sharded x{world}" if world > 1 else "1 GPU",
                        "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
@@ -195,6 +248,9 @@ def main():
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",
         }
+        if shard_info is not None:
+            line["config"]["shard"] = shard_info[1]
+            line["config"]["exchange"] = exch
         if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):
             line["batch_ms"] = roof_ms
             line["first_kernel"] = {"name": {N.PATH_GENERAL: "kcep_nfa_kernel" if sess.jit else "nfa_kernel",

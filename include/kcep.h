@@ -240,6 +240,41 @@ int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len
 /* Stream position the next batch's record 0 gets (0 for sessions without CEP_SESSION_CARRY). */
 int64_t cep_stream_position(const cep_session* s);
 
+/* --- key-hash sharding across the GPUs of one node ---
+ * The reference gets per-key independence from Kafka: the producer partitions records by key
+ * hash, so each key's NFA lives in exactly one stream task (README.md:348-355; per-key run
+ * counter NFAStates.java:36, buffer nodes keyed by (stage, topic, partition, offset), aggregates
+ * by (key, state, run)).  A node splits a batch the same way, one shard per GPU, and the shards
+ * are matched with no exchange; only match counts and offsets cross GPUs (kcep/shard.py, RCCL). */
+#define CEP_MAX_SHARDS 64
+/* MurmurHash3 fmix32 of the key id, and the default shard fmix32(key_id) % n_shards. */
+uint32_t cep_key_hash(int32_t key_id);
+int32_t cep_key_shard(int32_t key_id, int32_t n_shards);
+/* Shard plan for dense key ids [0, n_keys) with key_events[k] records each: key_shard[k] =
+ * cep_key_shard(k); with rebalance != 0 keys then move from the fullest shard to the emptiest
+ * (the largest key lighter than the gap, repeatedly) toward equal event counts.  A carry session's
+ * keys must keep their shard across batches: compute the plan once and pass it to every
+ * cep_partition.  shard_events (optional, n_shards entries) receives the planned loads. */
+int cep_shard_plan(const int64_t* key_events, int64_t n_keys, int32_t n_shards, int32_t rebalance,
+                   int32_t* key_shard, int64_t* shard_events);
+/* Stable split of a batch by shard: shard(i) = key_shard[key_id[i]] when key_shard != NULL and
+ * 0 <= key_id[i] < n_keys (entries outside [0, n_shards) fall back to the hash), else
+ * cep_key_shard(key_id[i]).  perm[j] = source record of output position j; shard s owns positions
+ * [shard_off[s], shard_off[s+1]) (n_shards + 1 entries), in batch order, so each shard keeps the
+ * batch's key grouping and per-key arrival order.  mem = CEP_MEM_HOST (computed in the call) or
+ * CEP_MEM_DEVICE (every array on the device, kernels enqueued on `stream`, no host sync).
+ * n_shards <= CEP_MAX_SHARDS. */
+int cep_partition(const int32_t* key_id, int64_t n, int32_t n_shards, const int32_t* key_shard, int64_t n_keys,
+                  int64_t* perm, int64_t* shard_off, int32_t mem, void* stream);
+/* dst[i] = src[perm[i]] for i < n, elements of elem_bytes (1, 4 or 8): a shard's columns from
+ * perm + shard_off[s].  Same memory rules as cep_partition. */
+int cep_gather(const void* src, int32_t elem_bytes, const int64_t* perm, int64_t n, void* dst, int32_t mem,
+               void* stream);
+/* Enqueue a copy of the last batch's device-resident match count (cep_device_match_count) to
+ * dst (device memory) on `stream`: a per-step slot for an RCCL all-gather of counts that
+ * overlaps the next batch (kcep/shard.py CountExchange). */
+int cep_match_count_to(const cep_session* s, int64_t* dst, void* stream);
+
 const char* cep_last_error(void);
 const char* cep_version(void);
 

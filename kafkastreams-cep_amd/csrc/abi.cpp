@@ -69,6 +69,11 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+}  // namespace
+namespace kcep {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace kcep
+namespace {
 
 #define HIPCHECK(x)                                                                                \
   do {                                                                                             \
@@ -787,7 +792,21 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   return push_general(s, b, st);
 }
 
-const int64_t* cep_device_match_count(const cep_session* s) { return s ? s->total.as<int64_t>() : nullptr; }
+const int64_t* cep_device_match_count(const cep_session* s) {
+  if (!s) return nullptr;
+  // general and runs batches keep the count where their compaction scan left it
+  return s->last_path == CEP_PATH_GENERAL || s->last_path == CEP_PATH_RUNS ? s->scal.as<int64_t>() + 3
+                                                                            : s->total.as<int64_t>();
+}
+
+int cep_match_count_to(const cep_session* s, int64_t* dst, void* stream) {
+  if (!s || !dst) return fail(CEP_E_ARG, "null argument");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->n == 0 || s->last_path == 0) HIPCHECK(hipMemsetAsync(dst, 0, 8, st));
+  else HIPCHECK(hipMemcpyAsync(dst, cep_device_match_count(s), 8, hipMemcpyDeviceToDevice, st));
+  return CEP_OK;
+}
 
 int cep_session_set_timing(cep_session* s, int on) {
   if (!s) return fail(CEP_E_ARG, "null argument");

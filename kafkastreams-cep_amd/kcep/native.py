@@ -69,7 +69,8 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position",
            "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels", "cep_live_run_hwm",
            "cep_batch_errors", "cep_session_set_timing",
-           "cep_key_profile"]
+           "cep_key_profile", "cep_key_hash", "cep_key_shard", "cep_shard_plan", "cep_partition", "cep_gather",
+           "cep_match_count_to"]
 
 _lib = None
 
@@ -123,6 +124,14 @@ def lib():
     L.cep_key_profile.argtypes = [P, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
     L.cep_pattern_kernel_source.argtypes = [P, C.c_int32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
     L.cep_pattern_build_kernels.argtypes = [P, C.c_int32]
+    L.cep_key_hash.argtypes = [C.c_int32]
+    L.cep_key_hash.restype = C.c_uint32
+    L.cep_key_shard.argtypes = [C.c_int32, C.c_int32]
+    L.cep_key_shard.restype = C.c_int32
+    L.cep_shard_plan.argtypes = [P, C.c_int64, C.c_int32, C.c_int32, P, P]
+    L.cep_partition.argtypes = [P, C.c_int64, C.c_int32, P, C.c_int64, P, P, C.c_int32, P]
+    L.cep_gather.argtypes = [P, C.c_int32, P, C.c_int64, P, C.c_int32, P]
+    L.cep_match_count_to.argtypes = [P, P, P]
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -310,6 +319,10 @@ class Session:
 
     def stream_position(self):
         return lib().cep_stream_position(self.h)
+
+    def match_count_to(self, dst_ptr: int, stream=None):
+        """Enqueue a copy of the last batch's device match count (int64) to device address dst_ptr."""
+        check(lib().cep_match_count_to(self.h, C.c_void_p(dst_ptr), C.c_void_p(stream) if stream else None))
 
     def last_kernel_ms(self):
         ms = C.c_float()
