@@ -39,7 +39,7 @@ extern "C" {
 #define CEP_E_CLASS_CAST 6        /* state read with another boxed type than it was folded with */
 #define CEP_E_INDEX 7             /* DeweyVersion.addRun out of bounds  DeweyVersion.java:62-67 */
 #define CEP_E_BAD_IR 8            /* malformed pattern IR */
-#define CEP_E_RUN_CAPACITY 9      /* a key exceeded the device run/buffer capacity even after regrowth */
+#define CEP_E_RUN_CAPACITY 9      /* a key exceeded the device run/buffer capacity (per key: cep_opts.max_key_words) */
 #define CEP_E_HIP 10              /* HIP runtime error */
 #define CEP_E_ARG 11              /* invalid argument */
 #define CEP_E_UNSUPPORTED 12      /* pattern feature not lowered to the device */
@@ -84,6 +84,13 @@ typedef struct {
   int64_t max_events;      /* capacity of one batch */
   int64_t max_keys;        /* CEP_SESSION_CARRY: key ids are dense in [0, max_keys) */
   double arena_scale;      /* general path: per-key workspace multiplier (0 = default 1.0) */
+  int64_t max_key_words;   /* general path: device workspace words one key may take (0 = no limit but the
+                              pool).  A key over it -- or still out of pool after the pool regrowths -- is
+                              handed back per key: cep_batch_errors lists it with CEP_E_RUN_CAPACITY at the
+                              record where it ran out, its matches before that record are emitted, a carry
+                              session keeps its state as of the batch start, and every other key of the
+                              batch completes normally.  The host routes that key to the reference CPU path
+                              (a key over capacity falls back per key). */
 } cep_opts;
 
 /* Session flags */

@@ -468,6 +468,8 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.ctab = s->carry ? s->ctab.as<int64_t>() : nullptr;
     A.cpool = s->carry ? s->cpool.as<int32_t>() : nullptr;
     A.cpool_cap = s->carry ? s->cpool_words : 0;
+    A.last_attempt = attempt >= kMaxRetry ? 1 : 0;     // then an overflowing key is handed back per key
+    A.max_key_words = s->opts.max_key_words;
     unsigned long long init[4] = {0, (unsigned long long)s->cpool_used, 0, 0};
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
@@ -484,7 +486,8 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       if (s->carry) s->cpool_used = int64_t(res[1]);
       break;
     }
-    if (attempt >= kMaxRetry) return fail(CEP_E_RUN_CAPACITY, "a key exceeded the largest NFA workspace");
+    if (attempt >= kMaxRetry && fl[0]) return fail(CEP_E_RUN_CAPACITY, "the NFA workspace pool cannot grow");
+    if (attempt >= kMaxRetry && fl[1]) return fail(CEP_E_RUN_CAPACITY, "the carried-state pool cannot grow");
     if (fl[0]) {                                   // workspace pool exhausted: twice the pool, same inputs
       s->pool.release();
       s->pool_words *= 2;

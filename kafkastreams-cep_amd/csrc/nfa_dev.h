@@ -65,6 +65,9 @@ struct Lane {
   int64_t runs_delta;
   int32_t err;
   int32_t overflow;
+  int32_t cap_hit;             // the key went over NfaArgs.max_key_words
+  int32_t rec_out_top;         // output words / matches before the current record (capacity rollback)
+  int64_t rec_nmatch;
   int32_t r;                   // current local event
   int64_t g;                   // its batch record index
   int64_t nmatch;
@@ -92,6 +95,7 @@ struct Lane {
 // every allocation is a multiple of 16 bytes (queues are read as int4)
 __device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words) {
   const int64_t w = (words + 3) & ~int64_t(3);
+  if (l.A->max_key_words > 0 && l.pool_words + w > l.A->max_key_words) { l.overflow = 1; l.cap_hit = 1; return nullptr; }
   const unsigned long long at = atomicAdd(l.A->pool_top, (unsigned long long)w);
   if (at + (unsigned long long)w > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
   l.pool_words += w;
@@ -924,6 +928,10 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   const auto& P = KCEP_PROG(l);
   l.seg0 = A.seg_start[seg];
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
+  l.g = l.seg0;
+  l.cap_hit = 0;
+  l.rec_out_top = 0;
+  l.rec_nmatch = 0;
   l.err = 0; l.overflow = 0; l.nmatch = 0; l.flen = 0; l.tlen = 0; l.qlen = 0;
   l.nhwm = 0; l.runs = 1; l.runs_delta = 0; l.slm = 0; l.sle = 0;
   l.C = 0; l.cev = nullptr;
@@ -957,7 +965,12 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
                         int64_t(3) * nst * l.seqcap + l.heapcap + l.outcap;
   int32_t* p = pool_alloc(l, fixed);
   if (!p) {
-    atomicAdd(&A.flags[0], 1);
+    if (A.last_attempt || l.cap_hit) {                                 // handed back per key
+      A.res_err[seg] = CEP_E_RUN_CAPACITY;
+      A.res_err_rec[seg] = A.base + l.seg0;
+    } else {
+      atomicAdd(&A.flags[0], 1);
+    }
     return;
   }
   l.hwm = p; p += 3 * HWM_MAX;
@@ -973,6 +986,11 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   for (int64_t i = 0; i < int64_t(3) * nst * l.seqcap; i++) l.aggs[i] = 0;   // all states null
   if (blob) {
     if (!import_state(l, blob)) {
+      if (l.overflow && (A.last_attempt || l.cap_hit)) {
+        A.res_err[seg] = CEP_E_RUN_CAPACITY;
+        A.res_err_rec[seg] = A.base + l.seg0;
+        return;
+      }
       if (l.overflow) atomicAdd(&A.flags[0], 1);
       A.res_err[seg] = l.err;
       return;
@@ -1012,6 +1030,8 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
     }
     eval_event_only(l);
     evals += l.qlen;
+    l.rec_out_top = l.out_top;
+    l.rec_nmatch = l.nmatch;
     if (!step(l, fr)) {
       if (l.err) err_rec = A.base + g;
       break;
@@ -1047,12 +1067,24 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
     pr[14] = 0;                                                        // (no LDS workspace)
     pr[15] = l.pool_words;
   }
+  if (l.overflow && (A.last_attempt || l.cap_hit)) {
+    // over capacity: the key stops at this record and is handed back (CEP_E_RUN_CAPACITY); the
+    // matches of its earlier records stand, like the records before a reference exception
+    A.res_err[seg] = CEP_E_RUN_CAPACITY;
+    A.res_err_rec[seg] = A.base + l.g;
+    l.overflow = 0;
+    if (l.nmatch > l.rec_nmatch) {                                     // none of the failing record's
+      l.nmatch = l.rec_nmatch;                                         // matches is emitted
+      l.out_top = l.rec_out_top;
+    }
+  } else {
+    A.res_err[seg] = l.overflow ? 0 : l.err;
+    A.res_err_rec[seg] = l.overflow ? -1 : err_rec;
+  }
+  if (l.overflow) atomicAdd(&A.flags[0], 1);
   A.res_matches[seg] = l.nmatch;
   A.res_words[seg] = l.out_top;
   A.res_out[seg] = int64_t(reinterpret_cast<uintptr_t>(l.out));
-  A.res_err[seg] = l.overflow ? 0 : l.err;
-  A.res_err_rec[seg] = l.overflow ? -1 : err_rec;
-  if (l.overflow) atomicAdd(&A.flags[0], 1);
 }
 
 }  // namespace kcep

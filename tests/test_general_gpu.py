@@ -11,6 +11,7 @@ import pytest
 import oracle as O
 from kcep import native as N
 from golden_util import scenarios, event_arrays, seq_repr
+from gpu_util import oracle_matches, product_matches
 import patterns_lib as PL
 
 pytestmark = pytest.mark.gpu
@@ -177,3 +178,25 @@ def test_null_records_and_high_water_mark():
     ir = PL.any_any().to_ir(PL.I32)
     want, got, oerr, gerr = run_both(ir, O.MODE_PROCESSOR, key, [val], [1], valid=valid, offset=offset)
     assert oerr is None and gerr is None and got == want and len(got) > 0
+
+
+def test_over_capacity_key_is_handed_back_alone():
+    """a key whose runs outgrow the device capacity falls back per key.  With a small
+    per-key workspace cap (cep_opts.max_key_words) the exploding skip-till-any key stops at the record
+    where it ran out and is listed by cep_batch_errors with CEP_E_RUN_CAPACITY; its matches before
+    that record and every other key's matches equal the oracle's, and the batch itself succeeds."""
+    rng = np.random.default_rng(4)
+    lens = [12] * 40
+    lens[7] = 400                                          # the exploding key
+    key = np.repeat(np.arange(40, dtype=np.int32), lens)
+    val = rng.integers(0, 4, len(key)).astype(np.int32)
+    ir = PL.any_any().to_ir(PL.I32)
+    want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
+    s = N.Session(N.CompiledPattern(ir), len(key), force_path=N.PATH_GENERAL, max_key_words=1 << 15)
+    s.push(len(key), key, [val])
+    out = s.collect(raise_on_error=False)
+    rec, code = s.batch_errors()
+    assert list(code) == [9] and key[rec[0]] == 7
+    got = product_matches(s, out)
+    assert got == [m for m in want if m[1] != 7 or m[0] < rec[0]]
+    assert any(m[1] == 7 for m in got) and any(m[1] == 7 and m[0] >= rec[0] for m in want)
