@@ -31,6 +31,7 @@ hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t n
                         const StencilProgram* P, unsigned long long* sum, hipStream_t st);
 
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf);
+hipError_t nfa_wave_launch(const NfaArgs& A, int64_t nwg, hipStream_t st, hipFunction_t jf);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
 hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
@@ -110,6 +111,19 @@ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// The wave kernel (nfa_wave.h) evaluates a record's runs in parallel: it needs a pattern whose
+// evaluations read nothing but the record -- every edge predicate event-only, no folds, no states.
+bool wave_ok(const DevProgram& D) {
+  if (D.nstates || D.ndefined) return false;
+  for (int s = 0; s < D.nstages; s++) {
+    const DevStage& t = D.st[s];
+    if (t.nfolds) return false;
+    for (int e = 0; e < t.nedges; e++)
+      if (t.pred[e] >= 0 && t.sl[e] < 0) return false;
+  }
+  return true;
+}
+
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
 constexpr NfaCaps kCaps{16, 64, 16, 32, 8, 16};
 constexpr int kMaxRetry = 8;                       // pool doublings before CEP_E_RUN_CAPACITY
@@ -157,6 +171,7 @@ struct cep_session {
   std::shared_ptr<const JitModule> jitg;   // general path (built at open, or at the first general batch)
   bool jitg_tried = false;
   int64_t live_hwm = 0;                    // general path: most live runs any key held in the last batch
+  bool wave = false;                       // general path: one key per wave (nfa_wave.h) for this pattern
   DBuf r_prof;                             // CEP_SESSION_PROFILE: per key segment {live max, evaluations, cycles}
   std::string jit_why;
   int32_t g_err = CEP_OK;
@@ -473,7 +488,9 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     unsigned long long init[4] = {0, (unsigned long long)s->cpool_used, 0, 0};
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
-    HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
+    A.wave_seg = nullptr;
+    if (s->wave) HIPCHECK(nfa_wave_launch(A, nseg, st, s->jitg ? s->jitg->nfa_wave : nullptr));
+    else HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
     if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
     timed = true;
     unsigned long long res[4];
@@ -664,6 +681,8 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   }
   if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
     return cleanup(fail(CEP_E_HIP, "event create failed"));
+  const char* env_wave = getenv("KCEP_NFA_WAVE");      // 0: the lane kernel for every pattern (A/B runs)
+  s->wave = P.general_ok && wave_ok(P.dev) && !(opts->flags & CEP_SESSION_LANE_NFA) && !(env_wave && !strcmp(env_wave, "0"));
   const char* env_jit = getenv("KCEP_JIT");
   s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
   if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels

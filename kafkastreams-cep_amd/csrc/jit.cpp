@@ -335,9 +335,12 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // waves per SIMD the register budget is cut for (KCEP_NFA_WAVES, tuning only)
   const char* wenv = getenv("KCEP_NFA_WAVES");
   const int waves = wenv ? std::min(8, std::max(1, atoi(wenv))) : 2;
-  o += "#include \"nfa_dev.h\"\nextern \"C\" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(" +
-       std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
+  o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
+       "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
   kcep::nfa_kernel_body(A);
+}
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void kcep_nfa_wave(kcep::NfaArgs A) {
+  kcep::nfa_wave_body(A);
 }
 )";
   return o;
@@ -346,9 +349,9 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
 std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why, bool phases) {
   const std::string src = jit_source_general(P, why, phases);
   if (src.empty()) return nullptr;
-  static const char* const names[] = {"kcep_nfa_kernel"};
-  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa};
-  return build(src, names, slots, 1, why);
+  static const char* const names[] = {"kcep_nfa_kernel", "kcep_nfa_wave"};
+  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa, &JitModule::nfa_wave};
+  return build(src, names, slots, 2, why);
 }
 
 bool jit_check_general(const Program& P, std::string& why) {

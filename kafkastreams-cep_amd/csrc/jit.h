@@ -16,6 +16,7 @@ struct JitModule {
   hipFunction_t runs_sim = nullptr;     // runs_dev.h runs_sim_body<JitTab>
   hipFunction_t runs_write = nullptr;   // runs_dev.h runs_write_body<JitTab>
   hipFunction_t nfa = nullptr;          // nfa_dev.h nfa_kernel_body (general path)
+  hipFunction_t nfa_wave = nullptr;     // nfa_wave.h nfa_wave_body (general path, patterns without aggregates)
   ~JitModule();
 };
 

@@ -145,6 +145,7 @@ struct NfaArgs {
   int64_t* profile;               // CEP_SESSION_PROFILE: NFA_PROFILE_W words per segment (nfa_dev.h)
   int32_t spread;                 // key segments per wave (1..64)
   int32_t last_attempt;           // 1: no pool regrowth follows -- an overflowing key reports CEP_E_RUN_CAPACITY
+  const int32_t* wave_seg;        // wave kernel: the segment of each workgroup (nullptr: workgroup = segment)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY
 };
 

@@ -43,11 +43,17 @@
 #include "kcep_internal.h"
 #include "interp.h"
 #include "nfa_dev.h"
+#include "nfa_wave.h"
 
 namespace kcep {
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nfa_kernel(NfaArgs A) {
   nfa_kernel_body(A);
+}
+
+// one key per wave, one queued run per lane (nfa_wave.h); patterns without aggregates
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nfa_wave_kernel(NfaArgs A) {
+  nfa_wave_body(A);
 }
 
 // ---- segments, scans, output compaction, carry commit ----
@@ -137,6 +143,18 @@ hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf) {
     return hipModuleLaunchKernel(jf, grid, 1, 1, 64, 1, 1, 0, st, args, nullptr);
   }
   hipLaunchKernelGGL(nfa_kernel, dim3(grid), dim3(64), 0, st, A);
+  return hipGetLastError();
+}
+
+// jf: the pattern's compiled wave kernel, nullptr for the built-in one.  nwg workgroups of one wave.
+hipError_t nfa_wave_launch(const NfaArgs& A, int64_t nwg, hipStream_t st, hipFunction_t jf) {
+  if (nwg <= 0) return hipSuccess;
+  if (jf) {
+    NfaArgs a = A;
+    void* args[] = {&a};
+    return hipModuleLaunchKernel(jf, unsigned(nwg), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+  }
+  hipLaunchKernelGGL(nfa_wave_kernel, dim3(unsigned(nwg)), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 

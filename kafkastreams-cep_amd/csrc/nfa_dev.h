@@ -73,6 +73,13 @@ struct Lane {
   int64_t nmatch;
   uint64_t slm, sle;           // event-only edge predicates on record r: values / deferred errors
   int64_t pool_words;          // taken from the pool (profile)
+  // ---- wave mode (nfa_wave.h: one key per wave, one queued run per lane) ----
+  int32_t wave;                // 1: heap allocations are shared by the wave, buffer operations are logged
+  int32_t* wtop;               // wave: the key's heap top, in LDS
+  int32_t* log;                // wave: this lane's run's deferred buffer operations, WL words each
+  int32_t log_cap, log_n;
+  int32_t nph;                 // wave: run-counter increments of this lane's run (seq placeholders)
+  int32_t wgrow;               // wave: the shared heap was too small (grow it and re-run the round)
 #ifdef KCEP_PHASES
   uint64_t ph[11];             // profiling kernels only: clocks in evaluate / predicates / buffer puts+branch /
                                // removePattern / matchConstruction / first_compatible / add_pred / versions,
@@ -132,6 +139,11 @@ __device__ __forceinline__ bool is_fwd_final(const Lane& l, int sid, int eps) { 
 
 // ---- heap: versions and predecessor pointers ----
 __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
+  if (l.wave) {                                    // versions are immutable: any allocation order will do
+    const int at = atomicAdd(l.wtop, words);
+    if (at + words > l.heapcap) { l.wgrow = 1; l.overflow = 1; return -1; }
+    return at;
+  }
   if (l.heap_top + words > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + words))
     return -1;
   const int at = l.heap_top;
@@ -210,9 +222,25 @@ __device__ __forceinline__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslo
   KPH_END(l, 6);
   return ok;
 }
+// wave mode: a buffer operation is logged (WL words: kind | cur sid << 8 | prev sid << 16, event, prev
+// event, version) and applied in queue order after the round (nfa_wave.h)
+constexpr int WL = 4;
+enum : int32_t { WOP_PUT5 = 1, WOP_PUT3 = 2, WOP_BRANCH = 3 };
+__device__ __forceinline__ void wlog(Lane& l, int kind, int sid, int psid, int ev, int pev, int ver) {
+  if (l.log_n >= l.log_cap) {
+    int32_t capw = l.log_cap * WL;
+    if (!regrow(l, l.log, capw, int64_t(l.log_n) * WL, int64_t(l.log_n + 1) * WL * 2)) return;
+    l.log_cap = capw / WL;
+  }
+  int32_t* o = l.log + l.log_n * WL;
+  o[0] = kind | (sid << 8) | ((psid & 0xFF) << 16);
+  o[1] = ev; o[2] = pev; o[3] = ver;
+  l.log_n++;
+}
 // put 5-arg (SharedVersionedBufferStoreImpl.java:101-126)
 __device__ __forceinline__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_sid, int pev, int ver) {
   if (pev < 0) { l.err = CEP_E_NPE; return; }
+  if (l.wave) { wlog(l, WOP_PUT5, cur_sid, prev_sid, ev, pev, ver); return; }
   const int ps = slot_of(l, prev_sid);
   if (!exists(node(l, ps, pev))) { l.err = CEP_E_ILLEGAL_STATE; return; }
   int32_t* c = node(l, slot_of(l, cur_sid), ev);
@@ -221,6 +249,7 @@ __device__ __forceinline__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_
 }
 // put 3-arg (:149-157): a fresh node overwrites
 __device__ __forceinline__ void buf_put3(Lane& l, int cur_sid, int ev, int ver) {
+  if (l.wave) { wlog(l, WOP_PUT3, cur_sid, 0xFF, ev, -1, ver); return; }
   int32_t* c = node(l, slot_of(l, cur_sid), ev);
   c[0] = 1; c[1] = -1; c[2] = -1; c[3] = NF_EXISTS;
   add_pred(l, c, ver, -1, 0);
@@ -244,6 +273,7 @@ __device__ __forceinline__ int first_compatible(const Lane& l, const int32_t* nd
 // branch (:132-142)
 __device__ __forceinline__ void buf_branch(Lane& l, int sid, int ev, int ver) {
   if (ev < 0) { l.err = CEP_E_NPE; return; }
+  if (l.wave) { wlog(l, WOP_BRANCH, sid, 0xFF, ev, ev, ver); return; }
   int slot = slot_of(l, sid), e = ev, pv = ver;
   for (;;) {
     int32_t* nd = node(l, slot, e);
@@ -431,6 +461,13 @@ __device__ __forceinline__ void eval_event_only(Lane& l) {
   }
 }
 
+// NFA.runs++ (NFA.java:297, :331).  Wave mode: a placeholder -(2 + k) for the lane's k-th increment;
+// the wave numbers them in queue order after the round (nfa_wave.h wave_fix_seq)
+__device__ __forceinline__ int next_seq(Lane& l) {
+  if (l.wave) return -(2 + l.nph++);
+  return ++l.runs;
+}
+
 // queues keep their capacity in runs; regrow works in words
 __device__ __forceinline__ bool push_run(Lane& l, int32_t*& q, int32_t& cap_runs, int32_t& len, const Run& x) {
   if (len >= cap_runs) {
@@ -554,7 +591,7 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
     const int ver = f.cs.ver, seq = f.cs.seq, pev = f.cs.ev;
     if (f.branching) {                                               // :289-317
       if (f.consumed) {
-        const int nseq = ++l.runs;
+        const int nseq = next_seq(l);
         const int last = f.ignored ? pev : l.r;
         if (f.prev_sid < 0) { l.err = CEP_E_NPE; return false; }    // Stage.newEpsilonState(null, ...)
         const bool pb = is_begin(l, f.prev_sid);
@@ -597,7 +634,7 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
     const int csid = r_sid(f.cs), ceps = r_eps(f.cs);
     if (is_begin(l, csid) && !is_forwarding(l, csid, ceps)) {         // begin re-add :323-338
       if (f.consumed) {
-        const int nseq = ++l.runs;
+        const int nseq = next_seq(l);
         int nv = ver;
         if (l.tlen != f.nbase) { nv = dw_add_run(l, ver, 1); if (nv < 0) return false; }
         if (!push_t(l, mk_run(csid, ceps, nv, -1, nseq, false, false))) return false;
@@ -917,11 +954,10 @@ __device__ __forceinline__ int64_t export_state(Lane& l) {
   return int64_t(at);
 }
 
-__device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int seg = (gid >> 6) * A.spread + (gid & 63);
-  if ((gid & 63) >= A.spread || seg >= A.nseg) return;
-  Lane l;
+// Per-key setup shared by the lane kernel and the wave kernel (nfa_wave.h): workspace from the
+// pool, carried state (NFAStoreImpl.find, CEPProcessor.loadNFA :111-124) or NFA.build.  Returns
+// false if the key has nothing to run (its result words are then final).
+__device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg) {
   l.A = &A;
   l.P = A.P;
   l.pool_words = 0;
@@ -929,6 +965,7 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   l.seg0 = A.seg_start[seg];
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
   l.g = l.seg0;
+  l.wave = 0; l.wtop = nullptr; l.log = nullptr; l.log_cap = 0; l.log_n = 0; l.nph = 0; l.wgrow = 0;
   l.cap_hit = 0;
   l.rec_out_top = 0;
   l.rec_nmatch = 0;
@@ -942,11 +979,10 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   A.res_err[seg] = 0;
   A.res_err_rec[seg] = -1;
   if (A.carry) A.res_carry[seg] = -1;
-  // carried state of this key (NFAStoreImpl.find, CEPProcessor.loadNFA :111-124)
   const int32_t* blob = nullptr;
   if (A.carry) {
     const int32_t k = A.key[l.seg0];
-    if (k < 0 || k >= A.max_keys) { atomicAdd(&A.flags[2], 1); return; }
+    if (k < 0 || k >= A.max_keys) { atomicAdd(&A.flags[2], 1); return false; }
     const int64_t bo = A.ctab[k];
     if (bo >= 0) {
       blob = A.cpool + bo;
@@ -971,7 +1007,7 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
     } else {
       atomicAdd(&A.flags[0], 1);
     }
-    return;
+    return false;
   }
   l.hwm = p; p += 3 * HWM_MAX;
   l.nodes = p; p += int64_t(NW) * ns * l.nev;
@@ -989,11 +1025,11 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
       if (l.overflow && (A.last_attempt || l.cap_hit)) {
         A.res_err[seg] = CEP_E_RUN_CAPACITY;
         A.res_err_rec[seg] = A.base + l.seg0;
-        return;
+        return false;
       }
       if (l.overflow) atomicAdd(&A.flags[0], 1);
       A.res_err[seg] = l.err;
-      return;
+      return false;
     }
   } else {
     // NFA.build (NFA.java:73-79), Stages.initialComputationStage (Stages.java:53-60)
@@ -1004,52 +1040,35 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
     l.qlen = 1;
     l.runs = 1;
   }
-  Frame fr[MAXD];
-  int64_t err_rec = -1;
-  const bool proc = A.mode == CEP_MODE_PROCESSOR;
-#ifdef KCEP_PHASES
-  for (int i = 0; i < 11; i++) l.ph[i] = 0;
-#endif
-  int32_t live_max = l.qlen;                                         // live-run high-water mark of the key
-  int64_t evals = 0;
-  const uint64_t t0 = A.profile ? wall_clock64() : 0;
-  for (int i = 0; i < l.L && !l.err && !l.overflow; i++) {
-    const int r = l.C + i;
-    const int64_t g = l.seg0 + i;
-    l.r = r;
-    l.g = g;
-    for (int s = 0; s < ns; s++) { int32_t* nd = node(l, s, r); nd[0] = 0; nd[1] = -1; nd[2] = -1; nd[3] = 0; }
-    if (proc) {
-      if (A.valid && !A.valid[g]) continue;                           // CEPProcessor.java:136-138
-      for (int k = 0; k < l.qlen; k++) l.qa[4 * k] &= ~(1 << 17);      // isIgnored not serialised (Q3)
-      const int h = hwm_find(l, b_topic(l, g));
-      if (h < l.nhwm) {                                                // checkHighWaterMark :152-160
-        const int64_t hw = cw64(l.hwm + 3 * h + 1);
-        if (b_off(l, g) < hw) continue;
-      }
-    }
-    eval_event_only(l);
-    evals += l.qlen;
-    l.rec_out_top = l.out_top;
-    l.rec_nmatch = l.nmatch;
-    if (!step(l, fr)) {
-      if (l.err) err_rec = A.base + g;
-      break;
-    }
-    live_max = l.qlen > live_max ? l.qlen : live_max;
-    if (proc) {
-      const int h = hwm_find(l, b_topic(l, g));
-      if (h == l.nhwm) {
-        if (l.nhwm == HWM_MAX) { l.overflow = 1; break; }
-        l.nhwm++;
-        l.hwm[3 * h] = b_topic(l, g);
-      }
-      const int64_t hw = b_off(l, g) + 1;
-      l.hwm[3 * h + 1] = int32_t(uint32_t(uint64_t(hw)));
-      l.hwm[3 * h + 2] = int32_t(uint32_t(uint64_t(hw) >> 32));
-    }
+  return true;
+}
+
+// CEPProcessor's record filters before the step (:136-138 null key/value, :152-160 high-water
+// mark); false: the record is dropped
+__device__ __forceinline__ bool record_admitted(const Lane& l, int64_t g) {
+  if (l.A->valid && !l.A->valid[g]) return false;
+  const int h = hwm_find(l, b_topic(l, g));
+  return !(h < l.nhwm && b_off(l, g) < cw64(l.hwm + 3 * h + 1));
+}
+// the high-water mark after a processed record; false: too many topics for one key
+__device__ __forceinline__ bool record_hwm(Lane& l, int64_t g) {
+  const int h = hwm_find(l, b_topic(l, g));
+  if (h == l.nhwm) {
+    if (l.nhwm == HWM_MAX) return false;
+    l.nhwm++;
+    l.hwm[3 * h] = b_topic(l, g);
   }
-  if (A.carry && !l.err && !l.overflow) {                              // NFAStoreImpl.put (:144-147)
+  const int64_t hw = b_off(l, g) + 1;
+  l.hwm[3 * h + 1] = int32_t(uint32_t(uint64_t(hw)));
+  l.hwm[3 * h + 2] = int32_t(uint32_t(uint64_t(hw) >> 32));
+  return true;
+}
+
+// Per-key results: carried state (NFAStoreImpl.put :144-147), profile, the capacity hand-off,
+// match counts.
+__device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int64_t err_rec, int32_t live_max,
+                                        int64_t evals, uint64_t t0) {
+  if (A.carry && !l.err && !l.overflow) {
     const int64_t at = export_state(l);
     if (at >= 0) A.res_carry[seg] = at;
   }
@@ -1085,6 +1104,48 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   A.res_matches[seg] = l.nmatch;
   A.res_words[seg] = l.out_top;
   A.res_out[seg] = int64_t(reinterpret_cast<uintptr_t>(l.out));
+}
+
+// One lane runs one key segment (A.spread segments per wave).
+__device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int seg = (gid >> 6) * A.spread + (gid & 63);
+  if ((gid & 63) >= A.spread || seg >= A.nseg) return;
+  Lane l;
+  if (!key_begin(l, A, seg)) return;
+  const auto& P = KCEP_PROG(l);
+  const int ns = P.nslots;
+  Frame fr[MAXD];
+  int64_t err_rec = -1;
+  const bool proc = A.mode == CEP_MODE_PROCESSOR;
+#ifdef KCEP_PHASES
+  for (int i = 0; i < 11; i++) l.ph[i] = 0;
+#endif
+  int32_t live_max = l.qlen;                                         // live-run high-water mark of the key
+  int64_t evals = 0;
+  const uint64_t t0 = A.profile ? wall_clock64() : 0;
+  for (int i = 0; i < l.L && !l.err && !l.overflow; i++) {
+    const int r = l.C + i;
+    const int64_t g = l.seg0 + i;
+    l.r = r;
+    l.g = g;
+    for (int s = 0; s < ns; s++) { int32_t* nd = node(l, s, r); nd[0] = 0; nd[1] = -1; nd[2] = -1; nd[3] = 0; }
+    if (proc) {
+      if (!record_admitted(l, g)) continue;
+      for (int k = 0; k < l.qlen; k++) l.qa[4 * k] &= ~(1 << 17);      // isIgnored not serialised (Q3)
+    }
+    eval_event_only(l);
+    evals += l.qlen;
+    l.rec_out_top = l.out_top;
+    l.rec_nmatch = l.nmatch;
+    if (!step(l, fr)) {
+      if (l.err) err_rec = A.base + g;
+      break;
+    }
+    live_max = l.qlen > live_max ? l.qlen : live_max;
+    if (proc && !record_hwm(l, g)) { l.overflow = 1; break; }
+  }
+  key_end(l, A, seg, err_rec, live_max, evals, t0);
 }
 
 }  // namespace kcep

@@ -1,0 +1,429 @@
+// nfa_wave.h — the general NFA path with one key per wave and one queued run per lane.
+//
+// NFA.matchPattern (nfa/NFA.java:134-149) polls the key's run queue in order and evaluates
+// each run (NFA.evaluate :190-341).  For a pattern without aggregates (no folds, no state reads,
+// no SequenceMatcher -- DevProgram.wave_ok) an evaluation reads nothing another run of the same
+// record writes: edge predicates depend on the record only, Dewey versions are immutable values,
+// and the shared buffer is only written.  The runs of a record are therefore evaluated in rounds
+// of 64, one per lane, and their side effects are committed afterwards in queue order:
+//
+//   * new runs: each lane's results go to a private list; a wave prefix scan gives every lane its
+//     place in the next queue (and in the final-run list, matchConstruction :151-158), so the
+//     queue order is the reference's;
+//   * NFA.runs++ (:297, :331): placeholders, numbered in queue order by a prefix scan;
+//   * buffer puts / branches (SharedVersionedBufferStoreImpl.java:101-157): logged per lane.  If no
+//     run of the round died and none raised, they commute except for the predecessor order of the
+//     current record's nodes: branch walks only touch earlier records' nodes (refs++, atomically;
+//     their predecessor lists cannot change without a remove), and a node of the current record
+//     ends as "the last 3-arg put, then every later 5-arg put, in queue order" -- a contiguous
+//     block of predecessor entries placed by per-node prefix counts.  Otherwise (a dead run's
+//     removePattern :160-163, or an exception) lane 0 replays the round's operations in queue
+//     order with the sequential buffer code, stopping where the reference throws.
+//   * matchConstruction runs on lane 0 after the last round.
+//
+// The key's workspace is the lane kernel's (nfa_dev.h): nodes, queues and heap in the pool, with
+// the heap allocated by an LDS atomic; a round that outgrows the heap is re-run after the wave has
+// doubled it.
+#pragma once
+#include "nfa_dev.h"
+
+namespace kcep {
+
+constexpr int WAVE = 64;
+
+// the key's shared workspace descriptor (LDS); lanes keep register copies in their Lane
+struct WaveShared {
+  int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm;
+  int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs;
+  int64_t nmatch, pool_words;
+  int32_t err, overflow, cap_hit;
+  int32_t* logp[WAVE];
+  int32_t logn[WAVE], errc[WAVE];
+  int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
+  int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
+};
+
+__device__ __forceinline__ void ws_to_lane(Lane& l, const WaveShared& w) {
+  l.nodes = w.nodes; l.heap = w.heap; l.qa = w.qa; l.qb = w.qb; l.fq = w.fq; l.out = w.out; l.hwm = w.hwm;
+  l.heapcap = w.heapcap; l.heap_top = w.heap_top; l.qa_cap = w.qa_cap; l.qb_cap = w.qb_cap; l.fq_cap = w.fq_cap;
+  l.qlen = w.qlen; l.outcap = w.outcap; l.out_top = w.out_top; l.nhwm = w.nhwm; l.runs = w.runs;
+  l.nmatch = w.nmatch; l.err = w.err; l.overflow = w.overflow; l.cap_hit = w.cap_hit;
+}
+__device__ __forceinline__ void lane_to_ws(WaveShared& w, const Lane& l) {
+  w.nodes = l.nodes; w.heap = l.heap; w.qa = l.qa; w.qb = l.qb; w.fq = l.fq; w.out = l.out; w.hwm = l.hwm;
+  w.heapcap = l.heapcap; w.heap_top = l.heap_top; w.qa_cap = l.qa_cap; w.qb_cap = l.qb_cap; w.fq_cap = l.fq_cap;
+  w.qlen = l.qlen; w.outcap = l.outcap; w.out_top = l.out_top; w.nhwm = l.nhwm; w.runs = l.runs;
+  w.nmatch = l.nmatch; w.err = l.err; w.overflow = l.overflow; w.cap_hit = l.cap_hit;
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
+  int x = v;
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  total = __shfl(x, WAVE - 1);
+  return x - v;
+}
+
+// A shared array of `cap` words (used up to `used`) re-allocated at >= need words: lane 0 draws it
+// from the pool, the wave copies.  Returns the new array (nullptr: pool exhausted -> w.overflow).
+__device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared& w, int32_t* a, int32_t& cap, int64_t used,
+                                                int64_t need, int lane) {
+  int64_t nc = int64_t(cap) * 2;
+  if (nc < need) nc = need;
+  __syncthreads();
+  if (lane == 0) {
+    w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc);
+    if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
+    w.pool_words = l.pool_words;
+  }
+  __syncthreads();
+  int32_t* na = w.grown;
+  if (!na) return nullptr;
+  for (int64_t i = lane; i < used; i += WAVE) na[i] = a[i];
+  cap = int32_t(nc);
+  __syncthreads();
+  return na;
+}
+
+__device__ __forceinline__ bool wave_heap_reserve(Lane& l, WaveShared& w, int64_t need_top, int lane) {
+  if (need_top <= w.heapcap) return true;
+  int32_t cap = w.heapcap;
+  int32_t* na = wave_regrow(l, w, w.heap, cap, w.heap_top, need_top, lane);
+  if (!na) return false;
+  if (lane == 0) { w.heap = na; w.heapcap = cap; }
+  __syncthreads();
+  return true;
+}
+
+// the round's buffer operations, none of which can see another's effect (see the header): branch
+// walks with atomic refcounts and the existence checks, then the current record's nodes.  Returns
+// the reference exception of the first failing operation in queue order (CEP_OK if none).
+__device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int lane, int r, int nact) {
+  const auto& P = KCEP_PROG(l);
+  const int ns = P.nslots;
+  // (1) existence of every 5-arg put's predecessor node; branch walks (refs++)
+  int my_err = 0;
+  for (int k = 0; k < l.log_n && !my_err; k++) {
+    const int32_t* o = l.log + k * WL;
+    const int kind = o[0] & 0xFF, sid = (o[0] >> 8) & 0xFF;
+    if (kind == WOP_PUT5) {
+      const int psid = (o[0] >> 16) & 0xFF;
+      if (!exists(node(l, slot_of(l, psid), o[2]))) my_err = CEP_E_ILLEGAL_STATE;
+    } else if (kind == WOP_BRANCH) {                        // branch (:132-142)
+      int slot = slot_of(l, sid), e = o[1], pv = o[3];
+      for (;;) {
+        int32_t* nd = node(l, slot, e);
+        if (!exists(nd)) { my_err = CEP_E_NPE; break; }
+        atomicAdd(nd, 1);
+        const int p = first_compatible(l, nd, pv, nullptr);
+        if (p < 0 || l.heap[p + 1] < 0) break;
+        pv = l.heap[p]; slot = l.heap[p + 1]; e = l.heap[p + 2];
+      }
+    }
+  }
+  const uint64_t em = __ballot(my_err != 0);
+  if (em) return __shfl(my_err, __builtin_ctzll(em));
+  // (2) the current record's nodes: the last 3-arg put of a node overwrites, later 5-arg puts append
+  int before = 0, total = 0;
+  before = wave_excl_scan(l.log_n, lane, total);
+  for (int s = lane; s < ns; s += WAVE) { w.lastp3[s] = -1; w.scnt[s] = 0; }
+  __syncthreads();
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if ((o[0] & 0xFF) == WOP_PUT3) atomicMax(&w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)], before + k);
+  }
+  __syncthreads();
+  auto survives = [&](const int32_t* o, int gi) {
+    const int kind = o[0] & 0xFF;
+    if (kind == WOP_BRANCH) return false;
+    const int lp = w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)];
+    return kind == WOP_PUT3 ? gi == lp : gi > lp;
+  };
+  int npred = 0;
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if (survives(o, before + k)) { atomicAdd(&w.scnt[slot_of(l, (o[0] >> 8) & 0xFF)], 1); npred++; }
+  }
+  int all = 0;
+  wave_excl_scan(npred, lane, all);
+  __syncthreads();
+  if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(PW) * all, lane)) return CEP_OK;   // w.overflow
+  if (lane == 0) {
+    int top = w.heap_top;
+    for (int s = 0; s < ns; s++)
+      if (w.scnt[s]) { w.sblk[s] = top; top += PW * w.scnt[s]; }
+    w.heap_top = top;
+  }
+  __syncthreads();
+  l.heap = w.heap;
+  l.heapcap = w.heapcap;
+  for (int s = 0; s < ns; s++) {                             // uniform loop over the record's slots
+    const int cnt = w.scnt[s];
+    if (!cnt) continue;
+    int mine = 0;
+    for (int k = 0; k < l.log_n; k++) {
+      const int32_t* o = l.log + k * WL;
+      if (survives(o, before + k) && slot_of(l, (o[0] >> 8) & 0xFF) == s) mine++;
+    }
+    int tot = 0;
+    const int ex = wave_excl_scan(mine, lane, tot);
+    int j = 0;
+    for (int k = 0; k < l.log_n; k++) {
+      const int32_t* o = l.log + k * WL;
+      if (!survives(o, before + k) || slot_of(l, (o[0] >> 8) & 0xFF) != s) continue;
+      const int idx = ex + j++;
+      const int p = w.sblk[s] + PW * idx;
+      const int ver = o[3];
+      const bool p3 = (o[0] & 0xFF) == WOP_PUT3;
+      l.heap[p] = ver;                                       // MatchedEvent.addPredecessor
+      l.heap[p + 1] = p3 ? -1 : slot_of(l, (o[0] >> 16) & 0xFF);
+      l.heap[p + 2] = p3 ? 0 : o[2];
+      l.heap[p + 3] = idx + 1 < cnt ? p + PW : -1;
+      l.heap[p + 4] = l.heap[ver];
+      l.heap[p + 5] = l.heap[ver + 1];
+    }
+    if (lane == 0) {
+      int32_t* nd = node(l, s, r);
+      const int last = w.sblk[s] + PW * (cnt - 1);
+      if (w.lastp3[s] >= 0 || !exists(nd)) {                 // overwritten by a 3-arg put, or created: refs 1
+        nd[0] = 1; nd[1] = w.sblk[s]; nd[2] = last; nd[3] = NF_EXISTS;
+      } else {                                               // made by an earlier round: appended to
+        if (nd[1] < 0) nd[1] = w.sblk[s];
+        else l.heap[nd[2] + 3] = w.sblk[s];
+        nd[2] = last;
+      }
+    }
+  }
+  (void)nact;
+  return CEP_OK;
+}
+
+__device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
+  __shared__ WaveShared w;
+  const int lane = threadIdx.x;
+  const int seg = A.wave_seg ? A.wave_seg[blockIdx.x] : int(blockIdx.x);
+  if (seg >= A.nseg) return;
+  Lane l;
+  int ok = 1;
+  if (lane == 0) {
+    ok = key_begin(l, A, seg) ? 1 : 0;
+    if (ok) {
+      lane_to_ws(w, l);
+      w.pool_words = l.pool_words;
+    }
+  }
+  ok = __shfl(ok, 0);
+  if (!ok) return;
+  __syncthreads();
+  if (lane != 0) {
+    l.A = &A; l.P = A.P;
+    l.seg0 = A.seg_start[seg];
+    l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
+    l.wave = 0; l.cap_hit = 0;
+  }
+  // every lane: the key's fixed shape (lane 0's key_begin set it)
+  l.C = __shfl(l.C, 0);
+  l.nev = __shfl(l.nev, 0);
+  l.evw = __shfl(l.evw, 0);
+  l.cev = reinterpret_cast<const int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.cev), 0));
+  l.tq = reinterpret_cast<int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.tq), 0));
+  l.tq_cap = __shfl(l.tq_cap, 0);
+  l.aggs = reinterpret_cast<int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.aggs), 0));
+  l.seqcap = __shfl(l.seqcap, 0);
+  l.runs_delta = __shfl(l.runs_delta, 0);
+  l.pool_words = 0;
+  l.rec_out_top = 0; l.rec_nmatch = 0;
+  l.slm = 0; l.sle = 0; l.flen = 0; l.tlen = 0;
+  ws_to_lane(l, w);
+  // private run lists and operation logs
+  __shared__ int32_t* s_priv;
+  const int q0 = 16;
+  if (lane == 0) {
+    s_priv = pool_alloc(l, int64_t(WAVE) * 4 * (q0 + q0 * WL / 4 + 4));
+    if (!s_priv) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
+  }
+  __syncthreads();
+  const auto& P = KCEP_PROG(l);
+  const int ns = P.nslots;
+  Frame fr[MAXD];
+  int64_t err_rec = -1;
+  const bool proc = A.mode == CEP_MODE_PROCESSOR;
+#ifdef KCEP_PHASES
+  for (int i = 0; i < 11; i++) l.ph[i] = 0;
+#endif
+  int32_t live_max = w.qlen;
+  int64_t evals = 0;
+  const uint64_t t0 = A.profile ? wall_clock64() : 0;
+  if (!w.overflow) {
+    int32_t* pv = s_priv + int64_t(lane) * 4 * (q0 + q0 * WL / 4 + 4);
+    l.tq = pv;
+    l.tq_cap = q0;
+    l.log = pv + 4 * q0;
+    l.log_cap = q0;
+  }
+  l.wtop = &w.heap_top;
+  for (int i = 0; i < l.L && !w.err && !w.overflow; i++) {
+    const int r = l.C + i;
+    const int64_t g = l.seg0 + i;
+    l.r = r;
+    l.g = g;
+    ws_to_lane(l, w);
+    for (int x = lane; x < ns * NW; x += WAVE) {                 // the record's buffer nodes: none yet
+      const int k = x & (NW - 1);
+      l.nodes[(int64_t(r) * ns) * NW + x] = (k == 1 || k == 2) ? -1 : 0;
+    }
+    if (proc) {
+      if (!record_admitted(l, g)) { __syncthreads(); continue; }
+      for (int k = lane; k < w.qlen; k += WAVE) l.qa[4 * k] &= ~(1 << 17);   // isIgnored not serialised (Q3)
+    }
+    __syncthreads();
+    eval_event_only(l);
+    const int n = w.qlen;
+    evals += n;
+    if (lane == 0) { l.rec_out_top = w.out_top; l.rec_nmatch = w.nmatch; }
+    int qn = 0, flen = 0;
+    for (int base = 0; base < n && !w.err && !w.overflow; base += WAVE) {
+      const int my = base + lane;
+      const bool act = my < n;
+      Run run{0, 0, 0, 0};
+      if (act) {
+        const int4 x = reinterpret_cast<const int4*>(l.qa)[my];
+        run = Run{x.x, x.y, x.z, x.w};
+      }
+      const int top0 = w.heap_top;
+      bool good = true;
+      for (;;) {                                               // evaluate; re-run if the heap was short
+        l.heap = w.heap; l.heapcap = w.heapcap;
+        l.tlen = 0; l.log_n = 0; l.nph = 0; l.err = 0; l.overflow = 0; l.wgrow = 0;
+        l.wave = 1;
+        good = true;
+        if (act) good = evaluate(l, run, fr);
+        l.wave = 0;
+        const bool grow = __ballot(l.wgrow) != 0;
+        const bool pool_out = __ballot(l.overflow && !l.wgrow) != 0;
+        if (pool_out) {                                        // a private list could not grow
+          if (lane == 0) w.overflow = 1;
+          const uint64_t ch = __ballot(l.cap_hit);
+          if (lane == 0 && ch) w.cap_hit = 1;
+          break;
+        }
+        if (!grow) break;
+        __syncthreads();
+        if (lane == 0) w.heap_top = top0;
+        __syncthreads();
+        if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, lane)) break;
+      }
+      __syncthreads();
+      if (w.overflow) break;
+      // commit in queue order
+      const bool err_lane = act && !good && l.err;
+      const bool dead = act && good && l.tlen == 0;
+      const uint64_t emask = __ballot(err_lane), dmask = __ballot(dead);
+      const int nact = n - base < WAVE ? n - base : WAVE;
+      if (!emask && !dmask) {
+        const int e = wave_commit_parallel(l, w, lane, r, nact);
+        if (lane == 0 && e) w.err = e;
+        __syncthreads();
+      } else {
+        w.logp[lane] = l.log;
+        w.logn[lane] = l.log_n;
+        w.errc[lane] = err_lane ? l.err : 0;
+        __syncthreads();
+        if (lane == 0) {                                       // the reference's order, sequentially
+          ws_to_lane(l, w);
+          l.err = 0; l.overflow = 0;
+          for (int j = 0; j < nact && !l.err && !l.overflow; j++) {
+            const int32_t* lg = w.logp[j];
+            for (int k = 0; k < w.logn[j] && !l.err && !l.overflow; k++) {
+              const int32_t* o = lg + k * WL;
+              const int kind = o[0] & 0xFF, sid = (o[0] >> 8) & 0xFF, psid = (o[0] >> 16) & 0xFF;
+              if (kind == WOP_PUT5) buf_put5(l, sid, o[1], psid, o[2], o[3]);
+              else if (kind == WOP_PUT3) buf_put3(l, sid, o[1], o[3]);
+              else buf_branch(l, sid, o[1], o[3]);
+            }
+            if (l.err || l.overflow) break;
+            if ((emask >> j) & 1) { l.err = w.errc[j]; break; }
+            if ((dmask >> j) & 1) {                            // removePattern (:160-163)
+              const int4 x = reinterpret_cast<const int4*>(l.qa)[base + j];
+              buf_peek(l, x.x & 0xFF, x.z, x.y, true, nullptr, 0);
+            }
+          }
+          lane_to_ws(w, l);
+          w.pool_words += l.pool_words;
+          l.pool_words = 0;
+        }
+        __syncthreads();
+        ws_to_lane(l, w);
+      }
+      if (w.err || w.overflow) break;
+      // NFA.runs: the round's placeholders in queue order
+      int nrun = 0;
+      const int rb = w.runs + wave_excl_scan(l.nph, lane, nrun);
+      int nf = 0, nq = 0;
+      for (int t = 0; t < l.tlen; t++) {
+        int4* y = reinterpret_cast<int4*>(l.tq) + t;
+        if (y->w < -1) y->w = rb + (-y->w - 2) + 1;
+        if (is_fwd_final(l, y->x & 0xFF, (y->x >> 8) & 0xFF)) nf++; else nq++;
+      }
+      int tf = 0, tq = 0;
+      const int ef = wave_excl_scan(nf, lane, tf), eq = wave_excl_scan(nq, lane, tq);
+      __syncthreads();
+      if (lane == 0) w.runs += nrun;
+      // room in the next queue and the final list
+      if (qn + tq > w.qb_cap) {
+        int32_t capw = w.qb_cap * 4;
+        int32_t* na = wave_regrow(l, w, w.qb, capw, int64_t(qn) * 4, int64_t(qn + tq) * 4, lane);
+        if (!na) break;
+        if (lane == 0) { w.qb = na; w.qb_cap = capw / 4; }
+      }
+      if (flen + tf > w.fq_cap) {
+        int32_t capw = w.fq_cap * 4;
+        int32_t* na = wave_regrow(l, w, w.fq, capw, int64_t(flen) * 4, int64_t(flen + tf) * 4, lane);
+        if (!na) break;
+        if (lane == 0) { w.fq = na; w.fq_cap = capw / 4; }
+      }
+      __syncthreads();
+      int a = qn + eq, b = flen + ef;
+      for (int t = 0; t < l.tlen; t++) {
+        const int4 y = reinterpret_cast<const int4*>(l.tq)[t];
+        if (is_fwd_final(l, y.x & 0xFF, (y.x >> 8) & 0xFF)) reinterpret_cast<int4*>(w.fq)[b++] = y;
+        else reinterpret_cast<int4*>(w.qb)[a++] = y;
+      }
+      qn += tq;
+      flen += tf;
+      __syncthreads();
+    }
+    if (w.err) { err_rec = A.base + g; break; }
+    if (w.overflow) break;
+    // swap the queues; matchConstruction (:151-158) and the high-water mark on lane 0
+    if (lane == 0) {
+      int32_t* t = w.qa; w.qa = w.qb; w.qb = t;
+      const int32_t c = w.qa_cap; w.qa_cap = w.qb_cap; w.qb_cap = c;
+      w.qlen = qn;
+      ws_to_lane(l, w);
+      l.err = 0; l.overflow = 0;
+      for (int k = 0; k < flen && !l.err && !l.overflow; k++) {
+        const int4 y = reinterpret_cast<const int4*>(w.fq)[k];
+        emit_match(l, Run{y.x, y.y, y.z, y.w});
+      }
+      if (!l.err && !l.overflow && proc && !record_hwm(l, g)) l.overflow = 1;
+      lane_to_ws(w, l);
+      w.pool_words += l.pool_words;
+      l.pool_words = 0;
+    }
+    __syncthreads();
+    if (w.err) { err_rec = A.base + g; break; }
+    live_max = w.qlen > live_max ? w.qlen : live_max;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    ws_to_lane(l, w);
+    l.pool_words = w.pool_words;
+    l.wave = 0;
+    key_end(l, A, seg, err_rec, live_max, evals, t0);
+  }
+}
+
+}  // namespace kcep

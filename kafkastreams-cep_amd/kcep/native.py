@@ -28,6 +28,7 @@ BATCH_OFFSETS_MONOTONE = 1
 SESSION_CARRY = 1
 SESSION_INTERPRET = 2
 SESSION_PROFILE = 4
+SESSION_LANE_NFA = 8
 
 
 class CepError(RuntimeError):
@@ -197,7 +198,7 @@ class Session:
     """One ``cep_session`` (one stream task's processor on one GPU)."""
 
     def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0,
-                 carry=False, max_keys=0, interpret=False, profile=False, max_key_words=0):
+                 carry=False, max_keys=0, interpret=False, profile=False, max_key_words=0, lane_nfa=False):
         """``carry=True``: every key's NFA state continues across batches (CEP_SESSION_CARRY);
         key ids must then be dense in [0, max_keys) and record positions are stream positions.
         ``interpret=True``: the built-in interpreting kernels instead of kernels compiled for the
@@ -207,7 +208,7 @@ class Session:
         self.pattern = pattern
         self.h = C.c_void_p()
         flags = ((SESSION_CARRY if carry else 0) | (SESSION_INTERPRET if interpret else 0) |
-                 (SESSION_PROFILE if profile else 0))
+                 (SESSION_PROFILE if profile else 0) | (SESSION_LANE_NFA if lane_nfa else 0))
         o = Opts(device, mode, force_path, flags, max_events, max_keys, 0.0, max_key_words)
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)

@@ -43,11 +43,11 @@ def batches_of(key, cuts):
     return bounds, np.concatenate(order) if order else np.zeros(0, np.int64)
 
 
-def run_carry(ir, key, cols, bounds, mode=N.MODE_PROCESSOR, max_keys=None, sess=None, **kw):
+def run_carry(ir, key, cols, bounds, mode=N.MODE_PROCESSOR, max_keys=None, sess=None, lane_nfa=False, **kw):
     cp = N.CompiledPattern(ir) if sess is None else sess.pattern
     if sess is None:
         sess = N.Session(cp, max(1, max(b - a for a, b in zip(bounds[:-1], bounds[1:]))), mode=mode, carry=True,
-                         max_keys=max_keys or int(key.max()) + 1)
+                         max_keys=max_keys or int(key.max()) + 1, lane_nfa=lane_nfa)
     got = []
     for a, b in zip(bounds[:-1], bounds[1:]):
         if b == a:
@@ -83,10 +83,11 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
 @pytest.mark.parametrize("nbatch", [2, 7])
 @pytest.mark.parametrize("mode", [N.MODE_PROCESSOR, N.MODE_NFA])
 @pytest.mark.parametrize("name,mk,vmax,gen", CASES, ids=[c[0] for c in CASES])
-def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch):
+def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch, lane_nfa):
     per_key = 8 if name in ("c4_any", "any_any") else 25
     key, val = rand_stream(len(name) * 7 + nbatch, 150, per_key, vmax)
     if gen is not None:
@@ -97,7 +98,7 @@ def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch):
     ir = mk().to_ir(PL.I32)
     omode = O.MODE_PROCESSOR if mode == N.MODE_PROCESSOR else O.MODE_NFA_PER_KEY
     want, r, oerr = oracle_run(ir, key, [val], [1], omode)
-    got, sess, gerr = run_carry(ir, key, [val], bounds, mode=mode)
+    got, sess, gerr = run_carry(ir, key, [val], bounds, mode=mode, lane_nfa=lane_nfa)
     assert oerr is None and gerr is None
     assert len(want) > 0
     assert got == want

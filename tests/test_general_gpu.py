@@ -27,7 +27,7 @@ def grouped(fx):
     return out, order
 
 
-def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, interpret=False, **kw):
+def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, interpret=False, lane_nfa=False, **kw):
     p = O.OraclePattern(ir)
     r = O.OracleRun(p, mode)
     oerr = None
@@ -37,7 +37,7 @@ def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, interpret=Fals
         oerr = (e.code, e.record)
     want = [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)]
     cp = N.CompiledPattern(ir)
-    s = N.Session(cp, max(1, len(key)), mode=mode, force_path=force, interpret=interpret)
+    s = N.Session(cp, max(1, len(key)), mode=mode, force_path=force, interpret=interpret, lane_nfa=lane_nfa)
     if force == N.PATH_GENERAL:
         assert s.jit == (not interpret)       # kernel compiled for the pattern unless asked otherwise
     s.push(len(key), np.ascontiguousarray(key, np.int32), [np.ascontiguousarray(c) for c in cols], **kw)
@@ -63,18 +63,33 @@ def run_both(ir, mode, key, cols, coltypes, force=N.PATH_GENERAL, interpret=Fals
 SC = scenarios()
 
 
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
 @pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("fx", SC, ids=[f["name"] for f in SC])
-def test_golden_general(fx, interpret):
+def test_golden_general(fx, interpret, lane_nfa):
     g, order = grouped(fx)
     kw = {k: g[k] for k in ("topic", "partition", "offset", "ts", "valid") if g[k] is not None}
     want, got, oerr, gerr = run_both(bytes.fromhex(fx["ir"]), fx["mode"], g["key"], g["cols"], g["coltypes"],
-                                     interpret=interpret, **kw)
+                                     interpret=interpret, lane_nfa=lane_nfa, **kw)
     assert oerr is None and gerr is None
     assert got == want
-    # and the reference's own expectation, mapped back to the fixture's record indices
-    exp = sorted(tuple(map(tuple, seq_repr(s))) for s in fx["expected"]["sequences"])
-    assert len(got) == len(exp)
+    # and the reference's own expectation, compared directly: each device sequence as its stage
+    # groups (first-seen stage order reversed, Sequence.Builder.build(true)) of fixture records
+    exp = [[(gr["stage"], sorted(gr["events"])) for gr in sq] for sq in fx["expected"]["sequences"]]
+    assert sorted(map(repr, device_sequences(got, order))) == sorted(map(repr, exp))
+
+
+def device_sequences(got, order):
+    out = []
+    for _rec, _key, trav in got:
+        groups, seen = {}, []
+        for nm, r in trav:
+            if nm not in groups:
+                groups[nm] = set()
+                seen.append(nm)
+            groups[nm].add(int(order[r]))
+        out.append([(nm, sorted(groups[nm])) for nm in reversed(seen)])
+    return out
 
 
 def rand_stream(seed, n_keys, per_key, vmax, grouped_keys=True):
@@ -94,10 +109,11 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
 @pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
 @pytest.mark.parametrize("mode", [O.MODE_PROCESSOR, O.MODE_NFA_PER_KEY])
 @pytest.mark.parametrize("name,mk,vmax,gen", CASES, ids=[c[0] for c in CASES])
-def test_random_general(name, mk, vmax, gen, mode, interpret):
+def test_random_general(name, mk, vmax, gen, mode, interpret, lane_nfa):
     per_key = 8 if name in ("c4_any", "any_any") else 30
     key, val = rand_stream(hash(name) % 1000, 300, per_key, vmax)
     if gen is not None:
@@ -109,7 +125,7 @@ def test_random_general(name, mk, vmax, gen, mode, interpret):
     r.process(O.BatchArrays(key, [val], [1]))
     want = [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)]
     cp = N.CompiledPattern(ir)
-    s = N.Session(cp, len(key), mode=gmode, force_path=N.PATH_GENERAL, interpret=interpret)
+    s = N.Session(cp, len(key), mode=gmode, force_path=N.PATH_GENERAL, interpret=interpret, lane_nfa=lane_nfa)
     assert s.jit == (not interpret)
     s.push(len(key), key, [val])
     out = s.collect()
@@ -200,3 +216,18 @@ def test_over_capacity_key_is_handed_back_alone():
     got = product_matches(s, out)
     assert got == [m for m in want if m[1] != 7 or m[0] < rec[0]]
     assert any(m[1] == 7 for m in got) and any(m[1] == 7 and m[0] >= rec[0] for m in want)
+
+
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
+def test_c4_heavy_keys(lane_nfa):
+    """C4 (skip-till-any times(3) + zeroOrMore) keys long enough that one record's run queue holds
+    several rounds of 64 runs on the wave kernel; every match, in order, as the oracle's."""
+    from kcep import synth
+    key, val, _ = synth.c4_stream_np(400, L=16)
+    ir = synth.c4_pattern().to_ir(PL.I32)
+    want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
+    s = N.Session(N.CompiledPattern(ir), len(key), force_path=N.PATH_GENERAL, lane_nfa=lane_nfa)
+    s.push(len(key), key, [val])
+    got = product_matches(s, s.collect())
+    assert got == want and len(want) > 0
+    assert s.live_run_hwm() > 128
