@@ -335,11 +335,14 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // waves per SIMD the register budget is cut for (KCEP_NFA_WAVES, tuning only)
   const char* wenv = getenv("KCEP_NFA_WAVES");
   const int waves = wenv ? std::min(8, std::max(1, atoi(wenv))) : 2;
+  // the same for the wave kernel (KCEP_NFA_WAVE_OCC)
+  const char* oenv = getenv("KCEP_NFA_WAVE_OCC");
+  const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 3;   // measured best on C4 (2: 13.3, 3: 10.8, 4: 11.8 ms)
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
        "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
   kcep::nfa_kernel_body(A);
 }
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void kcep_nfa_wave(kcep::NfaArgs A) {
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()" + std::to_string(wave_occ) + R"())) void kcep_nfa_wave(kcep::NfaArgs A) {
   kcep::nfa_wave_body(A);
 }
 )";

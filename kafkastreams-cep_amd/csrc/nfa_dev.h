@@ -80,6 +80,7 @@ struct Lane {
   int32_t log_cap, log_n;
   int32_t nph;                 // wave: run-counter increments of this lane's run (seq placeholders)
   int32_t wgrow;               // wave: the shared heap was too small (grow it and re-run the round)
+  unsigned long long* wpool;   // wave: the key's pool words, in LDS (every lane allocates for the key)
 #ifdef KCEP_PHASES
   uint64_t ph[11];             // profiling kernels only: clocks in evaluate / predicates / buffer puts+branch /
                                // removePattern / matchConstruction / first_compatible / add_pred / versions,
@@ -102,7 +103,12 @@ struct Lane {
 // every allocation is a multiple of 16 bytes (queues are read as int4)
 __device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words) {
   const int64_t w = (words + 3) & ~int64_t(3);
-  if (l.A->max_key_words > 0 && l.pool_words + w > l.A->max_key_words) { l.overflow = 1; l.cap_hit = 1; return nullptr; }
+  if (l.wpool) {                                   // wave mode: one counter for the key
+    const int64_t was = int64_t(atomicAdd(l.wpool, (unsigned long long)w));
+    if (l.A->max_key_words > 0 && was + w > l.A->max_key_words) { l.overflow = 1; l.cap_hit = 1; return nullptr; }
+  } else if (l.A->max_key_words > 0 && l.pool_words + w > l.A->max_key_words) {
+    l.overflow = 1; l.cap_hit = 1; return nullptr;
+  }
   const unsigned long long at = atomicAdd(l.A->pool_top, (unsigned long long)w);
   if (at + (unsigned long long)w > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
   l.pool_words += w;
@@ -966,6 +972,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg) {
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
   l.g = l.seg0;
   l.wave = 0; l.wtop = nullptr; l.log = nullptr; l.log_cap = 0; l.log_n = 0; l.nph = 0; l.wgrow = 0;
+  l.wpool = nullptr;
   l.cap_hit = 0;
   l.rec_out_top = 0;
   l.rec_nmatch = 0;

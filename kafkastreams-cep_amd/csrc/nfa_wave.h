@@ -19,7 +19,8 @@
 //     block of predecessor entries placed by per-node prefix counts.  Otherwise (a dead run's
 //     removePattern :160-163, or an exception) lane 0 replays the round's operations in queue
 //     order with the sequential buffer code, stopping where the reference throws.
-//   * matchConstruction runs on lane 0 after the last round.
+//   * matchConstruction after the last round: the final runs' buffer walks, 64 at a time, stepped
+//     event by event (wave_emit_matches).
 //
 // The key's workspace is the lane kernel's (nfa_dev.h): nodes, queues and heap in the pool, with
 // the heap allocated by an LDS atomic; a round that outgrows the heap is re-run after the wave has
@@ -35,12 +36,15 @@ constexpr int WAVE = 64;
 struct WaveShared {
   int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm;
   int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs;
-  int64_t nmatch, pool_words;
+  int64_t nmatch;
+  unsigned long long pool_words;   // the key's pool words (every lane allocates for the key)
   int32_t err, overflow, cap_hit;
   int32_t* logp[WAVE];
   int32_t logn[WAVE], errc[WAVE];
   int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
   int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
+  // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
+  int32_t ms_slot[WAVE], ms_e[WAVE], ms_pv[WAVE], ms_cnt[WAVE], ms_done[WAVE], ms_err[WAVE];
 };
 
 __device__ __forceinline__ void ws_to_lane(Lane& l, const WaveShared& w) {
@@ -76,7 +80,6 @@ __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared& w, int32_t*
   if (lane == 0) {
     w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc);
     if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
-    w.pool_words = l.pool_words;
   }
   __syncthreads();
   int32_t* na = w.grown;
@@ -200,6 +203,135 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
   return CEP_OK;
 }
 
+// matchConstruction (NFA.java:151-158) of the record's final runs, 64 walks at a time in final-run
+// order.  A walk (SharedVersionedBufferStoreImpl.remove -> peek :176-201) persists a change only at
+// a node whose refs are <= 1 (the decrement of a copy is written back only at 0, Q4); nodes with
+// refs >= 2 stay so for the whole construction and are read-only.  Walks step to strictly earlier
+// events, so the walks are advanced event by event from the latest one (the frontier): at a
+// read-only node each lane picks its predecessor in parallel; the walks standing at a changing node
+// are stepped by lane 0 in final-run order -- every walk that will ever reach that node is there,
+// since none is left above the frontier.  The result is the sequential construction's.
+__device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int lane, int flen) {
+  const auto& P = KCEP_PROG(l);
+  const int64_t pos = l.A->base + l.g;
+  const int maxp = l.nev + 1;                                  // one node per event at most
+  for (int base = 0; base < flen; base += WAVE) {
+    const int nact = flen - base < WAVE ? flen - base : WAVE;
+    const bool act = lane < nact;
+    if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(WAVE) * 2 * maxp, lane)) return false;
+    l.heap = w.heap;
+    l.heapcap = w.heapcap;
+    int32_t* paths = w.heap + w.heap_top;                      // scratch above the heap top
+    int32_t* path = paths + lane * 2 * maxp;
+    int slot = 0, e = -1, pv = 0, cnt = 0, my_err = 0;
+    bool done = !act;
+    if (act) {
+      const int4 y = reinterpret_cast<const int4*>(w.fq)[base + lane];
+      slot = slot_of(l, y.x & 0xFF); e = y.z; pv = y.y;
+      if (e < 0) my_err = CEP_E_NPE;
+    }
+    for (;;) {
+      const bool live = !done && !my_err;
+      int fr = live ? e : -1;
+      for (int d = 32; d > 0; d >>= 1) { const int o = __shfl_xor(fr, d); fr = o > fr ? o : fr; }
+      if (fr < 0) break;
+      const bool at = live && e == fr;
+      bool mut = false;
+      if (at) {
+        int32_t* nd = node(l, slot, e);
+        if (!exists(nd)) my_err = CEP_E_NPE;
+        else mut = nd[0] <= 1;
+        if (!my_err && !mut) {                                 // read-only node: a parallel step
+          path[2 * cnt] = slot; path[2 * cnt + 1] = e; cnt++;
+          const int p = first_compatible(l, nd, pv, nullptr);
+          if (p < 0 || l.heap[p + 1] < 0) done = true;
+          else { pv = l.heap[p]; slot = l.heap[p + 1]; e = l.heap[p + 2]; }
+        }
+      }
+      const uint64_t mm = __ballot(at && !my_err && mut);
+      if (mm) {                                                // changing nodes: lane 0, in walk order
+        w.ms_slot[lane] = slot; w.ms_e[lane] = e; w.ms_pv[lane] = pv; w.ms_cnt[lane] = cnt; w.ms_done[lane] = done;
+        w.ms_err[lane] = my_err;
+        __syncthreads();
+        if (lane == 0) {
+          for (uint64_t m = mm; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            const int sj = w.ms_slot[j], ej = w.ms_e[j], c = w.ms_cnt[j];
+            int32_t* nd = node(l, sj, ej);
+            if (!exists(nd)) { w.ms_err[j] = CEP_E_NPE; continue; }
+            int32_t* pj = paths + j * 2 * maxp;
+            pj[2 * c] = sj; pj[2 * c + 1] = ej;
+            w.ms_cnt[j] = c + 1;
+            const bool single = nd[1] < 0 || l.heap[nd[1] + 3] < 0;
+            int pp = -1;
+            const int p = first_compatible(l, nd, w.ms_pv[j], &pp);
+            if (p >= 0) {                                      // refs_left == 0: removePredecessor + put
+              nd[0] = 0;
+              const int nx = l.heap[p + 3];
+              if (pp < 0) nd[1] = nx; else l.heap[pp + 3] = nx;
+              if (nd[2] == p) nd[2] = pp;
+              nd[3] |= NF_EXISTS;
+            } else if (single) {
+              nd[3] &= ~NF_EXISTS;                             // delete
+            }
+            if (p < 0 || l.heap[p + 1] < 0) w.ms_done[j] = 1;
+            else { w.ms_pv[j] = l.heap[p]; w.ms_slot[j] = l.heap[p + 1]; w.ms_e[j] = l.heap[p + 2]; }
+          }
+        }
+        __syncthreads();
+        if ((mm >> lane) & 1) {
+          slot = w.ms_slot[lane]; e = w.ms_e[lane]; pv = w.ms_pv[lane]; cnt = w.ms_cnt[lane];
+          done = w.ms_done[lane]; my_err = w.ms_err[lane];
+        }
+      }
+    }
+    const uint64_t em = __ballot(my_err != 0);
+    if (em) {                                                  // the reference throws at the first failing walk
+      const int code = __shfl(my_err, __builtin_ctzll(em));
+      if (lane == 0) w.err = code;
+      __syncthreads();
+      return true;
+    }
+    // the matches, in final-run order: [pos lo, pos hi, cnt, (name, pos lo, pos hi) x cnt]
+    int total = 0;
+    const int words = act ? 3 + 3 * cnt : 0;
+    const int off = wave_excl_scan(words, lane, total);
+    if (w.out_top + total > w.outcap) {
+      int32_t cap = w.outcap;
+      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, lane);
+      if (!na) return false;
+      if (lane == 0) { w.out = na; w.outcap = cap; }
+      __syncthreads();
+    }
+    if (act) {
+      int32_t* o = w.out + w.out_top + off;
+      o[0] = int32_t(uint32_t(uint64_t(pos)));
+      o[1] = int32_t(uint32_t(uint64_t(pos) >> 32));
+      o[2] = cnt;
+      for (int i = 0; i < cnt; i++) {
+        const int64_t q = ev_pos(l, path[2 * i + 1]);
+        o[3 + 3 * i] = P.slot_name[path[2 * i]];
+        o[4 + 3 * i] = int32_t(uint32_t(uint64_t(q)));
+        o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
+      }
+    }
+    __syncthreads();
+    if (lane == 0) { w.out_top += total; w.nmatch += nact; }
+    __syncthreads();
+  }
+  return true;
+}
+
+// profiling kernels (KCEP_PHASES): lane 0's clocks per phase of the record loop -- record setup,
+// evaluation rounds, buffer commit, run numbering + queue placement, matchConstruction
+#ifdef KCEP_PHASES
+#define KWP_MARK(t) const uint64_t t = clock64()
+#define KWP_ADD(i, t) l.ph[i] += clock64() - t
+#else
+#define KWP_MARK(t)
+#define KWP_ADD(i, t)
+#endif
+
 __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   __shared__ WaveShared w;
   const int lane = threadIdx.x;
@@ -223,6 +355,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
     l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
     l.wave = 0; l.cap_hit = 0;
   }
+  l.wpool = &w.pool_words;
   // every lane: the key's fixed shape (lane 0's key_begin set it)
   l.C = __shfl(l.C, 0);
   l.nev = __shfl(l.nev, 0);
@@ -269,6 +402,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
     const int64_t g = l.seg0 + i;
     l.r = r;
     l.g = g;
+    KWP_MARK(t_rec);
     ws_to_lane(l, w);
     for (int x = lane; x < ns * NW; x += WAVE) {                 // the record's buffer nodes: none yet
       const int k = x & (NW - 1);
@@ -284,6 +418,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
     evals += n;
     if (lane == 0) { l.rec_out_top = w.out_top; l.rec_nmatch = w.nmatch; }
     int qn = 0, flen = 0;
+    KWP_ADD(0, t_rec);
     for (int base = 0; base < n && !w.err && !w.overflow; base += WAVE) {
       const int my = base + lane;
       const bool act = my < n;
@@ -294,6 +429,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       }
       const int top0 = w.heap_top;
       bool good = true;
+      KWP_MARK(t_ev);
       for (;;) {                                               // evaluate; re-run if the heap was short
         l.heap = w.heap; l.heapcap = w.heapcap;
         l.tlen = 0; l.log_n = 0; l.nph = 0; l.err = 0; l.overflow = 0; l.wgrow = 0;
@@ -316,8 +452,10 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, lane)) break;
       }
       __syncthreads();
+      KWP_ADD(1, t_ev);
       if (w.overflow) break;
       // commit in queue order
+      KWP_MARK(t_cm);
       const bool err_lane = act && !good && l.err;
       const bool dead = act && good && l.tlen == 0;
       const uint64_t emask = __ballot(err_lane), dmask = __ballot(dead);
@@ -351,14 +489,14 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
             }
           }
           lane_to_ws(w, l);
-          w.pool_words += l.pool_words;
-          l.pool_words = 0;
         }
         __syncthreads();
         ws_to_lane(l, w);
       }
+      KWP_ADD(2, t_cm);
       if (w.err || w.overflow) break;
       // NFA.runs: the round's placeholders in queue order
+      KWP_MARK(t_pl);
       int nrun = 0;
       const int rb = w.runs + wave_excl_scan(l.nph, lane, nrun);
       int nf = 0, nq = 0;
@@ -394,24 +532,27 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       qn += tq;
       flen += tf;
       __syncthreads();
+      KWP_ADD(3, t_pl);
     }
     if (w.err) { err_rec = A.base + g; break; }
     if (w.overflow) break;
-    // swap the queues; matchConstruction (:151-158) and the high-water mark on lane 0
+    // swap the queues; matchConstruction (:151-158); the high-water mark on lane 0
     if (lane == 0) {
       int32_t* t = w.qa; w.qa = w.qb; w.qb = t;
       const int32_t c = w.qa_cap; w.qa_cap = w.qb_cap; w.qb_cap = c;
       w.qlen = qn;
+    }
+    __syncthreads();
+    KWP_MARK(t_mc);
+    if (flen && !wave_emit_matches(l, w, lane, flen)) {
+      if (lane == 0) w.overflow = 1;
+    }
+    __syncthreads();
+    KWP_ADD(4, t_mc);
+    if (lane == 0 && !w.err && !w.overflow) {
       ws_to_lane(l, w);
-      l.err = 0; l.overflow = 0;
-      for (int k = 0; k < flen && !l.err && !l.overflow; k++) {
-        const int4 y = reinterpret_cast<const int4*>(w.fq)[k];
-        emit_match(l, Run{y.x, y.y, y.z, y.w});
-      }
-      if (!l.err && !l.overflow && proc && !record_hwm(l, g)) l.overflow = 1;
+      if (proc && !record_hwm(l, g)) l.overflow = 1;
       lane_to_ws(w, l);
-      w.pool_words += l.pool_words;
-      l.pool_words = 0;
     }
     __syncthreads();
     if (w.err) { err_rec = A.base + g; break; }
@@ -420,7 +561,8 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   __syncthreads();
   if (lane == 0) {
     ws_to_lane(l, w);
-    l.pool_words = w.pool_words;
+    l.pool_words = int64_t(w.pool_words);
+    l.wpool = nullptr;
     l.wave = 0;
     key_end(l, A, seg, err_rec, live_max, evals, t0);
   }

@@ -196,7 +196,8 @@ def test_null_records_and_high_water_mark():
     assert oerr is None and gerr is None and got == want and len(got) > 0
 
 
-def test_over_capacity_key_is_handed_back_alone():
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
+def test_over_capacity_key_is_handed_back_alone(lane_nfa):
     """a key whose runs outgrow the device capacity falls back per key.  With a small
     per-key workspace cap (cep_opts.max_key_words) the exploding skip-till-any key stops at the record
     where it ran out and is listed by cep_batch_errors with CEP_E_RUN_CAPACITY; its matches before
@@ -208,7 +209,8 @@ def test_over_capacity_key_is_handed_back_alone():
     val = rng.integers(0, 4, len(key)).astype(np.int32)
     ir = PL.any_any().to_ir(PL.I32)
     want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
-    s = N.Session(N.CompiledPattern(ir), len(key), force_path=N.PATH_GENERAL, max_key_words=1 << 15)
+    s = N.Session(N.CompiledPattern(ir), len(key), force_path=N.PATH_GENERAL, max_key_words=1 << 17,
+                  lane_nfa=lane_nfa)
     s.push(len(key), key, [val])
     out = s.collect(raise_on_error=False)
     rec, code = s.batch_errors()

@@ -41,6 +41,9 @@ print("workspace words: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %d; heaviest ke
       (ws.mean(), np.median(ws), np.percentile(ws, 90), np.percentile(ws, 99), ws.max(), ws[o[0]]))
 ph = prof[:, 4:15].astype(np.float64)
 if (ph >= 0).all():
+    tot = ph.sum(axis=0)
+    print("phase clock sums:", [f"{x:.3e}" for x in tot[:8]], "share:",
+          [round(float(x / max(1.0, tot[:5].sum())), 3) for x in tot[:5]])
     names = ["evaluate", "predicates", "buffer put+branch", "removePattern", "matchConstruction", "scans",
              "add_pred", "versions"]
     for sel, nm in ((slice(None), "all keys"), (o[:100], "top-100 keys")):
