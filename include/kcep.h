@@ -98,8 +98,12 @@ typedef struct {
                                 NFAStore/buffer/aggregate stores (CEPProcessor.java:111-124, 144-147): a batch
                                 continues each key's runs, Dewey versions, buffer and folds where the previous
                                 one stopped.  Record positions in cep_matches are then stream positions
-                                (records pushed before the batch + index in the batch).  Runs on the general
-                                path. */
+                                (records pushed before the batch + index in the batch).  Strict fixed-length
+                                patterns stay on the stencil path, which carries only each key's last K-1
+                                records and then takes batches without null records (valid) and with
+                                per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE; the host applies the
+                                high-water-mark rule); every other pattern carries its full NFA state on the
+                                general path. */
 
 #define CEP_SESSION_INTERPRET 2  /* runs path: use the built-in kernels, which interpret the pattern's predicates
                                     and folds, instead of kernels compiled for the pattern at cep_session_open

@@ -29,6 +29,8 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
 int64_t stencil_tiles(int64_t n);
 hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t nm, int32_t* mkey,
                         const StencilProgram* P, unsigned long long* sum, hipStream_t st);
+hipError_t stencil_resolve_launch(const int32_t* key, const int32_t* out, int k, int64_t nm, const StencilCarry& C,
+                                  int64_t* pos, const StencilProgram* P, unsigned long long* sum, hipStream_t st);
 
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf);
 hipError_t nfa_wave_launch(const NfaArgs& A, int64_t nwg, hipStream_t st, hipFunction_t jf);
@@ -162,6 +164,10 @@ struct cep_session {
   DBuf ctab, cpool;             // per key id: blob offset (-1 none); blobs (int32 words)
   DBuf kstamp;                  // per key id: number of the last batch that had a segment of it
   int32_t batch_no = 0;
+  // ---- carried halos of the stencil path (CEP_SESSION_CARRY, kcep_internal.h HaloSlot) ----
+  DBuf halo, hflags, opos;
+  int32_t halo_stamp = 0;
+  int64_t halo_base = 0;        // stream position of the last stencil batch's record 0
   int64_t cpool_words = 0, cpool_used = 0;
   // ---- deterministic runs workspace ----
   DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof;
@@ -184,6 +190,12 @@ struct cep_session {
 };
 
 namespace {
+
+// the halo arguments of the last stencil batch (its stamp and stream position)
+StencilCarry carry_args(const cep_session* s) {
+  return StencilCarry{s->halo.as<HaloSlot>(), s->halo_stamp, int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
+                      s->halo_base, s->hflags.as<unsigned long long>()};
+}
 
 int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const StencilProgram& SP = s->pat->prog.stencil;
@@ -216,7 +228,14 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int64_t ntiles = stencil_tiles(b->n);
   StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic, SP.chain,
                   s->slots.as<int32_t>(), tc, tc + ntiles + 1, s->counter.as<int64_t>(), s->out.as<int32_t>(),
-                  s->out_cap, s->total.as<int64_t>()};
+                  s->out_cap, s->total.as<int64_t>(), StencilCarry{}};
+  if (s->carry) {                                // the keys' halos: read the previous, write the next
+    HIPCHECK(hipMemsetAsync(s->hflags.p, 0, 8, st));
+    L.carry = StencilCarry{s->halo.as<HaloSlot>(), ++s->halo_stamp, int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
+                           s->base, s->hflags.as<unsigned long long>()};
+    s->halo_base = s->base;
+    s->base += b->n;
+  }
   HIPCHECK(stencil_launch(L, s->timing ? s->ev0 : nullptr, s->timing ? s->ev1 : nullptr, st));
   if (s->timing) HIPCHECK(hipEventRecord(s->eb1, st));
   return CEP_OK;
@@ -633,8 +652,8 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   const bool carry = opts->flags & CEP_SESSION_CARRY;
   if (carry && (opts->max_keys <= 0 || opts->max_keys > INT32_MAX))
     return fail(CEP_E_ARG, "carry sessions need max_keys (dense key ids in [0, max_keys))");
-  if (carry && path != CEP_PATH_GENERAL) {
-    if (opts->force_path) return fail(CEP_E_UNSUPPORTED, "carried state runs on the general NFA path");
+  if (carry && path != CEP_PATH_GENERAL && path != CEP_PATH_STENCIL) {   // (chain / runs: not carried yet)
+    if (opts->force_path) return fail(CEP_E_UNSUPPORTED, "carried state runs on the stencil and general paths");
     path = CEP_PATH_GENERAL;
   }
   if (carry && !P.general_ok)
@@ -671,7 +690,12 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
         hipMemcpy(s->dprog.p, &P.dev, sizeof(DevProgram), hipMemcpyHostToDevice))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   }
-  if (carry) {                                   // NFAStore: no key has state yet
+  if (carry && path == CEP_PATH_STENCIL) {       // per key two halo slots, none written yet
+    s->carry = true;
+    if (s->halo.ensure(size_t(opts->max_keys) * 2 * sizeof(HaloSlot)) || s->hflags.ensure(8) ||
+        hipMemset(s->halo.p, 0, size_t(opts->max_keys) * 2 * sizeof(HaloSlot)) || hipMemset(s->hflags.p, 0, 8))
+      return cleanup(fail(CEP_E_HIP, "device allocation failed"));
+  } else if (carry) {                            // NFAStore: no key has state yet
     s->carry = true;
     s->cpool_words = std::max<int64_t>(int64_t(1) << 20, opts->max_keys * 64);
     if (s->ctab.ensure(size_t(opts->max_keys) * 8) || s->cpool.ensure(size_t(s->cpool_words) * 4) ||
@@ -700,7 +724,7 @@ void cep_session_close(cep_session* s) {
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
-                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
+                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
                   &s->r_errcode, &s->r_endof, &s->r_prof})
     b->release();
   for (auto& c : s->h_cols) c.release();
@@ -808,6 +832,9 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
     s->last_path = s->path;
     return push_stencil(s, b, st);
   }
+  if (s->carry && s->path == CEP_PATH_STENCIL)   // the halo cannot be carried through the general path
+    return fail(CEP_E_UNSUPPORTED, "a stencil carry session takes batches without null records (valid) and with "
+                                   "per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE)");
   if (!P.general_ok)
     return fail(CEP_E_UNSUPPORTED, "batch needs the general NFA path, which this pattern cannot use: " + P.general_why);
   s->last_path = CEP_PATH_GENERAL;
@@ -897,6 +924,22 @@ int cep_collect(cep_session* s, cep_matches* o) {
       HIPCHECK(hipMemcpyAsync(s->match_key.data(), s->mkey.p, size_t(nm) * 4, hipMemcpyDeviceToHost, s->stream));
       HIPCHECK(hipStreamSynchronize(s->stream));
     }
+    // carry sessions: every entry as a stream position (halo entries from the keys' halos)
+    std::vector<int64_t> pos_host;
+    if (s->carry) {
+      unsigned long long hf = 0;
+      HIPCHECK(hipMemcpy(&hf, s->hflags.p, 8, hipMemcpyDeviceToHost));
+      if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+      if (hf & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+    }
+    if (s->carry && nm > 0) {
+      if (s->opos.ensure(size_t(nm) * k * 8)) return fail(CEP_E_HIP, "allocation failed");
+      HIPCHECK(stencil_resolve_launch(s->d_key, s->out.as<int32_t>(), k, nm, carry_args(s), s->opos.as<int64_t>(),
+                                      nullptr, nullptr, s->stream));
+      pos_host.resize(size_t(nm) * k);
+      HIPCHECK(hipMemcpyAsync(pos_host.data(), s->opos.p, pos_host.size() * 8, hipMemcpyDeviceToHost, s->stream));
+      HIPCHECK(hipStreamSynchronize(s->stream));
+    }
     // traversal order of SharedVersionedBufferStoreImpl.peek: final stage first;
     // chain matches carry -1 for the optional stages they skipped
     s->match_record.resize(size_t(nm));
@@ -905,14 +948,14 @@ int cep_collect(cep_session* s, cep_matches* o) {
     s->ent_record.resize(size_t(nm) * k);
     int64_t ne = 0;
     for (int64_t m = 0; m < nm; m++) {
-      s->match_record[m] = s->out_host[m * k + k - 1];
+      s->match_record[m] = s->carry ? pos_host[m * k + k - 1] : s->out_host[m * k + k - 1];
       s->ent_off[m] = ne;
       for (int i = 0; i < k; i++) {
         const int st = k - 1 - i;
         const int32_t r = s->out_host[m * k + st];
-        if (r < 0) continue;
+        if (r == -1) continue;
         s->ent_name[ne] = SP.name[st];
-        s->ent_record[ne] = r;
+        s->ent_record[ne] = s->carry ? pos_host[m * k + st] : r;
         ne++;
       }
     }
@@ -958,8 +1001,14 @@ int cep_checksum(cep_session* s, uint64_t* sum, int64_t* n_matches) {
   nm = std::min(nm, s->out_cap);
   HIPCHECK(hipMemsetAsync(s->sum.p, 0, 8, s->stream));
   const StencilProgram& SP = s->pat->prog.stencil;
-  HIPCHECK(stencil_post(s->d_key, s->out.as<int32_t>(), SP.k, nm, nullptr, s->prog.as<StencilProgram>(),
-                        s->sum.as<unsigned long long>(), s->stream));
+  if (s->carry) {                                  // over stream positions
+    if (s->opos.ensure(size_t(std::max<int64_t>(nm, 1)) * SP.k * 8)) return fail(CEP_E_HIP, "allocation failed");
+    HIPCHECK(stencil_resolve_launch(s->d_key, s->out.as<int32_t>(), SP.k, nm, carry_args(s), s->opos.as<int64_t>(),
+                                    s->prog.as<StencilProgram>(), s->sum.as<unsigned long long>(), s->stream));
+  } else {
+    HIPCHECK(stencil_post(s->d_key, s->out.as<int32_t>(), SP.k, nm, nullptr, s->prog.as<StencilProgram>(),
+                          s->sum.as<unsigned long long>(), s->stream));
+  }
   uint64_t h = 0;
   HIPCHECK(hipMemcpyAsync(&h, s->sum.p, 8, hipMemcpyDeviceToHost, s->stream));
   HIPCHECK(hipStreamSynchronize(s->stream));
@@ -980,6 +1029,72 @@ int need_carry(cep_session* s) {
 }
 }  // namespace
 
+// stencil carry sessions: "KCSH", version 1, int64 next stream position, int32 key count, then per key
+// with a halo: int32 key id, int32 records, uint64 stage masks, int64 stream positions[records]
+constexpr uint32_t kHaloMagic = 0x4853434Bu;   // "KCSH"
+bool halo_session(const cep_session* s) { return s->carry && s->path == CEP_PATH_STENCIL; }
+const HaloSlot* halo_newest(const HaloSlot* h) { return h[1].stamp > h[0].stamp ? h + 1 : h; }
+
+int halo_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed) {
+  std::vector<HaloSlot> tab(size_t(std::max(0, key_hi - key_lo)) * 2);
+  if (!tab.empty())
+    HIPCHECK(hipMemcpy(tab.data(), s->halo.as<HaloSlot>() + 2 * int64_t(key_lo), tab.size() * sizeof(HaloSlot),
+                       hipMemcpyDeviceToHost));
+  size_t bytes = 20;
+  int32_t nkeys = 0;
+  for (size_t i = 0; i < tab.size(); i += 2) {
+    const HaloSlot* h = halo_newest(&tab[i]);
+    if (h->stamp > 0 && h->cnt > 0) { bytes += 16 + 8 * size_t(h->cnt); nkeys++; }
+  }
+  *needed = bytes;
+  if (!buf) return CEP_OK;
+  if (cap < bytes) return fail(CEP_E_ARG, "export buffer too small");
+  uint8_t* p = static_cast<uint8_t*>(buf);
+  const uint32_t ver = 1;
+  memcpy(p, &kHaloMagic, 4); memcpy(p + 4, &ver, 4); memcpy(p + 8, &s->base, 8); memcpy(p + 16, &nkeys, 4);
+  p += 20;
+  for (size_t i = 0; i < tab.size(); i += 2) {
+    const HaloSlot* h = halo_newest(&tab[i]);
+    if (h->stamp <= 0 || h->cnt <= 0) continue;
+    const int32_t k = key_lo + int32_t(i / 2);
+    memcpy(p, &k, 4); memcpy(p + 4, &h->cnt, 4); memcpy(p + 8, &h->masks, 8);
+    memcpy(p + 16, h->pos, 8 * size_t(h->cnt));
+    p += 16 + 8 * size_t(h->cnt);
+  }
+  return CEP_OK;
+}
+
+int halo_import(cep_session* s, const uint8_t* p, size_t len) {
+  int64_t base;
+  int32_t nkeys;
+  memcpy(&base, p + 8, 8); memcpy(&nkeys, p + 16, 4);
+  const int K = s->pat->prog.stencil.k;
+  std::vector<std::pair<int32_t, HaloSlot>> rows;
+  size_t at = 20;
+  if (s->halo_stamp == 0) s->halo_stamp = 1;     // imported slots count as written before the next batch
+  for (int32_t i = 0; i < nkeys; i++) {
+    if (at + 16 > len) return fail(CEP_E_ARG, "truncated state blob");
+    HaloSlot h{};
+    int32_t k;
+    memcpy(&k, p + at, 4); memcpy(&h.cnt, p + at + 4, 4); memcpy(&h.masks, p + at + 8, 8);
+    if (k < 0 || k >= s->opts.max_keys || h.cnt < 0 || h.cnt > K - 1 || at + 16 + 8 * size_t(h.cnt) > len)
+      return fail(CEP_E_ARG, "bad key entry in the state blob");
+    memcpy(h.pos, p + at + 16, 8 * size_t(h.cnt));
+    h.stamp = s->halo_stamp;
+    rows.push_back({k, h});
+    at += 16 + 8 * size_t(h.cnt);
+  }
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  const HaloSlot empty{};
+  for (auto& r : rows) {
+    HaloSlot two[2] = {r.second, empty};
+    HIPCHECK(hipMemcpy(s->halo.as<HaloSlot>() + 2 * int64_t(r.first), two, sizeof two, hipMemcpyHostToDevice));
+  }
+  s->base = std::max(s->base, base);
+  return CEP_OK;
+}
+
 int cep_state_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed) {
   int rc = need_carry(s);
   if (rc) return rc;
@@ -988,6 +1103,7 @@ int cep_state_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, 
   if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
   key_lo = std::max<int32_t>(key_lo, 0);
   key_hi = int32_t(std::min<int64_t>(key_hi, s->opts.max_keys));
+  if (halo_session(s)) return halo_export(s, key_lo, key_hi, buf, cap, needed);
   std::vector<int64_t> tab(size_t(std::max(0, key_hi - key_lo)));
   if (!tab.empty()) HIPCHECK(hipMemcpy(tab.data(), s->ctab.as<int64_t>() + key_lo, tab.size() * 8, hipMemcpyDeviceToHost));
   std::vector<int32_t> pool(size_t(s->cpool_used));
@@ -1022,6 +1138,10 @@ int cep_state_import(cep_session* s, const void* buf, size_t len) {
   int64_t base;
   int32_t nkeys;
   memcpy(&magic, p, 4); memcpy(&ver, p + 4, 4); memcpy(&base, p + 8, 8); memcpy(&nkeys, p + 16, 4);
+  if (halo_session(s)) {
+    if (magic != kHaloMagic || ver != 1 || nkeys < 0) return fail(CEP_E_ARG, "bad state blob (stencil sessions take KCSH)");
+    return halo_import(s, p, len);
+  }
   if (magic != kStateMagic || ver != 1 || nkeys < 0) return fail(CEP_E_ARG, "bad state blob");
   const DevProgram& D = s->pat->prog.dev;
   std::vector<std::pair<int32_t, size_t>> keys;    // key, byte offset of its blob
@@ -1068,9 +1188,14 @@ int cep_state_clear(cep_session* s) {
   if (rc) return rc;
   HIPCHECK(hipSetDevice(s->device));
   if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  s->base = 0;
+  if (halo_session(s)) {
+    HIPCHECK(hipMemset(s->halo.p, 0, size_t(s->opts.max_keys) * 2 * sizeof(HaloSlot)));
+    s->halo_stamp = 0;
+    return CEP_OK;
+  }
   HIPCHECK(hipMemset(s->ctab.p, 0xFF, size_t(s->opts.max_keys) * 8));
   s->cpool_used = 0;
-  s->base = 0;
   return CEP_OK;
 }
 
@@ -1078,6 +1203,8 @@ int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len
   int rc = need_carry(s);
   if (rc) return rc;
   if (!runs || !queue_len || key < 0 || key >= s->opts.max_keys) return fail(CEP_E_ARG, "bad argument");
+  if (halo_session(s))
+    return fail(CEP_E_UNSUPPORTED, "a stencil carry session keeps each key's last records, not its NFA runs");
   HIPCHECK(hipSetDevice(s->device));
   if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
   int64_t off = -1;

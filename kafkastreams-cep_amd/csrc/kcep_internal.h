@@ -111,6 +111,30 @@ struct Program {
   StencilProgram stencil{};
 };
 
+// ---- carried state of the stencil / chain paths (CEP_SESSION_CARRY) ----
+// A strict fixed-length match needs only the key's last K-1 records from earlier batches (SURVEY
+// Q9): per key two slots (the batch that wrote it, its records oldest first: stage masks and
+// stream positions).  A batch reads the newer slot written before it and writes the other one,
+// so readers and the writer of one key never touch the same slot.
+struct HaloSlot {
+  int32_t stamp;                     // batch number that wrote the slot, 0 = never
+  int32_t cnt;                       // records held (<= K-1)
+  uint64_t masks;                    // byte h: stage mask of record h
+  int64_t pos[STENCIL_MAX_K - 1];    // byte h: stream position of record h
+};
+struct StencilCarry {
+  HaloSlot* halo;                    // 2 slots per key id
+  int32_t stamp;                     // this batch's number (>= 1)
+  int32_t max_keys;
+  int64_t base;                      // stream position of batch record 0
+  unsigned long long* flags;         // bit 0: key id out of range, bit 1: a key in two segments
+};
+KCEP_HD inline const HaloSlot* halo_old(const HaloSlot* h, int32_t stamp) {
+  // the newer slot written before batch `stamp` (or an empty one)
+  const int32_t a = h[0].stamp < stamp ? h[0].stamp : -1, b = h[1].stamp < stamp ? h[1].stamp : -1;
+  return a >= b ? h : h + 1;
+}
+
 // ---- launch interfaces shared by abi.cpp and the .hip files ----
 struct StencilLaunch {
   const int32_t* key;
@@ -126,6 +150,7 @@ struct StencilLaunch {
   int32_t* out;                   // contiguous output, k ints per match
   int64_t out_cap;                // matches
   int64_t* total;                 // device: number of matches
+  StencilCarry carry;             // halo != nullptr: carry session
 };
 
 // compile.cpp

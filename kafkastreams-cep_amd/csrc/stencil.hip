@@ -251,11 +251,55 @@ struct ChainEnds {
   }
 };
 
-template <int K, class VT, bool TOPIC, bool CHAIN>
+// Carry sessions (CARRY): record j is a "boundary" record when fewer than K-1 records of its key
+// precede it in the batch -- the key's earlier records are in its halo (kcep_internal.h HaloSlot,
+// written by the previous batch that had the key).  The match test then takes the first stages
+// from the halo; the entries of those stages are written as -(1 + d), d = records before the
+// segment's first record (cep_collect resolves them to stream positions).  The thread holding a
+// segment's last record writes the key's new halo into the key's other slot.
+template <int K>
+__device__ __forceinline__ bool halo_match(const StencilCarry& C, int32_t k, int need) {
+  if (k < 0 || k >= C.max_keys) { atomicOr(C.flags, 1ull); return false; }
+  const HaloSlot* h = halo_old(C.halo + 2 * int64_t(k), C.stamp);
+  const int cnt = h->cnt;
+  if (h->stamp <= 0 || cnt < need) return false;
+  const uint64_t m = h->masks;
+  bool ok = true;
+#pragma unroll
+  for (int t = 0; t < K - 1; t++)
+    if (t < need) ok = ok && ((m >> (8 * (cnt - need + t) + t)) & 1);
+  return ok;
+}
+
+// the key's halo after this batch: its last K-1 records (older ones from the previous halo when the
+// segment is shorter); seg = segment records j-seg+1..j (<= K-1), wmk: their stage masks, oldest first
+template <int K>
+__device__ __forceinline__ void halo_write(const StencilCarry& C, int32_t k, int seg, uint64_t wmk, int64_t gj) {
+  if (k < 0 || k >= C.max_keys) { atomicOr(C.flags, 1ull); return; }
+  HaloSlot* h = C.halo + 2 * int64_t(k);
+  const HaloSlot* old = halo_old(h, C.stamp);
+  HaloSlot* nw = old == h ? h + 1 : h;
+  if (atomicMax(&nw->stamp, C.stamp) == C.stamp) { atomicOr(C.flags, 2ull); return; }   // a second segment
+  const int keep = old->stamp > 0 ? (K - 1 - seg < old->cnt ? K - 1 - seg : old->cnt) : 0;
+  uint64_t masks = 0;
+  int c = 0;
+  for (int t = old->cnt - keep; t < old->cnt; t++, c++) {
+    masks |= ((old->masks >> (8 * t)) & 0xFFull) << (8 * c);
+    nw->pos[c] = old->pos[t];
+  }
+  for (int t = 0; t < seg; t++, c++) {
+    masks |= ((wmk >> (8 * t)) & 0xFFull) << (8 * c);
+    nw->pos[c] = C.base + gj - (seg - 1) + t;
+  }
+  nw->masks = masks;
+  nw->cnt = c;
+}
+
+template <int K, class VT, bool TOPIC, bool CHAIN, bool CARRY>
 __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
     const int32_t* __restrict__ key, const VT* __restrict__ val, const int32_t* __restrict__ topic, int64_t n,
     const StencilProgram* __restrict__ P, int32_t* __restrict__ out, int64_t* __restrict__ tile_count,
-    int64_t ntiles) {
+    int64_t ntiles, StencilCarry C) {
   __shared__ __attribute__((aligned(16))) int32_t s_key[ST_KWORDS];   // keys; then the match list
   __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];
   __shared__ int32_t s_wsum[ST_SUB][ST_THREADS / 64];
@@ -290,6 +334,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
   }
 
   uint32_t hits[ST_SUB];
+  uint64_t bneed[CARRY ? ST_SUB : 1];              // carry: halo records of each hit (4 bits per record)
   int excl[ST_SUB], total[ST_SUB];
   uint32_t wpk[CHAIN ? ST_SUB : 1][2 * K], wsame[CHAIN ? ST_SUB : 1];   // chain: the window bits, kept for the write phase
   const uint32_t opt = CHAIN ? uint32_t(P->optmask) : 0u;
@@ -357,6 +402,40 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
             ok = ok && ((wm[w] >> s) & 1) && wk[w] == wk[8 + i];
           }
           hit |= uint32_t(ok) << i;
+        }
+        if constexpr (CARRY) {
+          bneed[j] = 0;
+          const int64_t g0 = base + tid * ST_EPT;            // batch index of own record 0
+          const int32_t nxt = tid + 1 < ST_THREADS ? s_key[kpos(lb + 24)]
+                                                   : (base + ST_TILE < n ? key[base + ST_TILE] : INT32_MIN);
+          for (int i = 0; i < ST_EPT; i++) {
+            if (g0 + i >= n) break;
+            const int32_t kj = wk[8 + i];
+            int o = 0;                                         // same-key records before j in the batch
+#pragma unroll
+            for (int t = 1; t < K; t++)
+              if (o == t - 1 && wk[8 + i - t] == kj) o = t;
+            if (o < K - 1 && !((hit >> i) & 1)) {              // a boundary record: the first stages in the halo
+              const int need = K - 1 - o;
+              bool inb = true;
+#pragma unroll
+              for (int t = 0; t < K; t++)
+                if (t <= o) inb = inb && ((wm[8 + i - o + t] >> (need + t)) & 1);
+              if (inb && halo_match<K>(C, kj, need)) {
+                hit |= 1u << i;
+                bneed[j] |= uint64_t(need) << (4 * i);
+              }
+            }
+            const int32_t kn = i + 1 < ST_EPT ? wk[8 + i + 1] : nxt;
+            if (kn != kj || g0 + i + 1 >= n) {                 // the segment's last record: the new halo
+              const int seg = o + 1 < K - 1 ? o + 1 : K - 1;
+              uint64_t wmk = 0;
+#pragma unroll
+              for (int t = 0; t < K - 1; t++)
+                if (t < seg) wmk |= uint64_t(wm[8 + i - (seg - 1) + t]) << (8 * t);
+              halo_write<K>(C, kj, seg, wmk, g0 + i);
+            }
+          }
         }
         cnt = __popc(hit);
       }
@@ -431,6 +510,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         while (h) {
           const int i = __ffs(h) - 1;
           h &= h - 1;
+          if constexpr (CARRY) s_aux[o] = uint8_t((bneed[j] >> (4 * i)) & 0xF);
           s_match[o++] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
         }
       }
@@ -442,6 +522,9 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         if constexpr (CHAIN) {                      // skipped optional stages: -1
           const uint32_t aux = s_aux[m], d = aux & 3u, cm = aux >> 2;
           rec = ((cm >> s) & 1) ? s_match[m] - int32_t(d) + __popc(cm & ((1u << s) - 1)) : -1;
+        } else if constexpr (CARRY) {                // halo stages: -(1 + records before the segment)
+          const int need = s_aux[m];
+          rec = s < need ? -(1 + (need - s)) : s_match[m] - (K - 1) + s;
         } else {
           rec = s_match[m] - (K - 1) + s;
         }
@@ -472,8 +555,16 @@ template <int K, class VT, bool TP, bool CH>
 static hipError_t launch_kt(const StencilLaunch& L, hipStream_t st) {
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
   const int64_t nsuper = (ntiles + ST_SUB - 1) / ST_SUB;
-  hipLaunchKernelGGL((stencil_kernel<K, VT, TP, CH>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
-                     static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles);
+  if (L.carry.halo) {
+    if constexpr (CH) return hipErrorInvalidValue;   // (chain carry: not compiled)
+    else
+      hipLaunchKernelGGL((stencil_kernel<K, VT, TP, CH, true>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
+                         L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles,
+                         L.carry);
+  } else {
+    hipLaunchKernelGGL((stencil_kernel<K, VT, TP, CH, false>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
+                       static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles, L.carry);
+  }
   return hipGetLastError();
 }
 
@@ -609,6 +700,42 @@ __global__ void stencil_checksum(const int32_t* __restrict__ out, int k, int64_t
   }
   for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
   if ((threadIdx.x & 63) == 0 && h) atomicAdd(sum, (unsigned long long)h);
+}
+
+// carry sessions: every entry as a stream position (int64), halo entries looked up in the key's
+// halo slot the batch read (kcep_internal.h halo_old); -1 stays (a skipped optional stage)
+__global__ void stencil_resolve(const int32_t* __restrict__ key, const int32_t* __restrict__ out, int k, int64_t nm,
+                                StencilCarry C, int64_t* __restrict__ pos) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= nm) return;
+  const int32_t last = out[i * k + k - 1];
+  const HaloSlot* h = halo_old(C.halo + 2 * int64_t(key[last]), C.stamp);
+  for (int s = 0; s < k; s++) {
+    const int32_t r = out[i * k + s];
+    pos[i * k + s] = r >= 0 ? C.base + r : (r == -1 ? -1 : h->pos[h->cnt - (-r - 1)]);
+  }
+}
+__global__ void stencil_checksum_pos(const int64_t* __restrict__ pos, int k, int64_t nm,
+                                     const StencilProgram* __restrict__ P, unsigned long long* __restrict__ sum) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint64_t h = 0;
+  if (i < nm) {
+    h = mix64(uint64_t(pos[i * k + k - 1]) * 0x9e3779b97f4a7c15ULL);
+    for (int s = k - 1; s >= 0; s--) {
+      const int64_t r = pos[i * k + s];
+      if (r >= 0) h = mix64(h ^ (uint64_t(r) << 8) ^ uint64_t(P->name[s]));
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d, 64);
+  if ((threadIdx.x & 63) == 0 && h) atomicAdd(sum, (unsigned long long)h);
+}
+hipError_t stencil_resolve_launch(const int32_t* key, const int32_t* out, int k, int64_t nm, const StencilCarry& C,
+                                  int64_t* pos, const StencilProgram* P, unsigned long long* sum, hipStream_t st) {
+  if (nm <= 0) return hipSuccess;
+  const unsigned blocks = unsigned((nm + 255) / 256);
+  hipLaunchKernelGGL(stencil_resolve, dim3(blocks), dim3(256), 0, st, key, out, k, nm, C, pos);
+  if (sum) hipLaunchKernelGGL(stencil_checksum_pos, dim3(blocks), dim3(256), 0, st, pos, k, nm, P, sum);
+  return hipGetLastError();
 }
 
 hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t nm, int32_t* mkey,

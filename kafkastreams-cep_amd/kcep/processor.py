@@ -60,11 +60,19 @@ _CB_HDR, _CB_NHWM, _CB_QLEN, _CB_NEV, _CB_NCOLS = 12, 3, 4, 5, 10
 
 
 def carried_positions(blob: bytes) -> set:
-    """Stream positions of every event a ``cep_state_export`` blob carries."""
+    """Stream positions of every event a ``cep_state_export`` blob carries: the general path's
+    "KCST" blobs (run queues, buffer nodes, events) or the stencil path's "KCSH" halos (each key's
+    last K-1 records)."""
     hdr = np.frombuffer(blob, np.int32, 5, 0)
     nkeys = int(hdr[4])
     out = set()
     at = 20
+    if blob[:4] == b"KCSH":
+        for _ in range(nkeys):
+            cnt = int(np.frombuffer(blob, np.int32, 1, at + 4)[0])
+            out.update(int(x) for x in np.frombuffer(blob, np.int64, cnt, at + 16))
+            at += 16 + 8 * cnt
+        return out
     for _ in range(nkeys):
         w = int(np.frombuffer(blob, np.int32, 1, at + 4)[0])
         words = np.frombuffer(blob, np.int32, w, at + 8)
@@ -102,6 +110,7 @@ class GpuCEPProcessor:
         self._pending: List[Tuple[int, tuple, int, int, int, int, Event]] = []
         self._log: Dict[int, Event] = {}          # stream position -> Event (carried runs point back here)
         self._failed: Optional[Exception] = None
+        self._hwm: Dict[Tuple[int, int], int] = {}  # stencil sessions: (key id, topic id) -> high-water mark
         self._prune_at = max(int(prune_at), 2 * self.batch_size)   # _log size that triggers a prune
         self._prune_min = self._prune_at
 
@@ -149,6 +158,23 @@ class GpuCEPProcessor:
         if not self._pending:
             return 0
         recs, self._pending = self._pending, []
+        flags = 0
+        if self.session.path in (N.PATH_STENCIL, N.PATH_CHAIN):
+            # the stencil path carries only each key's last records: the high-water-mark rule
+            # (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the
+            # batch handed over has increasing offsets per key and topic.  A strict fixed-length
+            # pattern never throws, so every admitted record is processed and moves the mark.
+            kept = []
+            for r in recs:
+                hk = (r[0], r[2])
+                if r[4] < self._hwm.get(hk, -1):
+                    continue
+                self._hwm[hk] = r[4] + 1
+                kept.append(r)
+            recs = kept
+            flags = N.BATCH_OFFSETS_MONOTONE
+            if not recs:
+                return 0
         n = len(recs)
         kid = np.fromiter((r[0] for r in recs), np.int32, n)
         perm = np.argsort(kid, kind="stable")             # the device wants the batch grouped by key
@@ -162,7 +188,7 @@ class GpuCEPProcessor:
         for i, r in enumerate(sorted_recs):
             self._log[base + i] = r[6]
         try:
-            self.session.push(n, kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts)
+            self.session.push(n, kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts, flags=flags)
             out = self.session.collect(raise_on_error=False)
         except N.CepError as e:                           # no state was committed for this batch:
             self._failed = e                              # the task fails, as the reference's does
@@ -208,7 +234,7 @@ class GpuCEPProcessor:
         and the records carried runs may still reference."""
         self.flush()
         return {"state": self.session.state_export(), "keys": dict(self._keys), "log": dict(self._log),
-                "topics": dict(self.schema.topics)}
+                "topics": dict(self.schema.topics), "hwm": dict(self._hwm)}
 
     def restore(self, snap: dict):
         self._check()
@@ -227,6 +253,7 @@ class GpuCEPProcessor:
         self.session.state_import(snap["state"])
         self._keys = dict(snap["keys"])
         self._log = dict(snap["log"])
+        self._hwm = dict(snap.get("hwm", {}))
 
     def _check(self):
         if self._failed is not None:

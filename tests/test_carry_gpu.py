@@ -102,6 +102,9 @@ def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch, lane_nfa):
     assert oerr is None and gerr is None
     assert len(want) > 0
     assert got == want
+    if sess.path == N.PATH_STENCIL:                     # carries each key's last records, not its runs
+        assert name == "c2_strict"
+        return
     for k in np.unique(key):                            # NFA.getRuns() and queue length per key
         assert sess.key_state(int(k)) == r.state(int(k)), int(k)
 
@@ -203,3 +206,58 @@ def test_interleaved_carry_batch_is_rejected():
     assert [s.key_state(k) for k in range(4)] == before
     s.push(2, np.array([1, 1], np.int32), [np.array([1, 2], np.int32)])   # the session still works
     s.collect()
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8])
+def test_stencil_carry_record_at_a_time(k):
+    """Strict k-stage patterns stay on the stencil path with carried state: each key's last k-1 records
+    (the halo) cross batch boundaries.  Batches of 1, 2 and 5 records: most matches take their first
+    stages from the halo."""
+    rng = np.random.default_rng(k)
+    key = rng.integers(0, 7, 400).astype(np.int32)
+    val = rng.integers(0, 2, 400).astype(np.int32)
+    q = PL.QueryBuilder().select("s0").where(PL.Event.value() == 0)
+    for i in range(1, k):
+        q = q.then().select(f"s{i}").where(PL.Event.value() == (i % 2))
+    ir = q.build().to_ir(PL.I32)
+    want, _, oerr = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    assert oerr is None and len(want) > 0
+    for step in (1, 2, 5):
+        bounds, order = batches_of(key, list(range(step, len(key), step)))
+        got, sess, err = run_carry(ir, key[order], [val[order]], bounds, max_keys=7)
+        assert sess.path == N.PATH_STENCIL and err is None
+        # the device saw the grouped batches: map its stream positions back to arrival order
+        got = [(int(order[m[0]]), m[1], [(nm, int(order[r])) for nm, r in m[2]]) for m in got]
+        assert sorted(got) == sorted(want)
+
+
+def test_stencil_carry_export_import():
+    """A stencil carry session's halos (cep_state_export "KCSH") restored into a fresh session: the
+    rest of the stream continues as in one session."""
+    key, val = rand_stream(21, 300, 20, 4)
+    bounds, order = batches_of(key, [len(key) // 3, 2 * len(key) // 3])
+    key, val = key[order], val[order]
+    ir = synth.c2_pattern().to_ir(PL.I32)
+    whole, s1, _ = run_carry(ir, key, [val], bounds)
+    part1, s2, _ = run_carry(ir, key, [val], bounds[:2])
+    assert s1.path == N.PATH_STENCIL
+    blob = s2.state_export()
+    assert blob[:4] == b"KCSH"
+    s3 = N.Session(N.CompiledPattern(ir), len(key), carry=True, max_keys=300)
+    s3.state_import(blob)
+    assert s3.stream_position() == bounds[1]
+    part2, _, _ = run_carry(ir, key, [val], bounds[1:], sess=s3)
+    assert part1 + part2 == whole and len(part2) > 0
+
+
+def test_stencil_carry_rejects_unclean_batches():
+    ir = synth.c2_pattern().to_ir(PL.I32)
+    s = N.Session(N.CompiledPattern(ir), 10, carry=True, max_keys=4)
+    assert s.path == N.PATH_STENCIL
+    with pytest.raises(N.CepError) as e:
+        s.push(2, np.array([1, 1], np.int32), [np.zeros(2, np.int32)], valid=np.ones(2, np.uint8))
+    assert e.value.code == 12
+    with pytest.raises(N.CepError) as e:                 # interleaved keys: found at collect
+        s.push(3, np.array([1, 2, 1], np.int32), [np.zeros(3, np.int32)])
+        s.collect()
+    assert e.value.code == 11

@@ -55,6 +55,8 @@ class StubSession:
     """Records pushed batches; answers each push with a match for every record whose
     value is in `complete` (traversal = that record alone), plus an optional error."""
 
+    path = N.PATH_GENERAL
+
     def __init__(self, complete=(), err_value=None):
         self.pos = 0
         self.pushes = []

@@ -24,6 +24,7 @@ from kcep.processor import GpuCEPProcessor, ProcessorFailed
 from kcep.sequence import Event as Ev, sequence_from_traversal
 from golden_util import scenarios
 import patterns_lib as PL
+from kcep import synth
 
 pytestmark = pytest.mark.gpu
 
@@ -127,7 +128,7 @@ def oracle_forward(pattern, sch, recs):
 
 
 @pytest.mark.parametrize("name,mk,vmax", [("any_any", PL.any_any, 4), ("next_one_or_more", PL.next_one_or_more, 4),
-                                          ("c3_stock", PL.c3_stock, 7)])
+                                          ("c3_stock", PL.c3_stock, 7), ("c2_strict", synth.c2_pattern, 4)])
 @pytest.mark.parametrize("batch", [7, 256])
 def test_random_streams_vs_oracle(name, mk, vmax, batch):
     recs = random_records(sum(map(ord, name)) * 31 + batch, 40, 1500, vmax)
@@ -140,6 +141,8 @@ def test_random_streams_vs_oracle(name, mk, vmax, batch):
     got = run_proc(proc, recs)
     assert len(want) > 0
     assert got == want
+    if name == "c2_strict":                             # strict fixed-length: the stencil kernel, carried
+        assert proc.compiled.info.stencil_ok
 
 
 def test_checkpoint_restore_mid_stream():
