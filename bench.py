@@ -59,6 +59,8 @@ def parse(argv=None):
                     help="oracle threads for cpu_baseline (default: nproc, every CPU this process may run on)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-input", action="store_true", help="skip the PCIe-inclusive (host buffer) figure")
+    ap.add_argument("--carry-batches", type=int, default=10,
+                    help="stencil/chain: also stream the batch through a carry session in this many batches")
     ap.add_argument("--gather-matches", action="store_true",
                     help="N > 1: after the timed steps, gather every rank's matches to rank 0 (12 B/match) and "
                          "time it")
@@ -261,6 +263,9 @@ def main():
             line["config"]["keys_on_cpu"] = 0                        # no CPU fallback: every key runs on the GPU
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and not args.no_host_input:
             line["pcie_inclusive"] = _pcie_inclusive(sess, n, key, cols, stream, csum)
+        if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and args.carry_batches > 1:
+            line["carry_stream"] = _carry_stream(pat, n, K, key, cols, stream, args.carry_batches, n_matches, csum,
+                                                 value / world)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = _cpu_baseline(args.config, key, cols, ts, ir, args.cpu_threads, n_matches, csum,
                                                  sess, stream)
@@ -291,6 +296,45 @@ def _pcie_inclusive(sess, n, key, cols, stream, csum, steps=3):
     return {"value": n / dt, "unit": "events/s", "ms_per_step": dt * 1e3, "host_memory": "pinned",
             "bytes_per_step": int(hk.numel() * hk.element_size() + sum(c.numel() * c.element_size() for c in hc)),
             "parity": c2 == csum}
+
+
+def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, reps=3):
+    """The same device-resident stream pushed through a CEP_SESSION_CARRY session (the
+    GpuCEPProcessor route) in `nb` consecutive batches: keys cut at batch boundaries continue from
+    their carried halos.  Parity: the batches' matches and checksums (over stream positions) add up
+    to the one-batch run.  Reported beside `value`, never as it."""
+    import torch
+    from kcep import native as N
+    per = -(-n // nb)
+    per = -(-per // 4096) * 4096                     # 16-B aligned batch starts
+    bounds = list(range(0, n, per)) + [n]
+    cs = N.Session(pat, per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K)
+    cs.set_timing(False)
+
+    def one_pass(check):
+        tot_m, tot_c = 0, 0
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            cs.push(b - a, key.data_ptr() + 4 * a, [c.data_ptr() + c.element_size() * a for c in cols],
+                    mem=N.MEM_DEVICE, stream=stream.cuda_stream, flags=N.BATCH_OFFSETS_MONOTONE)
+            if check:
+                m, c = cs.checksum()
+                tot_m, tot_c = tot_m + m, (tot_c + c) & 0xFFFFFFFFFFFFFFFF
+        return tot_m, tot_c
+
+    m, c = one_pass(True)
+    stream.synchronize()
+    times = []
+    for _ in range(reps):
+        cs.state_clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        one_pass(False)
+        stream.synchronize()
+        times.append(time.perf_counter() - t0)
+    dt = min(times)
+    return {"value": n / dt, "unit": "events/s", "batches": len(bounds) - 1, "events_per_batch": per,
+            "ms_per_pass": dt * 1e3, "vs_resident": n / dt / resident, "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain"}.get(cs.path, "general"),
+            "parity": bool(m == n_matches and c == csum), "matches": int(m)}
 
 
 def _pmc_traffic(cfg, n):

@@ -99,7 +99,8 @@ typedef struct {
                                 continues each key's runs, Dewey versions, buffer and folds where the previous
                                 one stopped.  Record positions in cep_matches are then stream positions
                                 (records pushed before the batch + index in the batch).  Strict fixed-length
-                                patterns stay on the stencil path, which carries only each key's last K-1
+                                patterns (with or without optional() stages) stay on the stencil / chain path,
+                                which carries only each key's last K-1
                                 records and then takes batches without null records (valid) and with
                                 per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE; the host applies the
                                 high-water-mark rule); every other pattern carries its full NFA state on the

@@ -164,8 +164,8 @@ struct cep_session {
   DBuf ctab, cpool;             // per key id: blob offset (-1 none); blobs (int32 words)
   DBuf kstamp;                  // per key id: number of the last batch that had a segment of it
   int32_t batch_no = 0;
-  // ---- carried halos of the stencil path (CEP_SESSION_CARRY, kcep_internal.h HaloSlot) ----
-  DBuf halo, hflags, opos;
+  // ---- carried halos of the stencil path (CEP_SESSION_CARRY, kcep_internal.h HaloHdr) ----
+  DBuf halo, hpos, hflags, opos;
   int32_t halo_stamp = 0;
   int64_t halo_base = 0;        // stream position of the last stencil batch's record 0
   int64_t cpool_words = 0, cpool_used = 0;
@@ -193,8 +193,9 @@ namespace {
 
 // the halo arguments of the last stencil batch (its stamp and stream position)
 StencilCarry carry_args(const cep_session* s) {
-  return StencilCarry{s->halo.as<HaloSlot>(), s->halo_stamp, int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
-                      s->halo_base, s->hflags.as<unsigned long long>()};
+  return StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), s->pat->prog.stencil.k - 1, s->halo_stamp,
+                      int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->halo_base,
+                      s->hflags.as<unsigned long long>(), 0};
 }
 
 int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
@@ -231,8 +232,10 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
                   s->out_cap, s->total.as<int64_t>(), StencilCarry{}};
   if (s->carry) {                                // the keys' halos: read the previous, write the next
     HIPCHECK(hipMemsetAsync(s->hflags.p, 0, 8, st));
-    L.carry = StencilCarry{s->halo.as<HaloSlot>(), ++s->halo_stamp, int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
-                           s->base, s->hflags.as<unsigned long long>()};
+    const char* dbg = getenv("KCEP_CARRY_DBG");   // A/B probes of the carry kernel's parts (tools/carry_probe.py)
+    L.carry = StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), SP.k - 1, ++s->halo_stamp,
+                           int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->base,
+                           s->hflags.as<unsigned long long>(), dbg ? atoi(dbg) : 0};
     s->halo_base = s->base;
     s->base += b->n;
   }
@@ -652,8 +655,8 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   const bool carry = opts->flags & CEP_SESSION_CARRY;
   if (carry && (opts->max_keys <= 0 || opts->max_keys > INT32_MAX))
     return fail(CEP_E_ARG, "carry sessions need max_keys (dense key ids in [0, max_keys))");
-  if (carry && path != CEP_PATH_GENERAL && path != CEP_PATH_STENCIL) {   // (chain / runs: not carried yet)
-    if (opts->force_path) return fail(CEP_E_UNSUPPORTED, "carried state runs on the stencil and general paths");
+  if (carry && path == CEP_PATH_RUNS) {          // (runs: not carried yet)
+    if (opts->force_path) return fail(CEP_E_UNSUPPORTED, "carried state runs on the stencil, chain and general paths");
     path = CEP_PATH_GENERAL;
   }
   if (carry && !P.general_ok)
@@ -674,12 +677,15 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   if (P.stencil_ok && path != CEP_PATH_GENERAL) {
     const int k = P.stencil.k;
     const int64_t nt = stencil_tiles(cap);
+    // a run ends at most once, so a batch has at most one match per start: its records, plus on chain
+    // carry sessions the (at most K-1) starts in each batch key's halo
+    const int64_t out_cap = carry && P.stencil.chain ? cap + std::min<int64_t>(cap, opts->max_keys) * (k - 1) : cap;
     if (s->prog.ensure(sizeof(StencilProgram)) || s->status.ensure(sizeof(int64_t) * size_t(2 * nt + 2)) ||
         s->counter.ensure(sizeof(int64_t) * size_t(nt / 1024 + 4)) || s->total.ensure(64) || s->sum.ensure(64) ||
-        s->out.ensure(sizeof(int32_t) * size_t(k) * size_t(cap)) ||
+        s->out.ensure(sizeof(int32_t) * size_t(k) * size_t(out_cap)) ||
         s->slots.ensure(sizeof(int32_t) * size_t(k) * size_t(nt) * 4096))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
-    s->out_cap = cap;
+    s->out_cap = out_cap;
     if (hipMemcpy(s->prog.p, &P.stencil, sizeof(StencilProgram), hipMemcpyHostToDevice) ||
         hipMemset(s->status.p, 0, s->status.cap) || hipMemset(s->counter.p, 0, s->counter.cap) ||
         hipMemset(s->total.p, 0, s->total.cap))
@@ -690,10 +696,11 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
         hipMemcpy(s->dprog.p, &P.dev, sizeof(DevProgram), hipMemcpyHostToDevice))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   }
-  if (carry && path == CEP_PATH_STENCIL) {       // per key two halo slots, none written yet
+  if (carry && (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN)) {   // per key two halo slots, none written yet
     s->carry = true;
-    if (s->halo.ensure(size_t(opts->max_keys) * 2 * sizeof(HaloSlot)) || s->hflags.ensure(8) ||
-        hipMemset(s->halo.p, 0, size_t(opts->max_keys) * 2 * sizeof(HaloSlot)) || hipMemset(s->hflags.p, 0, 8))
+    if (s->halo.ensure(size_t(opts->max_keys) * sizeof(HaloHdr)) || s->hflags.ensure(8) ||
+        s->hpos.ensure(size_t(opts->max_keys) * 2 * size_t(std::max(1, P.stencil.k - 1)) * 8) ||
+        hipMemset(s->halo.p, 0, size_t(opts->max_keys) * sizeof(HaloHdr)) || hipMemset(s->hflags.p, 0, 8))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   } else if (carry) {                            // NFAStore: no key has state yet
     s->carry = true;
@@ -724,7 +731,7 @@ void cep_session_close(cep_session* s) {
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
-                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
+                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
                   &s->r_errcode, &s->r_endof, &s->r_prof})
     b->release();
   for (auto& c : s->h_cols) c.release();
@@ -832,7 +839,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
     s->last_path = s->path;
     return push_stencil(s, b, st);
   }
-  if (s->carry && s->path == CEP_PATH_STENCIL)   // the halo cannot be carried through the general path
+  if (s->carry && (s->path == CEP_PATH_STENCIL || s->path == CEP_PATH_CHAIN))   // the halo cannot be carried through the general path
     return fail(CEP_E_UNSUPPORTED, "a stencil carry session takes batches without null records (valid) and with "
                                    "per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE)");
   if (!P.general_ok)
@@ -931,6 +938,7 @@ int cep_collect(cep_session* s, cep_matches* o) {
       HIPCHECK(hipMemcpy(&hf, s->hflags.p, 8, hipMemcpyDeviceToHost));
       if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
       if (hf & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+      if (hf & 4) return fail(CEP_E_RUN_CAPACITY, "chain carry batch: more runs completing in one tile than its match space");
     }
     if (s->carry && nm > 0) {
       if (s->opos.ensure(size_t(nm) * k * 8)) return fail(CEP_E_HIP, "allocation failed");
@@ -1032,19 +1040,25 @@ int need_carry(cep_session* s) {
 // stencil carry sessions: "KCSH", version 1, int64 next stream position, int32 key count, then per key
 // with a halo: int32 key id, int32 records, uint64 stage masks, int64 stream positions[records]
 constexpr uint32_t kHaloMagic = 0x4853434Bu;   // "KCSH"
-bool halo_session(const cep_session* s) { return s->carry && s->path == CEP_PATH_STENCIL; }
-const HaloSlot* halo_newest(const HaloSlot* h) { return h[1].stamp > h[0].stamp ? h + 1 : h; }
+bool halo_session(const cep_session* s) { return s->carry && (s->path == CEP_PATH_STENCIL || s->path == CEP_PATH_CHAIN); }
+int halo_newest(const HaloHdr& h) { return h.stamp[1] > h.stamp[0] ? 1 : 0; }
 
 int halo_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed) {
-  std::vector<HaloSlot> tab(size_t(std::max(0, key_hi - key_lo)) * 2);
-  if (!tab.empty())
-    HIPCHECK(hipMemcpy(tab.data(), s->halo.as<HaloSlot>() + 2 * int64_t(key_lo), tab.size() * sizeof(HaloSlot),
-                       hipMemcpyDeviceToHost));
+  const int km1 = s->pat->prog.stencil.k - 1;
+  const size_t nk = size_t(std::max(0, key_hi - key_lo));
+  std::vector<HaloHdr> tab(nk);
+  std::vector<int64_t> pos(nk * 2 * size_t(km1));
+  if (nk) {
+    HIPCHECK(hipMemcpy(tab.data(), s->halo.as<HaloHdr>() + key_lo, nk * sizeof(HaloHdr), hipMemcpyDeviceToHost));
+    if (km1)
+      HIPCHECK(hipMemcpy(pos.data(), s->hpos.as<int64_t>() + 2 * int64_t(key_lo) * km1, pos.size() * 8,
+                         hipMemcpyDeviceToHost));
+  }
   size_t bytes = 20;
   int32_t nkeys = 0;
-  for (size_t i = 0; i < tab.size(); i += 2) {
-    const HaloSlot* h = halo_newest(&tab[i]);
-    if (h->stamp > 0 && h->cnt > 0) { bytes += 16 + 8 * size_t(h->cnt); nkeys++; }
+  for (size_t i = 0; i < nk; i++) {
+    const int sl = halo_newest(tab[i]);
+    if (tab[i].stamp[sl] > 0 && tab[i].cnt[sl] > 0) { bytes += 16 + 8 * size_t(tab[i].cnt[sl]); nkeys++; }
   }
   *needed = bytes;
   if (!buf) return CEP_OK;
@@ -1053,13 +1067,14 @@ int halo_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_
   const uint32_t ver = 1;
   memcpy(p, &kHaloMagic, 4); memcpy(p + 4, &ver, 4); memcpy(p + 8, &s->base, 8); memcpy(p + 16, &nkeys, 4);
   p += 20;
-  for (size_t i = 0; i < tab.size(); i += 2) {
-    const HaloSlot* h = halo_newest(&tab[i]);
-    if (h->stamp <= 0 || h->cnt <= 0) continue;
-    const int32_t k = key_lo + int32_t(i / 2);
-    memcpy(p, &k, 4); memcpy(p + 4, &h->cnt, 4); memcpy(p + 8, &h->masks, 8);
-    memcpy(p + 16, h->pos, 8 * size_t(h->cnt));
-    p += 16 + 8 * size_t(h->cnt);
+  for (size_t i = 0; i < nk; i++) {
+    const int sl = halo_newest(tab[i]);
+    const int32_t cnt = tab[i].cnt[sl];
+    if (tab[i].stamp[sl] <= 0 || cnt <= 0) continue;
+    const int32_t k = key_lo + int32_t(i);
+    memcpy(p, &k, 4); memcpy(p + 4, &cnt, 4); memcpy(p + 8, &tab[i].masks[sl], 8);
+    memcpy(p + 16, &pos[(2 * i + size_t(sl)) * size_t(km1)], 8 * size_t(cnt));
+    p += 16 + 8 * size_t(cnt);
   }
   return CEP_OK;
 }
@@ -1069,27 +1084,32 @@ int halo_import(cep_session* s, const uint8_t* p, size_t len) {
   int32_t nkeys;
   memcpy(&base, p + 8, 8); memcpy(&nkeys, p + 16, 4);
   const int K = s->pat->prog.stencil.k;
-  std::vector<std::pair<int32_t, HaloSlot>> rows;
+  struct Row { int32_t k, cnt; uint64_t masks; int64_t pos[STENCIL_MAX_K - 1]; };
+  std::vector<Row> rows;
   size_t at = 20;
   if (s->halo_stamp == 0) s->halo_stamp = 1;     // imported slots count as written before the next batch
   for (int32_t i = 0; i < nkeys; i++) {
     if (at + 16 > len) return fail(CEP_E_ARG, "truncated state blob");
-    HaloSlot h{};
-    int32_t k;
-    memcpy(&k, p + at, 4); memcpy(&h.cnt, p + at + 4, 4); memcpy(&h.masks, p + at + 8, 8);
-    if (k < 0 || k >= s->opts.max_keys || h.cnt < 0 || h.cnt > K - 1 || at + 16 + 8 * size_t(h.cnt) > len)
+    Row r{};
+    memcpy(&r.k, p + at, 4); memcpy(&r.cnt, p + at + 4, 4); memcpy(&r.masks, p + at + 8, 8);
+    if (r.k < 0 || r.k >= s->opts.max_keys || r.cnt < 0 || r.cnt > K - 1 || at + 16 + 8 * size_t(r.cnt) > len)
       return fail(CEP_E_ARG, "bad key entry in the state blob");
-    memcpy(h.pos, p + at + 16, 8 * size_t(h.cnt));
-    h.stamp = s->halo_stamp;
-    rows.push_back({k, h});
-    at += 16 + 8 * size_t(h.cnt);
+    memcpy(r.pos, p + at + 16, 8 * size_t(r.cnt));
+    rows.push_back(r);
+    at += 16 + 8 * size_t(r.cnt);
   }
   HIPCHECK(hipSetDevice(s->device));
   if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
-  const HaloSlot empty{};
-  for (auto& r : rows) {
-    HaloSlot two[2] = {r.second, empty};
-    HIPCHECK(hipMemcpy(s->halo.as<HaloSlot>() + 2 * int64_t(r.first), two, sizeof two, hipMemcpyHostToDevice));
+  for (auto& r : rows) {                         // slot 0 holds the halo, slot 1 is empty
+    HaloHdr h{};
+    h.stamp[0] = s->halo_stamp;
+    h.claim = s->halo_stamp;
+    h.cnt[0] = uint8_t(r.cnt);
+    h.masks[0] = r.masks;
+    HIPCHECK(hipMemcpy(s->halo.as<HaloHdr>() + r.k, &h, sizeof h, hipMemcpyHostToDevice));
+    if (K > 1)
+      HIPCHECK(hipMemcpy(s->hpos.as<int64_t>() + 2 * int64_t(r.k) * (K - 1), r.pos, 8 * size_t(K - 1),
+                         hipMemcpyHostToDevice));
   }
   s->base = std::max(s->base, base);
   return CEP_OK;
@@ -1190,7 +1210,7 @@ int cep_state_clear(cep_session* s) {
   if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
   s->base = 0;
   if (halo_session(s)) {
-    HIPCHECK(hipMemset(s->halo.p, 0, size_t(s->opts.max_keys) * 2 * sizeof(HaloSlot)));
+    HIPCHECK(hipMemset(s->halo.p, 0, size_t(s->opts.max_keys) * sizeof(HaloHdr)));
     s->halo_stamp = 0;
     return CEP_OK;
   }

@@ -115,24 +115,34 @@ struct Program {
 // A strict fixed-length match needs only the key's last K-1 records from earlier batches (SURVEY
 // Q9): per key two slots (the batch that wrote it, its records oldest first: stage masks and
 // stream positions).  A batch reads the newer slot written before it and writes the other one,
-// so readers and the writer of one key never touch the same slot.
-struct HaloSlot {
-  int32_t stamp;                     // batch number that wrote the slot, 0 = never
-  int32_t cnt;                       // records held (<= K-1)
-  uint64_t masks;                    // byte h: stage mask of record h
-  int64_t pos[STENCIL_MAX_K - 1];    // byte h: stream position of record h
+// so readers and the writer of one key never touch the same slot.  What a batch reads is one
+// 32-byte header per key (both slots, dense by key id: consecutive keys of a batch share lines);
+// the stream positions, written per batch and read only when a match reaches into the halo, sit
+// in a separate dense array of (K-1) int64 per key and slot.
+struct HaloHdr {
+  int32_t stamp[2];                  // batch number that wrote slot s, 0 = never
+  int32_t claim;                     // the last batch that had a segment of the key
+  uint8_t cnt[2];                    // records held by slot s (<= K-1)
+  uint8_t pad[2];
+  uint64_t masks[2];                 // byte h of slot s: stage mask of its record h
 };
+static_assert(sizeof(HaloHdr) == 32, "HaloHdr is one 32-byte header per key");
 struct StencilCarry {
-  HaloSlot* halo;                    // 2 slots per key id
+  HaloHdr* hdr;                      // per key id
+  int64_t* pos;                      // [(2 * key + slot) * km1 + h]: stream position of record h
+  int32_t km1;                       // K - 1
   int32_t stamp;                     // this batch's number (>= 1)
   int32_t max_keys;
   int64_t base;                      // stream position of batch record 0
-  unsigned long long* flags;         // bit 0: key id out of range, bit 1: a key in two segments
+  unsigned long long* flags;         // bit 0: key id out of range, bit 1: a key in two segments,
+                                     // bit 2: chain carry batch beyond a tile's match space
+  int32_t dbg;                       // KCEP_CARRY_DBG (A/B probes only): bit 0 no claims, bit 1 no halo
+                                     // loads, bit 2 no halo writes
 };
-KCEP_HD inline const HaloSlot* halo_old(const HaloSlot* h, int32_t stamp) {
+KCEP_HD inline int halo_old(const HaloHdr& h, int32_t stamp) {
   // the newer slot written before batch `stamp` (or an empty one)
-  const int32_t a = h[0].stamp < stamp ? h[0].stamp : -1, b = h[1].stamp < stamp ? h[1].stamp : -1;
-  return a >= b ? h : h + 1;
+  const int32_t a = h.stamp[0] < stamp ? h.stamp[0] : -1, b = h.stamp[1] < stamp ? h.stamp[1] : -1;
+  return a >= b ? 0 : 1;
 }
 
 // ---- launch interfaces shared by abi.cpp and the .hip files ----

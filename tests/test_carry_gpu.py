@@ -102,8 +102,8 @@ def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch, lane_nfa):
     assert oerr is None and gerr is None
     assert len(want) > 0
     assert got == want
-    if sess.path == N.PATH_STENCIL:                     # carries each key's last records, not its runs
-        assert name == "c2_strict"
+    if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):     # carries each key's last records, not its runs
+        assert name == ("c2_strict" if sess.path == N.PATH_STENCIL else "c5_optional")
         return
     for k in np.unique(key):                            # NFA.getRuns() and queue length per key
         assert sess.key_state(int(k)) == r.state(int(k)), int(k)
@@ -261,3 +261,58 @@ def test_stencil_carry_rejects_unclean_batches():
         s.push(3, np.array([1, 2, 1], np.int32), [np.zeros(3, np.int32)])
         s.collect()
     assert e.value.code == 11
+
+
+CHAIN_PATTERNS = {
+    # A B? C where a record can end two runs at once (0 1 2: A B C, and A(1) skip-B C)
+    "abc3": lambda v: (PL.QueryBuilder().select("a").where((v == 0) | (v == 1)).then()
+                       .select("b").optional().where(v == 1).then().select("c").where(v == 2).build()),
+    # A B? C? D: two optional stages, runs reaching back K-1 = 3 records
+    "abcd4": lambda v: (PL.QueryBuilder().select("a").where(v <= 1).then()
+                        .select("b").optional().where(v == 1).then()
+                        .select("c").optional().where((v == 2) | (v == 1)).then()
+                        .select("d").where(v >= 2).build()),
+}
+
+
+@pytest.mark.parametrize("name", list(CHAIN_PATTERNS))
+def test_chain_carry_record_at_a_time(name):
+    """Chain patterns (strict with optional() stages) keep their carried state on the chain path:
+    runs that started in a key's halo are replayed at the key's first records of the next batch.
+    Batches of 1, 2, 3 and 7 records against one oracle run of the whole stream."""
+    rng = np.random.default_rng(len(name))
+    key = rng.integers(0, 5, 600).astype(np.int32)
+    val = rng.integers(0, 4, 600).astype(np.int32)
+    ir = CHAIN_PATTERNS[name](PL.Event.value()).to_ir(PL.I32)
+    want, _, oerr = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    assert oerr is None and len(want) > 0
+    for step in (1, 2, 3, 7):
+        bounds, order = batches_of(key, list(range(step, len(key), step)))
+        got, sess, err = run_carry(ir, key[order], [val[order]], bounds, max_keys=5)
+        assert sess.path == N.PATH_CHAIN and err is None
+        got = [(int(order[m[0]]), m[1], [(nm, int(order[r])) for nm, r in m[2]]) for m in got]
+        # per key the matches keep the reference's order (record, then oldest start first)
+        assert sorted(got) == sorted(want)
+        for k in range(5):
+            assert [m for m in got if m[1] == k] == [m for m in want if m[1] == k]
+
+
+def test_chain_carry_c5_random_cuts_and_export():
+    """C5's pattern streamed in random cuts (arrival order kept by grouping each batch), then a
+    checkpoint (KCSH) restored into a fresh session mid-stream."""
+    key, val = rand_stream(33, 400, 30, 64)
+    ir = synth.c5_pattern().to_ir(PL.I32)
+    rng = np.random.default_rng(4)
+    bounds, order = batches_of(key, list(rng.choice(np.arange(1, len(key)), 9, replace=False)))
+    key, val = key[order], val[order]
+    want, _, _ = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    whole, s1, err = run_carry(ir, key, [val], bounds)
+    assert s1.path == N.PATH_CHAIN and err is None and whole == want and len(want) > 0
+    half = len(bounds) // 2
+    part1, s2, _ = run_carry(ir, key, [val], bounds[:half + 1])
+    blob = s2.state_export()
+    assert blob[:4] == b"KCSH"
+    s3 = N.Session(N.CompiledPattern(ir), len(key), carry=True, max_keys=400)
+    s3.state_import(blob)
+    part2, _, _ = run_carry(ir, key, [val], bounds[half:], sess=s3)
+    assert part1 + part2 == whole
