@@ -51,8 +51,12 @@ hipError_t carry_keycheck_launch(int64_t max_seg, const int64_t* nseg, const int
 hipError_t carry_sizes_launch(const int64_t* ctab, int64_t nkeys, const int32_t* cpool, int64_t* words,
                               hipStream_t st);
 hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st, hipFunction_t jf);
+hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, const int64_t* ent_off,
+                              int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
+                              int64_t* ent_record, hipStream_t st);
 hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
-                               unsigned long long* out, hipStream_t st);
+                               unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
+                               int64_t* scan_tmp, hipStream_t st);
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
                      size_t* tmp_bytes, hipStream_t st);
 hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,
@@ -170,7 +174,7 @@ struct cep_session {
   int64_t halo_base = 0;        // stream position of the last stencil batch's record 0
   int64_t cpool_words = 0, cpool_used = 0;
   // ---- deterministic runs workspace ----
-  DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof;
+  DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof, r_segs, r_blk;
   // kernels compiled for the pattern (jit.cpp); null: the built-in interpreting kernels run
   bool jit_on = false;                     // allowed (not CEP_SESSION_INTERPRET / KCEP_JIT=0)
   std::shared_ptr<const JitModule> jit;    // runs path
@@ -190,6 +194,12 @@ struct cep_session {
 };
 
 namespace {
+
+// an environment switch for A/B runs ("1" on)
+bool getenv_flag(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '1';
+}
 
 // the halo arguments of the last stencil batch (its stamp and stream position)
 StencilCarry carry_args(const cep_session* s) {
@@ -337,7 +347,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   }
   if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
       s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 2) * 8) ||
-      s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->r_endof.ensure(size_t(n) * 4))
+      s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->r_endof.ensure(size_t(n) * 4) ||
+      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) || s->r_blk.ensure(size_t(n / 256 + 2) * 16))
     return fail(CEP_E_HIP, "allocation failed");
   RunsArgs A{};
   A.P = s->dprog.as<DevProgram>();
@@ -351,20 +362,25 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.match_key = s->rk.as<unsigned long long>();
   A.match_cap = n;
   A.err_code = s->r_errcode.as<int32_t>();
-  const unsigned long long init[2] = {0, ~0ull};
+  A.segs = s->r_segs.as<uint32_t>();             // the runs' consumed stages, for runs_expand
+  A.seg_over = ctl + 3;
+  const unsigned long long init[4] = {0, ~0ull, 0, 0};   // matches, first exception, entries, segment overflow
   HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
   HIPCHECK(runs_sim_launch(A, s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), st,
                            s->jit ? s->jit->runs_sim : nullptr));
   HIPCHECK(hipEventRecord(s->ev1, st));
   int64_t* scal0 = s->scal.as<int64_t>();
   HIPCHECK(exclusive_scan(s->flag.as<int64_t>(), n, s->idx.as<int64_t>(), scal0 + 3, s->scan_tmp.as<int64_t>(), st));
+  const int64_t nblk = n / 256 + 2;
   HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->r_endof.as<int32_t>(), n,
-                               s->rk.as<unsigned long long>(), st));
-  unsigned long long res[2];
+                               s->rk.as<unsigned long long>(), s->r_blk.as<int64_t>(), s->r_blk.as<int64_t>() + nblk,
+                               reinterpret_cast<int64_t*>(ctl + 2), s->scan_tmp.as<int64_t>(), st));
+  // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow
+  unsigned long long res[4];
   HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(&res[0], scal0 + 3, 8, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
-  const int64_t nm = int64_t(res[0]);
+  const int64_t nm = int64_t(res[0]), ne = int64_t(res[2]);
   if (nm > n) return fail(CEP_E_RUN_CAPACITY, "more completed runs than records");
   if (res[1] != ~0ull) {                           // the reference's first exception
     const int64_t at = int64_t(res[1] >> 31), j = int64_t(res[1] & 0x7FFFFFFFull);
@@ -376,12 +392,14 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     s->e_rec.push_back(at);                        // the runs path keeps only the first exception
     s->e_code.push_back(code);
   }
-  int bits = 31;
-  while ((int64_t(1) << (bits - 31)) <= n) bits++;
+  int bits = 1;                                    // bits of the completing record
+  while ((int64_t(1) << bits) <= n) bits++;
   size_t tmp_bytes = 0;
   HIPCHECK(runs_sort(nullptr, nullptr, nm, bits, nullptr, &tmp_bytes, st));
-  if (s->rk_tmp.ensure(std::max<size_t>(tmp_bytes, 16)) || s->r_len.ensure(size_t(std::max<int64_t>(nm, 1)) * 8) ||
-      s->r_entoff.ensure(size_t(std::max<int64_t>(nm, 1)) * 8) || s->scan_tmp.ensure(size_t(nm / 1024 + 2) * 8))
+  const size_t nmb = size_t(std::max<int64_t>(nm, 1)), neb = size_t(std::max<int64_t>(ne, 1));
+  if (s->rk_tmp.ensure(std::max<size_t>(tmp_bytes, 16)) || s->r_len.ensure(nmb * 8) || s->r_entoff.ensure(nmb * 8) ||
+      s->scan_tmp.ensure(size_t(nm / 1024 + 2) * 8) || s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) ||
+      s->o_entoff.ensure(nmb * 8) || s->o_name.ensure(neb * 4) || s->o_entrec.ensure(neb * 8))
     return fail(CEP_E_HIP, "allocation failed");
   if (nm > 0)
     HIPCHECK(runs_sort(s->rk.as<unsigned long long>(), s->rk_sorted.as<unsigned long long>(), nm, bits, s->rk_tmp.p,
@@ -391,17 +409,19 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                              s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
                              nullptr, nullptr, nullptr, st, true,
                              s->jit ? s->jit->runs_write : nullptr));
-  const int64_t ne = read_i64(scal + 4, st, &rc);
-  if (rc) return fail(rc, "entry count");
-  const size_t nmb = size_t(std::max<int64_t>(nm, 1)), neb = size_t(std::max<int64_t>(ne, 1));
-  if (s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) || s->o_entoff.ensure(nmb * 8) ||
-      s->o_name.ensure(neb * 4) || s->o_entrec.ensure(neb * 8))
-    return fail(CEP_E_HIP, "allocation failed");
-  HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
-                             s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), s->o_record.as<int64_t>(),
-                             s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
-                             s->o_entrec.as<int64_t>(), st, false,
-                             s->jit ? s->jit->runs_write : nullptr));
+  if (!res[3] && !getenv_flag("KCEP_RUNS_REWALK")) {
+    // the traversals from the stage segments runs_sim recorded
+    HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_entoff.as<int64_t>(),
+                                s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
+                                s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
+  } else {                                         // a run beyond RUNS_MAX_SEGS segments: walk every run again
+    A.segs = nullptr;
+    HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
+                               s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), s->o_record.as<int64_t>(),
+                               s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
+                               s->o_entrec.as<int64_t>(), st, false,
+                               s->jit ? s->jit->runs_write : nullptr));
+  }
   HIPCHECK(hipEventRecord(s->eb1, st));
   s->g_matches = nm;
   s->g_entries = ne;
@@ -731,7 +751,7 @@ void cep_session_close(cep_session* s) {
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
-                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_len, &s->r_entoff,
+                  &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_segs, &s->r_blk, &s->r_len, &s->r_entoff,
                   &s->r_errcode, &s->r_endof, &s->r_prof})
     b->release();
   for (auto& c : s->h_cols) c.release();

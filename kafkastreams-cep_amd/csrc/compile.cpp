@@ -96,6 +96,19 @@ ExprP parse_expr(Reader& r, Program& P, int depth) {
       e->t = T_F64;
       if (e->col >= int(P.coltypes.size())) { r.bad = true; return nullptr; }
       break;
+    case OP_SEQ_AGG: {                        // u8 kind, u16 column, stage name (null: every stage)
+      e->ct = r.get<uint8_t>();
+      e->col = r.get<uint16_t>();
+      bool isnull;
+      if (!r.str(e->sname, isnull)) { r.bad = true; return nullptr; }
+      e->name = isnull ? -1 : 0;              // resolved against the stage names at bytecode time
+      if (e->col >= int(P.coltypes.size()) || e->ct < SEQ_SUM || e->ct > SEQ_LAST) { r.bad = true; return nullptr; }
+      const uint8_t ctype = P.coltypes[e->col];
+      if ((e->ct == SEQ_FIRST || e->ct == SEQ_LAST) && isnull) { r.bad = true; return nullptr; }
+      if (e->ct == SEQ_SUM && ctype == T_F64) { r.bad = true; return nullptr; }   // (DoubleStream.sum: compensated)
+      e->t = e->ct == SEQ_COUNT || e->ct == SEQ_SUM ? T_I64 : ctype;
+      break;
+    }
     case OP_NOT:
       e->a = parse_expr(r, P, depth + 1);
       if (!boo(e->a)) { r.bad = true; return nullptr; }
@@ -472,6 +485,7 @@ bool same_expr(const ExprP& a, const ExprP& b) {
     case OP_CONST_I64: if (a->i64 != b->i64) return false; break;
     case OP_CONST_F64: if (memcmp(&a->f64, &b->f64, sizeof(double)) != 0) return false; break;
     case OP_FIELD: case OP_SEQ_AVG: if (a->col != b->col) return false; break;
+    case OP_SEQ_AGG: if (a->col != b->col || a->sname != b->sname || a->name != b->name) return false; break;
     case OP_STATE_GET: case OP_STATE_GET_OR_ELSE: if (a->name != b->name) return false; break;
     default: break;
   }
@@ -516,7 +530,9 @@ bool disjoint(const ExprP& p, const ExprP& q) {
     }
   return true;
 }
-bool uses_seq(const ExprP& e) { return e && (e->op == OP_SEQ_AVG || uses_seq(e->a) || uses_seq(e->b)); }
+bool uses_seq(const ExprP& e) {
+  return e && (e->op == OP_SEQ_AVG || e->op == OP_SEQ_AGG || uses_seq(e->a) || uses_seq(e->b));
+}
 
 // Strict patterns whose stages never take a branching edge combination
 // (NFA.java:392-397): without IGNORE edges that needs TAKE and PROCEED of a
@@ -552,6 +568,7 @@ void analyse_runs(Program& P) {
 
 // ---------------------------------------------------------------- bytecode
 struct CodeGen {
+  const std::vector<std::string>* names = nullptr;   // stage names (OP_SEQ_AGG filters)
   std::vector<int32_t> code;
   bool ok = true;
   std::string why;
@@ -560,7 +577,7 @@ struct CodeGen {
   static int effect(uint8_t o) {
     switch (o) {
       case BC_PUSH: case BC_FIELD: case BC_EV_KEY: case BC_EV_TS: case BC_EV_OFFSET: case BC_EV_PARTITION:
-      case BC_TOPIC_EQ: case BC_STATE_GET: case BC_FOLD_CURR: case BC_SEQ_AVG: return 1;
+      case BC_TOPIC_EQ: case BC_STATE_GET: case BC_FOLD_CURR: case BC_SEQ_AVG: case BC_SEQ_AGG: return 1;
       case BC_END: case BC_STATE_GET_OR_ELSE: case BC_NOT: case BC_NEG_I32: case BC_NEG_I64: case BC_NEG_F64:
       case BC_I64_TO_I32: case BC_I_TO_F64: case BC_F64_TO_I32: case BC_F64_TO_I64: return 0;
       default: return -1;           // binary operators, POP, and the fall-through of JZ/JNZ_KEEP
@@ -619,6 +636,16 @@ struct CodeGen {
       }
       case OP_FOLD_CURR: op(BC_FOLD_CURR, 0, e->ct); break;
       case OP_SEQ_AVG: op(BC_SEQ_AVG, e->col); break;
+      case OP_SEQ_AGG: {                      // a = column, b = kind; next word: stage name id
+        int sid = SEQ_ANY_STAGE;
+        if (e->name >= 0) {
+          const auto it = std::find(names->begin(), names->end(), e->sname);
+          sid = it == names->end() ? -2 : int(it - names->begin());   // unknown: never present
+        }
+        op(BC_SEQ_AGG, e->col, e->ct);
+        code.push_back(sid);
+        break;
+      }
       case OP_NOT: gen(e->a); op(BC_NOT); break;
       case OP_AND: { gen(e->a); int j = jump(BC_JZ_KEEP); gen(e->b); patch(j); break; }
       case OP_OR: { gen(e->a); int j = jump(BC_JNZ_KEEP); gen(e->b); patch(j); break; }
@@ -656,7 +683,7 @@ struct CodeGen {
 bool event_only(const ExprP& e) {
   if (!e) return true;
   switch (e->op) {
-    case OP_STATE_GET: case OP_STATE_GET_OR_ELSE: case OP_FOLD_CURR: case OP_SEQ_AVG: return false;
+    case OP_STATE_GET: case OP_STATE_GET_OR_ELSE: case OP_FOLD_CURR: case OP_SEQ_AVG: case OP_SEQ_AGG: return false;
     default: return event_only(e->a) && event_only(e->b);
   }
 }
@@ -692,6 +719,7 @@ int lower_general(Program& P, std::string& why) {
   // buffer-node slots: one per (stage name, stage type) pair (Matched.java:31-35)
   std::vector<std::pair<int, int>> slots;
   CodeGen cg;
+  cg.names = &P.names;
   for (auto& s : P.stages) {
     DevStage& d = D.st[s.id];
     d.name = s.name;

@@ -12,6 +12,7 @@
 //   int64_t part(); int32_t topic();
 //   bool state(int idx, int32_t& tag, int64_t& bits);   // false: failure already recorded
 //   bool seq_avg(int col, int64_t& bits);
+//   bool seq_agg(int kind, int col, int stage, int64_t& bits);
 //   void fail(int code);
 //   bool in_fold; int32_t curr_tag; int64_t curr;        // Aggregator's current value
 #pragma once
@@ -151,6 +152,13 @@ __device__ __forceinline__ bool interp(const int32_t* __restrict__ code, int pc,
         st.push(v);
         break;
       }
+      case BC_SEQ_AGG: {
+        int64_t v;
+        if (!env.seq_agg(b, a, code[pc], v)) return false;
+        pc++;
+        st.push(v);
+        break;
+      }
       case BC_JZ_KEEP: if (st.s[0] == 0) pc += 1 + code[pc]; else { st.pop(); pc++; } break;
       case BC_JNZ_KEEP: if (st.s[0] != 0) pc += 1 + code[pc]; else { st.pop(); pc++; } break;
       case BC_POP: st.pop(); break;
@@ -239,6 +247,15 @@ __device__ __forceinline__ bool interp_ls(const int32_t* __restrict__ code_flat,
           if (!env.seq_avg(a, v)) ok = false;
           else st.push(v);
         }
+        break;
+      }
+      case BC_SEQ_AGG: {
+        if (on) {
+          int64_t v;
+          if (!env.seq_agg(b, a, code[pc], v)) ok = false;
+          else st.push(v);
+        }
+        pc++;
         break;
       }
       case BC_JZ_KEEP: case BC_JNZ_KEEP: {

@@ -95,7 +95,7 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
     pc++;
     if (op == BC_END) break;
     if (op == BC_PUSH) pc += 2;
-    else if (op == BC_TOPIC_EQ) pc++;
+    else if (op == BC_TOPIC_EQ || op == BC_SEQ_AGG) pc++;
     else if (op == BC_STATE_GET_OR_ELSE || op == BC_JZ_KEEP || op == BC_JNZ_KEEP) {
       labels.insert(pc + 1 + word(pc));
       pc++;
@@ -168,6 +168,13 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
                  sv(depth).c_str());
         b += buf;
         depth++;
+        break;
+      case BC_SEQ_AGG:
+        snprintf(buf, sizeof buf, "{ int64_t v; if (!env.seq_agg(%d, %d, %d, v)) return false; %s = v; }\n", c, a,
+                 word(pc), sv(depth).c_str());
+        b += buf;
+        depth++;
+        pc++;
         break;
       case BC_JZ_KEEP: case BC_JNZ_KEEP: {         // jump keeps the operand; fall-through pops it
         if (!need(1)) return false;

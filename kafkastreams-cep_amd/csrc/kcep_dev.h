@@ -19,7 +19,7 @@ enum : uint8_t {
   OP_TRUE = 0x01, OP_FALSE = 0x02, OP_CONST_I32 = 0x03, OP_CONST_I64 = 0x04, OP_CONST_F64 = 0x05,
   OP_FIELD = 0x10, OP_EV_KEY = 0x11, OP_EV_TS = 0x12, OP_EV_TOPIC_EQ = 0x13, OP_EV_OFFSET = 0x14,
   OP_EV_PARTITION = 0x15, OP_STATE_GET = 0x20, OP_STATE_GET_OR_ELSE = 0x21, OP_FOLD_CURR = 0x22,
-  OP_SEQ_AVG = 0x23, OP_NOT = 0x30, OP_AND = 0x31, OP_OR = 0x32, OP_ADD = 0x40, OP_SUB = 0x41,
+  OP_SEQ_AVG = 0x23, OP_SEQ_AGG = 0x24, OP_NOT = 0x30, OP_AND = 0x31, OP_OR = 0x32, OP_ADD = 0x40, OP_SUB = 0x41,
   OP_MUL = 0x42, OP_DIV = 0x43, OP_REM = 0x44, OP_NEG = 0x45, OP_EQ = 0x50, OP_NE = 0x51,
   OP_LT = 0x52, OP_LE = 0x53, OP_GT = 0x54, OP_GE = 0x55, OP_CAST = 0x60
 };
@@ -36,7 +36,7 @@ enum : uint8_t { S_STRICT = 0, S_NEXT = 1, S_ANY = 2, S_NULL = 0xFF };
 // (unknown state, / by zero, ...) are raised exactly when Java would.
 enum : uint8_t {
   BC_END = 0, BC_PUSH, BC_FIELD, BC_EV_KEY, BC_EV_TS, BC_EV_OFFSET, BC_EV_PARTITION, BC_TOPIC_EQ,
-  BC_STATE_GET, BC_STATE_GET_OR_ELSE, BC_FOLD_CURR, BC_SEQ_AVG, BC_NOT, BC_JZ_KEEP, BC_JNZ_KEEP, BC_POP,
+  BC_STATE_GET, BC_STATE_GET_OR_ELSE, BC_FOLD_CURR, BC_SEQ_AVG, BC_SEQ_AGG, BC_NOT, BC_JZ_KEEP, BC_JNZ_KEEP, BC_POP,
   BC_ADD_I32, BC_SUB_I32, BC_MUL_I32, BC_DIV_I32, BC_REM_I32, BC_NEG_I32,
   BC_ADD_I64, BC_SUB_I64, BC_MUL_I64, BC_DIV_I64, BC_REM_I64, BC_NEG_I64,
   BC_ADD_F64, BC_SUB_F64, BC_MUL_F64, BC_DIV_F64, BC_REM_F64, BC_NEG_F64,
@@ -47,6 +47,11 @@ enum : uint8_t {
 };
 // instruction word: op | a << 8 | b << 16 (a, b: small operands); BC_PUSH is
 // followed by two words (lo, hi); jumps carry a signed word offset in the next word.
+
+// SequenceMatcher reductions (OP_SEQ_AGG kind): over the partial Sequence's events, or over one
+// stage's (Sequence.getByName(stage).getEvents(), a TreeSet: Sequence.java:57-60, 130-167)
+enum : int { SEQ_SUM = 1, SEQ_COUNT = 2, SEQ_MIN = 3, SEQ_MAX = 4, SEQ_FIRST = 5, SEQ_LAST = 6 };
+constexpr int SEQ_ANY_STAGE = -1;     // BC_SEQ_AGG stage word: no stage filter (-2: a stage that does not exist)
 
 constexpr int NFA_MAX_STAGES = 64;
 constexpr int NFA_MAX_EDGES = 4;
@@ -165,6 +170,12 @@ struct RunsArgs {
   int64_t match_cap;
   unsigned long long* err_min;    // min over failing runs of (record << 31 | start)
   int32_t* err_code;              // per start record (valid where it failed)
+  // runs_sim: the stages a run consumed, as up to RUNS_MAX_SEGS segments per start record j:
+  // segs[j * RUNS_MAX_SEGS + i] = stage << 24 | offset of the segment's first record from j,
+  // terminated by ~0u when shorter (a run's consumed stages never increase, runs.hip); null: off
+  uint32_t* segs;
+  unsigned long long* seg_over;   // set when a run needs more segments or an offset >= 2^24
 };
+constexpr int RUNS_MAX_SEGS = 8;
 
 }  // namespace kcep

@@ -16,6 +16,7 @@ struct Expr {
   int64_t i64 = 0;
   double f64 = 0;
   int col = 0, name = 0;
+  std::string sname;                 // OP_SEQ_AGG: the stage name filter
   std::shared_ptr<Expr> a, b;
 };
 using ExprP = std::shared_ptr<Expr>;

@@ -404,6 +404,64 @@ __device__ __forceinline__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t&
   return true;
 }
 
+// Other SequenceMatcher reductions over the same partial sequence (Sequence.java:57-60, 116-167):
+// every event (stage == SEQ_ANY_STAGE) or one stage's (getByName(stage).getEvents(), null -> NPE),
+// each stage's events a TreeSet (Event.compareTo, Event.java:118-122: duplicates dropped, first /
+// last are its ends).  SUM and COUNT are Java longs (mapToLong(...).sum(), count()); MIN / MAX /
+// FIRST / LAST keep the column's type.
+__device__ __forceinline__ int ev_cmp(const Lane& l, int a, int b) {
+  int64_t x, y;
+  if (ev_topic(l, a) != ev_topic(l, b) || ev_part(l, a) != ev_part(l, b)) { x = ev_ts(l, a); y = ev_ts(l, b); }
+  else { x = ev_off(l, a); y = ev_off(l, b); }
+  return x < y ? -1 : x > y ? 1 : 0;
+}
+__device__ __forceinline__ bool seq_agg(Lane& l, const Ctx& c, int kind, int col, int stage, int64_t& out) {
+  if (c.prev_sid < 0 || c.pev < 0) { l.err = CEP_E_NPE; return false; }
+  const int need = 2 * l.nev + 2;
+  if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need))
+    return false;
+  int32_t* tmp = l.heap + l.heap_top;
+  const int cnt = buf_peek(l, c.prev_sid, c.pev, c.ver, false, tmp, l.nev + 1);
+  if (cnt < 0) return false;
+  const auto& P = KCEP_PROG(l);
+  const int t = P.coltype[col];
+  int64_t n = 0, acc = 0;
+  int pick = -1;                                   // FIRST / LAST: the event chosen so far
+  for (int i = 0; i < cnt; i++) {
+    const int nm = P.slot_name[tmp[2 * i]];
+    if (stage != SEQ_ANY_STAGE && nm != stage) continue;
+    bool dup = false;
+    for (int j = 0; j < i && !dup; j++)
+      dup = P.slot_name[tmp[2 * j]] == nm && ev_same(l, tmp[2 * j + 1], tmp[2 * i + 1]);
+    if (dup) continue;
+    const int ev = tmp[2 * i + 1];
+    if (kind == SEQ_FIRST || kind == SEQ_LAST) {
+      if (pick < 0 || (kind == SEQ_FIRST ? ev_cmp(l, ev, pick) < 0 : ev_cmp(l, ev, pick) > 0)) pick = ev;
+    } else if (kind != SEQ_COUNT) {
+      const int64_t v = ev_field(l, col, t, ev);
+      if (kind == SEQ_SUM) acc += v;
+      else if (n == 0) acc = v;
+      else if (t == T_F64) {                       // Math.min / max on doubles: NaN wins, -0.0 < 0.0
+        const double a = as_f(acc), b = as_f(v);
+        const bool take = a != a ? false : b != b ? true
+                        : kind == SEQ_MIN ? (b < a || (b == 0 && a == 0 && __builtin_signbit(b) && !__builtin_signbit(a)))
+                                          : (b > a || (b == 0 && a == 0 && !__builtin_signbit(b) && __builtin_signbit(a)));
+        if (take) acc = v;
+      } else if (kind == SEQ_MIN ? v < acc : v > acc) {
+        acc = v;
+      }
+    }
+    n++;
+  }
+  if (n == 0) {                                     // no such stage in the sequence: getByName -> null
+    if (stage != SEQ_ANY_STAGE || kind == SEQ_MIN || kind == SEQ_MAX) { l.err = CEP_E_NPE; return false; }
+  }
+  if (kind == SEQ_COUNT) out = n;
+  else if (kind == SEQ_FIRST || kind == SEQ_LAST) out = ev_field(l, col, t, pick);
+  else out = acc;
+  return true;
+}
+
 // interpreter environment of the general kernel: the lane's current record,
 // the evaluating run's aggregates and partial sequence
 struct LaneEnv {
@@ -426,6 +484,9 @@ struct LaneEnv {
     return true;
   }
   __device__ __forceinline__ bool seq_avg(int col, int64_t& v) { return kcep::seq_avg(l, c, col, v); }
+  __device__ __forceinline__ bool seq_agg(int kind, int col, int stage, int64_t& v) {
+    return kcep::seq_agg(l, c, kind, col, stage, v);
+  }
   __device__ __forceinline__ void fail(int code) { l.err = code; }
 };
 

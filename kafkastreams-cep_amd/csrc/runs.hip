@@ -39,11 +39,59 @@ __global__ __launch_bounds__(RT) void runs_sim(RunsArgs A, int64_t* __restrict__
 
 __global__ __launch_bounds__(RT) void runs_write(WriteArgs W) { runs_write_body(InterpTab{W.R.P}, W); }
 
-// completed runs in start order: key (end << 31 | start)
-__global__ void runs_compact(const int64_t* __restrict__ flag, const int64_t* __restrict__ pos,
-                             const int32_t* __restrict__ end_of, int64_t n, unsigned long long* __restrict__ out) {
+// completed runs in start order: key (end << 31 | start); each workgroup's total of their lengths
+// (entries of the CSR) into blk_len[blockIdx] (summed by a scan: no contended atomic)
+__global__ __launch_bounds__(256) void runs_compact(const int64_t* __restrict__ flag, const int64_t* __restrict__ pos,
+                                                    const int32_t* __restrict__ end_of, int64_t n,
+                                                    unsigned long long* __restrict__ out, int64_t* __restrict__ blk_len) {
+  __shared__ int64_t s_w[4];
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (j < n && flag[j]) out[pos[j]] = (unsigned long long)(int64_t(end_of[j]) << 31 | j);
+  int64_t len = 0;
+  if (j < n && flag[j]) {
+    out[pos[j]] = (unsigned long long)(int64_t(end_of[j]) << 31 | j);
+    len = int64_t(end_of[j]) - j + 1;
+  }
+  for (int d = 32; d >= 1; d >>= 1) len += __shfl_xor(len, d, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = len;
+  __syncthreads();
+  if (threadIdx.x == 0) blk_len[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// the CSR of the sorted completed runs from their recorded stage segments (runs_sim with A.segs):
+// one lane per match, entries final stage first (peek, SharedVersionedBufferStoreImpl.java:176-201)
+__global__ void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
+                            const uint32_t* __restrict__ segs, const unsigned long long* __restrict__ sorted,
+                            int64_t nm, const int64_t* __restrict__ ent_off, int64_t base,
+                            int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
+                            int64_t* __restrict__ ent_off_out, int32_t* __restrict__ ent_name,
+                            int64_t* __restrict__ ent_record) {
+  const int64_t m = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (m >= nm) return;
+  const unsigned long long kv = sorted[m];
+  const int64_t j = int64_t(kv & 0x7FFFFFFFull), e = int64_t(kv >> 31);
+  const int64_t at = ent_off[m];
+  match_record[m] = base + e;
+  match_key[m] = key[j];
+  ent_off_out[m] = at;
+  uint32_t sg[RUNS_MAX_SEGS];
+  int ns = 0;
+#pragma unroll
+  for (int i = 0; i < RUNS_MAX_SEGS; i++) {
+    sg[i] = segs[j * RUNS_MAX_SEGS + i];
+    if (ns == i && sg[i] != ~0u) ns = i + 1;
+  }
+  int64_t hi = e - j;                                  // offsets of the current segment: [lo, hi]
+#pragma unroll
+  for (int i = RUNS_MAX_SEGS - 1; i >= 0; i--) {
+    if (i >= ns) continue;
+    const int64_t lo = int64_t(sg[i] & 0xFFFFFFu);
+    const int32_t name = P->st[sg[i] >> 24].name;
+    for (int64_t o = hi; o >= lo; o--) {
+      ent_name[at + (e - j - o)] = name;
+      ent_record[at + (e - j - o)] = base + j + o;
+    }
+    hi = lo - 1;
+  }
 }
 
 __global__ void runs_lengths(const unsigned long long* __restrict__ sorted, int64_t nm, int64_t* __restrict__ len) {
@@ -72,17 +120,32 @@ hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hi
   return hipGetLastError();
 }
 
+// blk_len: (n + 255) / 256 partial sums, then their exclusive scan in blk_pre with the total in *ent_total
 hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
-                               unsigned long long* out, hipStream_t st) {
+                               unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
+                               int64_t* scan_tmp, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(runs_compact, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st, flag, pos, end_of, n, out);
-  return hipGetLastError();
+  const int64_t nb = (n + 255) / 256;
+  hipLaunchKernelGGL(runs_compact, dim3(unsigned(nb)), dim3(256), 0, st, flag, pos, end_of, n, out, blk_len);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? exclusive_scan(blk_len, nb, blk_pre, ent_total, scan_tmp, st) : e;
 }
 
-// stable order of completed runs: (completing record, start record)
+// order of completed runs: (completing record, start record).  The compacted keys are already in
+// start order and the radix sort is stable, so only the completing record's bits [31, 31 + bits)
+// are sorted on.
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
                      size_t* tmp_bytes, hipStream_t st) {
-  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, size_t(nm), 0, bits, st);
+  return rocprim::radix_sort_keys(tmp, *tmp_bytes, in, out, size_t(nm), 31, 31 + bits, st);
+}
+
+hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, const int64_t* ent_off,
+                              int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
+                              int64_t* ent_record, hipStream_t st) {
+  if (nm <= 0) return hipSuccess;
+  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.segs, sorted, nm,
+                     ent_off, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
+  return hipGetLastError();
 }
 
 hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,

@@ -69,6 +69,7 @@ struct RunEnv {
     return true;
   }
   __device__ __forceinline__ bool seq_avg(int, int64_t&) { err = CEP_E_UNSUPPORTED; return false; }
+  __device__ __forceinline__ bool seq_agg(int, int, int, int64_t&) { err = CEP_E_UNSUPPORTED; return false; }
   __device__ __forceinline__ void fail(int code) { err = code; }
 };
 
@@ -229,12 +230,16 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
 }
 
 // end_of[j] = completing record of the run started at record j (flag[j] = 1), else flag 0
+// ... and, with A.segs, the run's consumed stages as segments (so runs_expand writes the traversal
+// without walking the run again)
 template <class Tab>
 __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, int64_t* __restrict__ flag,
                                               int32_t* __restrict__ end_of) {
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
   const int64_t i0 = wave * RUNS_CHUNK, i1 = i0 + RUNS_CHUNK < A.n ? i0 + RUNS_CHUNK : A.n;
   if (i0 >= A.n) return;
+  int64_t seg_item = -1;                                        // the lane's current start record
+  int seg_last = -1, seg_n = 0;
   run_engine(
       T, A, i0, i1, [&](int64_t i, int64_t* j, int64_t* stop) { *j = i; *stop = INT64_MAX; return true; },
       [&](int64_t i, const RunResult& res) {
@@ -244,8 +249,17 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
           A.err_code[i] = res.err;
           atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
         }
+        if (A.segs && res.end >= 0 && seg_item == i && seg_n < RUNS_MAX_SEGS) A.segs[i * RUNS_MAX_SEGS + seg_n] = ~0u;
       },
-      [](int64_t, int64_t, int) {});
+      [&](int64_t i, int64_t r, int stage) {
+        if (!A.segs) return;
+        if (i != seg_item) { seg_item = i; seg_last = -1; seg_n = 0; }
+        if (stage == seg_last) return;
+        seg_last = stage;
+        const int64_t off = r - i;
+        if (seg_n >= RUNS_MAX_SEGS || off >= (int64_t(1) << 24)) { atomicOr(A.seg_over, 1ull); return; }
+        A.segs[i * RUNS_MAX_SEGS + seg_n++] = uint32_t(stage) << 24 | uint32_t(off);
+      });
 }
 
 struct WriteArgs {

@@ -45,6 +45,8 @@ OP_STATE_GET = 0x20
 OP_STATE_GET_OR_ELSE = 0x21
 OP_FOLD_CURR = 0x22
 OP_SEQ_AVG = 0x23
+OP_SEQ_AGG = 0x24
+SEQ_SUM, SEQ_COUNT, SEQ_MIN, SEQ_MAX, SEQ_FIRST, SEQ_LAST = 1, 2, 3, 4, 5, 6
 OP_NOT = 0x30
 OP_AND = 0x31
 OP_OR = 0x32
@@ -316,6 +318,26 @@ class SeqAvg(Expr):
         out += struct.pack("<H", self.col)
 
 
+class SeqAgg(Expr):
+    """A reduction a ``SequenceMatcher`` computes over the partial sequence it receives
+    (SequenceMatcher.java:21-26): over every event, or over one stage's events
+    (``Sequence.getByName(stage).getEvents()``, a TreeSet in ``Event.compareTo`` order,
+    Sequence.java:57-60 / 130-167; a stage missing from the sequence gives null, i.e. a
+    NullPointerException in the matcher).  ``sum`` and ``count`` are Java longs
+    (``mapToLong(..).sum()``, ``count()``), ``min``/``max`` follow ``Math.min/max``,
+    ``first``/``last`` are the TreeSet's ends."""
+    op = OP_SEQ_AGG
+
+    def __init__(self, kind: int, col: int, t, stage):
+        self.kind, self.col, self.stage = kind, col, stage
+        self.t = type_code(t)
+
+    def payload(self, out):
+        out.append(self.kind)
+        out += struct.pack("<H", self.col)
+        _put_str(out, self.stage)
+
+
 def _promote(a, b):
     if T_BOOL in (a, b):
         raise TypeError("arithmetic on boolean")
@@ -468,8 +490,45 @@ class _CurrNS:
 
 
 class _SequenceNS:
+    """Reductions over the partial ``Sequence`` of a ``SequenceMatcher``: ``avg`` is
+    ``IntSummaryStatistics.getAverage`` over every event; the others take an optional stage
+    name (``first``/``last`` need one)."""
+
     def avg(self, name: str = None):
         return _SeqAvgRef(name)
+
+    def sum(self, name: str = None, stage: str = None):
+        return _SeqAggRef(SEQ_SUM, name, stage)
+
+    def count(self, stage: str = None):
+        return _SeqAggRef(SEQ_COUNT, None, stage)
+
+    def min(self, name: str = None, stage: str = None):
+        return _SeqAggRef(SEQ_MIN, name, stage)
+
+    def max(self, name: str = None, stage: str = None):
+        return _SeqAggRef(SEQ_MAX, name, stage)
+
+    def first(self, name: str = None, stage: str = None):
+        if stage is None:
+            raise ValueError("first() needs a stage: Sequence.getByName(stage).getEvents() is the TreeSet it reads")
+        return _SeqAggRef(SEQ_FIRST, name, stage)
+
+    def last(self, name: str = None, stage: str = None):
+        if stage is None:
+            raise ValueError("last() needs a stage: Sequence.getByName(stage).getEvents() is the TreeSet it reads")
+        return _SeqAggRef(SEQ_LAST, name, stage)
+
+
+class _SeqAggRef(Expr):
+    op = OP_SEQ_AGG
+
+    def __init__(self, kind, name, stage):
+        self.kind, self.name, self.stage = kind, name, stage
+        self.t = T_I64  # placeholder numeric type; real type set by bind()
+
+    def payload(self, out):
+        raise RuntimeError("unbound sequence column (bind a Schema first)")
 
 
 class _SeqAvgRef(Expr):
@@ -497,6 +556,15 @@ def bind(e: Expr, schema) -> Expr:
     if isinstance(e, _SeqAvgRef):
         col, _ = schema.resolve(e.name)
         return SeqAvg(col)
+    if isinstance(e, _SeqAggRef):
+        if e.kind == SEQ_COUNT:
+            return SeqAgg(SEQ_COUNT, 0, T_I64, e.stage)
+        col, t = schema.resolve(e.name)
+        if e.kind == SEQ_SUM:
+            if type_code(t) == T_F64:
+                raise TypeError("sum over a double column is DoubleStream.sum (compensated): not lowered")
+            t = T_I64
+        return SeqAgg(e.kind, col, t, e.stage)
     if isinstance(e, Bin):
         return Bin(e.op, bind(e.a, schema), bind(e.b, schema))
     if isinstance(e, Un):

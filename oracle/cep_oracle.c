@@ -129,7 +129,7 @@ enum {
   OP_TRUE = 0x01, OP_FALSE = 0x02, OP_CONST_I32 = 0x03, OP_CONST_I64 = 0x04, OP_CONST_F64 = 0x05,
   OP_FIELD = 0x10, OP_EV_KEY = 0x11, OP_EV_TS = 0x12, OP_EV_TOPIC_EQ = 0x13, OP_EV_OFFSET = 0x14,
   OP_EV_PARTITION = 0x15, OP_STATE_GET = 0x20, OP_STATE_GET_OR_ELSE = 0x21, OP_FOLD_CURR = 0x22,
-  OP_SEQ_AVG = 0x23, OP_NOT = 0x30, OP_AND = 0x31, OP_OR = 0x32, OP_ADD = 0x40, OP_SUB = 0x41,
+  OP_SEQ_AVG = 0x23, OP_SEQ_AGG = 0x24, OP_NOT = 0x30, OP_AND = 0x31, OP_OR = 0x32, OP_ADD = 0x40, OP_SUB = 0x41,
   OP_MUL = 0x42, OP_DIV = 0x43, OP_REM = 0x44, OP_NEG = 0x45, OP_EQ = 0x50, OP_NE = 0x51,
   OP_LT = 0x52, OP_LE = 0x53, OP_GT = 0x54, OP_GE = 0x55, OP_CAST = 0x60
 };
@@ -144,6 +144,8 @@ typedef struct Expr {
 } Expr;
 
 typedef struct { uint8_t t; union { int32_t i; int64_t l; double d; int b; } u; } Val;
+/* SequenceMatcher reductions (OP_SEQ_AGG kind) */
+enum { SEQ_SUM = 1, SEQ_COUNT = 2, SEQ_MIN = 3, SEQ_MAX = 4, SEQ_FIRST = 5, SEQ_LAST = 6 };
 
 /* ------------------------------------------------------------------------- */
 /* compiled pattern (StagesFactory.java:49-180, Stage.java:40-252)           */
@@ -244,6 +246,24 @@ static Expr* rd_expr(orc_pattern* p, Rd* r, int depth) {
       e->col = rd_u16(r); e->t = T_F64;
       if (e->col >= p->ncols) { r->bad = 1; return NULL; }
       break;
+    case OP_SEQ_AGG: {                /* kind, column, stage name (null: every stage) */
+      e->ct = rd_u8(r); e->col = rd_u16(r);
+      if (!rd_ok(r, 2)) { r->bad = 1; return NULL; }
+      const int isnull = r->p[r->i] == 0xFF && r->p[r->i + 1] == 0xFF;
+      char* s = rd_str(r);
+      if (r->bad || (!s && !isnull)) { r->bad = 1; return NULL; }
+      e->name = -1;                   /* every stage */
+      if (s) {                        /* a stage no one declared never appears: -2 */
+        e->name = -2;
+        for (int64_t i = 0; i < p->names.n; i++) if (!strcmp(p->names.a[i], s)) e->name = (int)i;
+        free(s);
+      }
+      if (e->col >= p->ncols || e->ct < SEQ_SUM || e->ct > SEQ_LAST) { r->bad = 1; return NULL; }
+      if ((e->ct == SEQ_FIRST || e->ct == SEQ_LAST) && isnull) { r->bad = 1; return NULL; }
+      if (e->ct == SEQ_SUM && p->coltype[e->col] == T_F64) { r->bad = 1; return NULL; }
+      e->t = (e->ct == SEQ_SUM || e->ct == SEQ_COUNT) ? T_I64 : p->coltype[e->col];
+      break;
+    }
     case OP_NOT:
       e->a = rd_expr(p, r, depth + 1);
       if (!e->a || e->a->t != T_BOOL) { r->bad = 1; return NULL; }
@@ -867,6 +887,63 @@ static int seq_avg(EC* c, int col, Val* out) {
   return ORC_OK;
 }
 
+/* Reductions a SequenceMatcher computes over the same partial Sequence (Sequence.java:57-60,
+   116-167): every event, or getByName(stage).getEvents() -- a TreeSet in Event.compareTo order
+   (Event.java:118-122), null for a stage the sequence lacks (NPE).  sum/count as Java longs
+   (mapToLong(..).sum(), count()), min/max as LongStream / DoubleStream (Math.min / max), first /
+   last the TreeSet's ends. */
+static int seq_agg(EC* c, int kind, int col, int stage, uint8_t t, Val* out) {
+  orc_run* R = c->R;
+  if (!c->has_prev || c->pev < 0) return err_at(R, ORC_E_NPE, "SequenceMatcher without previous stage/event");
+  int64_t eb, ee;
+  int rc = buf_peek(R, c->prev, c->pev, c->ver, 0, &eb, &ee);
+  if (rc) return rc;
+  int64_t gb, ge;
+  materialise(R, eb, ee, &gb, &ge);
+  int64_t n = 0; uint64_t isum = 0; Val acc = {0}; int64_t first = -1, last = -1;
+  const uint8_t ctype = R->p->coltype[col];
+  for (int64_t g = gb; g < ge && !rc; g++) {
+    if (stage != -1 && R->grp_name.a[g] != stage) continue;
+    for (int64_t i = 0; i < R->grp_cnt.a[g] && !rc; i++) {
+      const int64_t ev = R->grp_ev.a[R->grp_evoff.a[g] + i];
+      if (first < 0) first = ev;
+      last = ev;
+      Val v;
+      rc = read_col(R->b, R->p, col, ev, &v);
+      if (rc) break;
+      if (kind == SEQ_SUM) isum += (uint64_t)(v.t == T_I32 ? (int64_t)v.u.i : v.u.l);
+      else if (kind == SEQ_MIN || kind == SEQ_MAX) {
+        if (n == 0) acc = v;
+        else if (ctype == T_F64) {
+          const double a = acc.u.d, b = v.u.d;
+          int take;
+          if (a != a) take = 0;
+          else if (b != b) take = 1;
+          else if (kind == SEQ_MIN) take = b < a || (b == 0 && a == 0 && signbit(b) && !signbit(a));
+          else take = b > a || (b == 0 && a == 0 && !signbit(b) && signbit(a));
+          if (take) acc = v;
+        } else {
+          const int64_t a = acc.t == T_I32 ? acc.u.i : acc.u.l, b = v.t == T_I32 ? v.u.i : v.u.l;
+          if (kind == SEQ_MIN ? b < a : b > a) acc = v;
+        }
+      }
+      n++;
+    }
+  }
+  R->ent_name.n = eb; R->ent_ev.n = eb;                /* drop the temporary traversal + groups */
+  R->grp_ev.n = ge > gb ? R->grp_evoff.a[gb] : R->grp_ev.n;
+  R->grp_name.n = gb; R->grp_cnt.n = gb; R->grp_evoff.n = gb;
+  if (rc) return rc;
+  if (n == 0 && (stage != -1 || kind == SEQ_MIN || kind == SEQ_MAX))
+    return err_at(R, ORC_E_NPE, "Sequence.getByName: no such stage in the partial sequence");
+  out->t = t;
+  if (kind == SEQ_COUNT) out->u.l = n;
+  else if (kind == SEQ_SUM) out->u.l = (int64_t)isum;
+  else if (kind == SEQ_MIN || kind == SEQ_MAX) *out = acc;
+  else return read_col(R->b, R->p, col, kind == SEQ_FIRST ? first : last, out);
+  return ORC_OK;
+}
+
 static int eval(const Expr* e, EC* c, Val* out) {
   orc_run* R = c->R;
   Val a, b;
@@ -898,6 +975,7 @@ static int eval(const Expr* e, EC* c, Val* out) {
       if (c->curr->t != e->ct) return err_at(R, ORC_E_CLASS_CAST, "aggregate has another boxed type");
       *out = *c->curr; return 0;
     case OP_SEQ_AVG: return seq_avg(c, e->col, out);
+    case OP_SEQ_AGG: return seq_agg(c, e->ct, e->col, e->name, e->t, out);
     case OP_NOT:
       if ((rc = eval(e->a, c, &a))) return rc;
       out->t = T_BOOL; out->u.b = !a.u.b; return 0;
