@@ -12,6 +12,7 @@
 //   stencil  (stencil.hip)  strict single-cardinality patterns, SURVEY Q9
 //   general  (nfa.hip)      every pattern the IR expresses: one lane per key
 //                           running the reference NFA over an HBM arena
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -52,7 +53,7 @@ hipError_t carry_sizes_launch(const int64_t* ctab, int64_t nkeys, const int32_t*
                               hipStream_t st);
 hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hipStream_t st, hipFunction_t jf);
 hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, const int64_t* ent_off,
-                              int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
+                              int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st);
 hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
                                unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
@@ -194,6 +195,32 @@ struct cep_session {
 };
 
 namespace {
+
+// roctx ranges around the C-ABI calls (SURVEY §5 tracing), for rocprofv3 --marker-trace: on with
+// KCEP_ROCTX=1, the roctx library loaded at the first call (no link-time dependency, no cost when off)
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    const char* on = getenv("KCEP_ROCTX");
+    if (!on || on[0] != '1') return;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    if (!push || !pop) push = nullptr;
+  }
+};
+const Roctx& roctx() {
+  static const Roctx r;
+  return r;
+}
+struct RoctxRange {
+  bool on;
+  explicit RoctxRange(const char* name) : on(roctx().push != nullptr) { if (on) roctx().push(name); }
+  ~RoctxRange() { if (on) roctx().pop(); }
+};
 
 // an environment switch for A/B runs ("1" on)
 bool getenv_flag(const char* name) {
@@ -411,7 +438,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                              s->jit ? s->jit->runs_write : nullptr));
   if (!res[3] && !getenv_flag("KCEP_RUNS_REWALK")) {
     // the traversals from the stage segments runs_sim recorded
-    HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_entoff.as<int64_t>(),
+    HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_entoff.as<int64_t>(), ne,
                                 s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
                                 s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
   } else {                                         // a run beyond RUNS_MAX_SEGS segments: walk every run again
@@ -833,6 +860,9 @@ int cep_pattern_build_kernels(const cep_pattern* p, int path) {
 
 int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   if (!s || !b) return fail(CEP_E_ARG, "null argument");
+  static const char* const kRange[] = {"cep_push_batch", "cep_push_batch:stencil", "cep_push_batch:general",
+                                       "cep_push_batch:chain", "cep_push_batch:runs"};
+  RoctxRange range(kRange[s->path >= 1 && s->path <= 4 ? s->path : 0]);
   const Program& P = s->pat->prog;
   if (b->n < 0 || b->n > s->opts.max_events) return fail(CEP_E_ARG, "batch larger than the session capacity");
   if (b->n > 0 && !b->key_id) return fail(CEP_E_ARG, "key_id is required");
@@ -908,6 +938,7 @@ int cep_last_batch_ms(cep_session* s, float* ms) {
 
 int cep_collect(cep_session* s, cep_matches* o) {
   if (!s || !o) return fail(CEP_E_ARG, "null argument");
+  RoctxRange range("cep_collect");
   memset(o, 0, sizeof *o);
   HIPCHECK(hipSetDevice(s->device));
   if (s->last_path == CEP_PATH_GENERAL || s->last_path == CEP_PATH_RUNS) {

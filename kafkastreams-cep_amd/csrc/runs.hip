@@ -57,40 +57,56 @@ __global__ __launch_bounds__(256) void runs_compact(const int64_t* __restrict__ 
   if (threadIdx.x == 0) blk_len[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
-// the CSR of the sorted completed runs from their recorded stage segments (runs_sim with A.segs):
-// one lane per match, entries final stage first (peek, SharedVersionedBufferStoreImpl.java:176-201)
-__global__ void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
-                            const uint32_t* __restrict__ segs, const unsigned long long* __restrict__ sorted,
-                            int64_t nm, const int64_t* __restrict__ ent_off, int64_t base,
-                            int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
-                            int64_t* __restrict__ ent_off_out, int32_t* __restrict__ ent_name,
-                            int64_t* __restrict__ ent_record) {
-  const int64_t m = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (m >= nm) return;
-  const unsigned long long kv = sorted[m];
-  const int64_t j = int64_t(kv & 0x7FFFFFFFull), e = int64_t(kv >> 31);
-  const int64_t at = ent_off[m];
-  match_record[m] = base + e;
-  match_key[m] = key[j];
-  ent_off_out[m] = at;
-  uint32_t sg[RUNS_MAX_SEGS];
-  int ns = 0;
+// the CSR of the sorted completed runs from their recorded stage segments (runs_sim with A.segs),
+// entries final stage first (peek, SharedVersionedBufferStoreImpl.java:176-201).  A workgroup owns
+// 256 consecutive matches and writes their entries as one contiguous range, thread-strided (coalesced
+// stores); an entry finds its match by a binary search over the workgroup's entry offsets in LDS.
+__global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
+                                                   const uint32_t* __restrict__ segs,
+                                                   const unsigned long long* __restrict__ sorted, int64_t nm,
+                                                   const int64_t* __restrict__ ent_off, int64_t ne, int64_t base,
+                                                   int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
+                                                   int64_t* __restrict__ ent_off_out, int32_t* __restrict__ ent_name,
+                                                   int64_t* __restrict__ ent_record) {
+  __shared__ int64_t s_at[257];
+  __shared__ int64_t s_j[256], s_e[256];
+  __shared__ uint32_t s_seg[256][RUNS_MAX_SEGS];
+  const int tid = threadIdx.x;
+  const int64_t m0 = int64_t(blockIdx.x) * 256, m = m0 + tid;
+  const int cnt = nm - m0 < 256 ? int(nm - m0) : 256;
+  if (tid < cnt) {
+    const unsigned long long kv = sorted[m];
+    const int64_t j = int64_t(kv & 0x7FFFFFFFull), e = int64_t(kv >> 31);
+    const int64_t at = ent_off[m];
+    s_at[tid] = at;
+    s_j[tid] = j;
+    s_e[tid] = e;
+    match_record[m] = base + e;
+    match_key[m] = key[j];
+    ent_off_out[m] = at;
 #pragma unroll
-  for (int i = 0; i < RUNS_MAX_SEGS; i++) {
-    sg[i] = segs[j * RUNS_MAX_SEGS + i];
-    if (ns == i && sg[i] != ~0u) ns = i + 1;
+    for (int i = 0; i < RUNS_MAX_SEGS; i++) s_seg[tid][i] = segs[j * RUNS_MAX_SEGS + i];
   }
-  int64_t hi = e - j;                                  // offsets of the current segment: [lo, hi]
-#pragma unroll
-  for (int i = RUNS_MAX_SEGS - 1; i >= 0; i--) {
-    if (i >= ns) continue;
-    const int64_t lo = int64_t(sg[i] & 0xFFFFFFu);
-    const int32_t name = P->st[sg[i] >> 24].name;
-    for (int64_t o = hi; o >= lo; o--) {
-      ent_name[at + (e - j - o)] = name;
-      ent_record[at + (e - j - o)] = base + j + o;
+  if (tid == 0) s_at[cnt] = m0 + cnt < nm ? ent_off[m0 + cnt] : ne;
+  __syncthreads();
+  const int64_t E0 = s_at[0], E1 = s_at[cnt];
+  for (int64_t x = E0 + tid; x < E1; x += 256) {
+    int lo = 0, hi = cnt - 1;                        // the last match whose range starts at or before x
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_at[mid] <= x) lo = mid; else hi = mid - 1;
     }
-    hi = lo - 1;
+    const int64_t j = s_j[lo], e = s_e[lo];
+    const int64_t o = (e - j) - (x - s_at[lo]);       // offset of the entry's record from the start
+    uint32_t stage = 0;
+#pragma unroll
+    for (int i = 0; i < RUNS_MAX_SEGS; i++) {        // the segment holding offset o (segments ascend)
+      const uint32_t w = s_seg[lo][i];
+      if (w != ~0u && int64_t(w & 0xFFFFFFu) <= o) stage = w >> 24;
+      if (w == ~0u) break;
+    }
+    ent_name[x] = P->st[stage].name;
+    ent_record[x] = base + j + o;
   }
 }
 
@@ -140,11 +156,11 @@ hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int6
 }
 
 hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, const int64_t* ent_off,
-                              int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
+                              int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st) {
   if (nm <= 0) return hipSuccess;
   hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.segs, sorted, nm,
-                     ent_off, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
+                     ent_off, ne, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
   return hipGetLastError();
 }
 
