@@ -78,6 +78,7 @@ struct Lane {
   int32_t* wtop;               // wave: the key's heap top, in LDS
   int32_t* log;                // wave: this lane's run's deferred buffer operations, WL words each
   int32_t log_cap, log_n;
+  int32_t arena_used;             // wave kernel: LDS arena words key_begin took (-1: workspace in the pool)
   int32_t nph;                 // wave: run-counter increments of this lane's run (seq placeholders)
   int32_t wgrow;               // wave: the shared heap was too small (grow it and re-run the round)
   unsigned long long* wpool;   // wave: the key's pool words, in LDS (every lane allocates for the key)
@@ -1024,7 +1025,11 @@ __device__ __forceinline__ int64_t export_state(Lane& l) {
 // Per-key setup shared by the lane kernel and the wave kernel (nfa_wave.h): workspace from the
 // pool, carried state (NFAStoreImpl.find, CEPProcessor.loadNFA :111-124) or NFA.build.  Returns
 // false if the key has nothing to run (its result words are then final).
-__device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg) {
+// arena (wave kernel): LDS words for the key's hot workspace (hwm, nodes, queues, aggregates, heap);
+// used when they fit, the match output stays in the pool (the compaction reads it after the kernel).
+// Arrays that outgrow it are re-allocated in the pool like any other (generic pointers throughout).
+__device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, int32_t* arena = nullptr,
+                                         int64_t arena_words = 0) {
   l.A = &A;
   l.P = A.P;
   l.pool_words = 0;
@@ -1067,8 +1072,11 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg) {
   l.outcap = A.cap.out_base + A.cap.out_mult * l.L;
   const int64_t fixed = 3 * HWM_MAX + int64_t(NW) * ns * l.nev + 16 * int64_t(A.cap.q0) +
                         int64_t(3) * nst * l.seqcap + l.heapcap + l.outcap;
-  int32_t* p = pool_alloc(l, fixed);
-  if (!p) {
+  const bool in_lds = arena && fixed - l.outcap <= arena_words;
+  l.arena_used = in_lds ? int32_t(fixed - l.outcap) : -1;
+  int32_t* p = in_lds ? arena : pool_alloc(l, fixed);
+  int32_t* out_at = in_lds && p ? pool_alloc(l, l.outcap) : nullptr;
+  if (!p || (in_lds && !out_at)) {
     if (A.last_attempt || l.cap_hit) {                                 // handed back per key
       A.res_err[seg] = CEP_E_RUN_CAPACITY;
       A.res_err_rec[seg] = A.base + l.seg0;
@@ -1085,7 +1093,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg) {
   l.fq = p; p += 4 * A.cap.q0;
   l.aggs = p; p += int64_t(3) * nst * l.seqcap;
   l.heap = p; p += l.heapcap;
-  l.out = p;
+  l.out = in_lds ? out_at : p;
   l.heap_top = 0; l.out_top = 0;
   for (int64_t i = 0; i < int64_t(3) * nst * l.seqcap; i++) l.aggs[i] = 0;   // all states null
   if (blob) {

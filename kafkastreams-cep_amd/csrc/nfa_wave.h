@@ -31,6 +31,9 @@
 namespace kcep {
 
 constexpr int WAVE = 64;
+#ifndef WAVE_ARENA
+#define WAVE_ARENA 2048                    // LDS words per key workspace (KCEP_WAVE_ARENA A/B: 0 = pool only)
+#endif
 
 // the key's shared workspace descriptor (LDS); lanes keep register copies in their Lane
 struct WaveShared {
@@ -43,6 +46,7 @@ struct WaveShared {
   int32_t logn[WAVE], errc[WAVE];
   int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
   int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
+  int32_t *arena, arena_used;      // the key's LDS arena and its bump pointer (re-allocations go there first)
   // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
   int32_t ms_slot[WAVE], ms_e[WAVE], ms_pv[WAVE], ms_cnt[WAVE], ms_done[WAVE], ms_err[WAVE];
 };
@@ -72,13 +76,19 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
 
 // A shared array of `cap` words (used up to `used`) re-allocated at >= need words: lane 0 draws it
 // from the pool, the wave copies.  Returns the new array (nullptr: pool exhausted -> w.overflow).
+// lds_ok: the array may move into the key's LDS arena (not the match output, read after the kernel)
 __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared& w, int32_t* a, int32_t& cap, int64_t used,
-                                                int64_t need, int lane) {
+                                                int64_t need, int lane, bool lds_ok = true) {
   int64_t nc = int64_t(cap) * 2;
   if (nc < need) nc = need;
   __syncthreads();
   if (lane == 0) {
-    w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc);
+    if (lds_ok && w.arena_used + nc <= WAVE_ARENA) {   // room left in the LDS arena
+      w.grown = w.arena + w.arena_used;
+      w.arena_used += int32_t((nc + 3) & ~int64_t(3));
+    } else {
+      w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc);
+    }
     if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
   }
   __syncthreads();
@@ -298,7 +308,7 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
     const int off = wave_excl_scan(words, lane, total);
     if (w.out_top + total > w.outcap) {
       int32_t cap = w.outcap;
-      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, lane);
+      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, lane, false);
       if (!na) return false;
       if (lane == 0) { w.out = na; w.outcap = cap; }
       __syncthreads();
@@ -339,11 +349,14 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   if (seg >= A.nseg) return;
   Lane l;
   int ok = 1;
+  __shared__ __attribute__((aligned(16))) int32_t s_arena[WAVE_ARENA];   // the key's hot workspace, if it fits
   if (lane == 0) {
-    ok = key_begin(l, A, seg) ? 1 : 0;
+    ok = key_begin(l, A, seg, s_arena, WAVE_ARENA) ? 1 : 0;
     if (ok) {
       lane_to_ws(w, l);
       w.pool_words = l.pool_words;
+      w.arena = s_arena;
+      w.arena_used = l.arena_used >= 0 ? (l.arena_used + 3) & ~3 : WAVE_ARENA;
     }
   }
   ok = __shfl(ok, 0);
