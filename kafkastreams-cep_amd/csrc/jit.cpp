@@ -345,6 +345,9 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // the same for the wave kernel (KCEP_NFA_WAVE_OCC)
   const char* oenv = getenv("KCEP_NFA_WAVE_OCC");
   const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 3;   // measured best on C4 (2: 13.3, 3: 10.8, 4: 11.8 ms)
+  // LDS arena words of the wave kernel's key workspace (KCEP_WAVE_ARENA, tuning only)
+  const char* aenv = getenv("KCEP_WAVE_ARENA");
+  if (aenv) o += "#define WAVE_ARENA " + std::to_string(std::min(8192, std::max(4, atoi(aenv)))) + "\n";
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
        "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
   kcep::nfa_kernel_body(A);
