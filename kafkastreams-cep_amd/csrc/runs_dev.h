@@ -86,7 +86,7 @@ __device__ __forceinline__ bool wave_any(bool x) { return __builtin_amdgcn_ballo
 // A wave owns a chunk of RUNS_CHUNK items (start records, or completed runs to
 // write); a lane whose run ends takes the next item of the chunk at the next
 // step, so the wave does not idle behind its longest run.
-constexpr int RUNS_CHUNK = 512;
+constexpr int RUNS_CHUNK = 1024;
 
 struct RunResult {
   int64_t end;        // record where the run consumed its last stage, -1 none
