@@ -407,6 +407,18 @@ bool build_table(StencilProgram& S) {
     for (int s = 0; s < STENCIL_MAX_K; s++) m |= uint8_t(stage_accepts(S, s, isf, 0, NAN, trep)) << s;
     S.nan_mask[it] = m;
   }
+  S.lut_n = 0;
+  S.lut_lo = 0;
+  memset(S.lut, 0, sizeof S.lut);
+  // (worth it from ~6 breakpoints: C5's 8 -> kernel -2 %, C2's 4 -> +0.5 %, profiles/r02_ab_c2_c5_lut.log)
+  if (!isf && S.ntbp == 0 && nb >= 6 && bi.back() - bi.front() < int64_t(sizeof S.lut)) {
+    S.lut_lo = bi.front();
+    S.lut_n = int32_t(bi.back() - bi.front() + 1);
+    for (int r = 0, iv = 0; r < S.lut_n; r++) {   // iv = #{breakpoints <= lut_lo + r}
+      while (iv < nb && bi[iv] <= S.lut_lo + r) iv++;
+      S.lut[r] = S.table[iv];
+    }
+  }
   return true;
 }
 

@@ -92,6 +92,12 @@ struct StencilProgram {
   int32_t tbp[3];
   uint8_t table[64];
   uint8_t nan_mask[4];               // double columns: mask of a NaN value per topic interval
+  // Dense form of the same table for integer columns without topic atoms with >= 6 breakpoints spanning
+  // < 256 values: mask = lut[v - lut_lo] inside [lut_lo, lut_lo + lut_n), table[0] below,
+  // table[nbp] above (one LDS read per record instead of nbp compares); lut_n = 0: not used
+  int64_t lut_lo;
+  int32_t lut_n;
+  uint8_t lut[256];
 };
 
 struct Program {

@@ -130,7 +130,27 @@ __device__ __forceinline__ VT bp_at(const StencilProgram* __restrict__ P, int b)
 
 template <class VT, bool TOPIC>
 __device__ __forceinline__ void masks_of_chunk(const Chunk<VT, TOPIC>& c, const StencilProgram* __restrict__ P,
-                                               const uint8_t* s_tab, const uint8_t* s_nan, uint32_t (&packed)[4]) {
+                                               const uint8_t* s_tab, const uint8_t* s_nan, uint32_t (&packed)[4],
+                                               const uint8_t* s_lut) {
+  if constexpr (!TOPIC && !std::is_same<VT, double>::value) {
+    const int32_t lut_n = P->lut_n;
+    if (lut_n > 0) {                               // dense table: one LDS byte per record (uniform branch)
+      const int64_t lo = P->lut_lo;
+      const uint32_t below = s_tab[0], above = s_tab[P->nbp];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int64_t dv = int64_t(vget<VT>(c.v[q], i)) - lo;
+          const uint32_t m = dv < 0 ? below : dv >= lut_n ? above : uint32_t(s_lut[dv]);
+          w |= m << (8 * i);
+        }
+        packed[q] = w;
+      }
+      return;
+    }
+  }
   int iv[ST_EPT], it[ST_EPT];
 #pragma unroll
   for (int e = 0; e < ST_EPT; e++) { iv[e] = 0; it[e] = 0; }
@@ -385,6 +405,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];
   __shared__ int32_t s_wsum[SUB][ST_THREADS / 64];
   __shared__ uint8_t s_tab[64];
+  __shared__ uint8_t s_lut[256];
   __shared__ uint8_t s_nan[4];
   __shared__ uint32_t s_super;
 
@@ -392,6 +413,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
   const int lane = tid & 63, wid = tid >> 6;
   if (tid == 0) s_super = blockIdx.x;             // no ordering between workgroups is needed
   if (tid < 64) s_tab[tid] = P->table[tid];
+  s_lut[tid] = P->lut[tid];                       // (ST_THREADS == 256 entries)
   if (tid < 4) s_nan[tid] = P->nan_mask[tid];
   __syncthreads();
   const int64_t tile0 = int64_t(s_super) * SUB;
@@ -483,7 +505,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         }
       }
       uint32_t packed[4];
-      masks_of_chunk<VT, TOPIC>(cur, P, s_tab, s_nan, packed);
+      masks_of_chunk<VT, TOPIC>(cur, P, s_tab, s_nan, packed, s_lut);
 #pragma unroll
       for (int q = 0; q < ST_EPT / 4; q++) {
         const int local = q * (ST_THREADS * 4) + tid * 4;
