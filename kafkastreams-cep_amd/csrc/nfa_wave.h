@@ -385,7 +385,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   ws_to_lane(l, w);
   // private run lists and operation logs
   __shared__ int32_t* s_priv;
-  const int q0 = 16;
+  const int q0 = 2;
   if (lane == 0) {
     s_priv = pool_alloc(l, int64_t(WAVE) * 4 * (q0 + q0 * WL / 4 + 4));
     if (!s_priv) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
