@@ -183,6 +183,7 @@ struct cep_session {
   bool jitg_tried = false;
   int64_t live_hwm = 0;                    // general path: most live runs any key held in the last batch
   bool wave = false;                       // general path: one key per wave (nfa_wave.h) for this pattern
+  bool g_any_err = false;                  // general path: some key of the last batch raised
   DBuf r_prof;                             // CEP_SESSION_PROFILE: per key segment {live max, evaluations, cycles}
   std::string jit_why;
   int32_t g_err = CEP_OK;
@@ -533,6 +534,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.pool_top = ctl;
   A.cpool_top = ctl + 1;
   A.flags = reinterpret_cast<int32_t*>(ctl + 2);
+  A.err_any = ctl + 4;
   // key segments per wave (KCEP_NFA_SPREAD: experiments; fewer keys per wave diverge less but leave
   // the chip emptier -- tools/c4_profile.py)
   const char* spread_env = getenv("KCEP_NFA_SPREAD");
@@ -554,7 +556,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.cpool_cap = s->carry ? s->cpool_words : 0;
     A.last_attempt = attempt >= kMaxRetry ? 1 : 0;     // then an overflowing key is handed back per key
     A.max_key_words = s->opts.max_key_words;
-    unsigned long long init[4] = {0, (unsigned long long)s->cpool_used, 0, 0};
+    unsigned long long init[5] = {0, (unsigned long long)s->cpool_used, 0, 0, 0};
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
     A.wave_seg = nullptr;
@@ -562,9 +564,10 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     else HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
     if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
     timed = true;
-    unsigned long long res[4];
+    unsigned long long res[5];
     HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+    s->g_any_err = res[4] != 0;
     const int32_t* fl = reinterpret_cast<const int32_t*>(res + 2);
     if (fl[2]) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
     s->live_hwm = fl[3];
@@ -606,6 +609,12 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   }
   HIPCHECK(hipEventRecord(s->eb1, st));
   // the reference fails the task at its first exception: report the earliest failing record
+  if (!s->g_any_err) {                             // no key raised: nothing to read back
+    if (s->carry && s->cpool_used > s->cpool_words / 4 * 3) {
+      if ((rc = carry_gc(s, 0, st))) return rc;
+    }
+    return CEP_OK;
+  }
   std::vector<int32_t> err(static_cast<size_t>(nseg));
   std::vector<int64_t> erec(static_cast<size_t>(nseg));
   HIPCHECK(hipMemcpyAsync(err.data(), s->r_err.p, size_t(nseg) * 4, hipMemcpyDeviceToHost, st));

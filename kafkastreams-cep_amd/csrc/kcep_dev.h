@@ -152,6 +152,7 @@ struct NfaArgs {
   int32_t last_attempt;           // 1: no pool regrowth follows -- an overflowing key reports CEP_E_RUN_CAPACITY
   const int32_t* wave_seg;        // wave kernel: the segment of each workgroup (nullptr: workgroup = segment)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY
+  unsigned long long* err_any;    // set when any key reports an exception (the host reads res_err only then)
 };
 
 // deterministic-runs path (runs.hip)

@@ -1177,6 +1177,7 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
     A.res_err_rec[seg] = l.overflow ? -1 : err_rec;
   }
   if (l.overflow) atomicAdd(&A.flags[0], 1);
+  if (A.res_err[seg]) atomicOr(A.err_any, 1ull);
   A.res_matches[seg] = l.nmatch;
   A.res_words[seg] = l.out_top;
   A.res_out[seg] = int64_t(reinterpret_cast<uintptr_t>(l.out));
