@@ -544,6 +544,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.profile = s->r_prof.as<int64_t>();
   }
   bool timed = false;
+  int64_t tots[2] = {0, 0};                        // matches, entries of the batch
   for (int attempt = 0;; attempt++) {
     if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
     if (s->carry && s->cpool_used + nseg * 64 > s->cpool_words) {
@@ -564,8 +565,14 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     else HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
     if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
     timed = true;
+    // the CSR's match / entry counts are scanned right away, so that one synchronisation reads them
+    // with the pool flags (a retried attempt scans again)
+    HIPCHECK(nfa_entry_counts_launch(s->r_words.as<int64_t>(), s->r_matches.as<int64_t>(), nseg, s->ents.as<int64_t>(), st));
+    HIPCHECK(exclusive_scan(s->r_matches.as<int64_t>(), nseg, s->moff.as<int64_t>(), scal + 3, s->scan_tmp.as<int64_t>(), st));
+    HIPCHECK(exclusive_scan(s->ents.as<int64_t>(), nseg, s->eoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), st));
     unsigned long long res[5];
     HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(tots, scal + 3, 16, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     s->g_any_err = res[4] != 0;
     const int32_t* fl = reinterpret_cast<const int32_t*>(res + 2);
@@ -585,13 +592,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       if ((rc = carry_gc(s, 2 * s->cpool_words, st))) return rc;
     }
   }
-  // compaction into the CSR
-  HIPCHECK(nfa_entry_counts_launch(s->r_words.as<int64_t>(), s->r_matches.as<int64_t>(), nseg, s->ents.as<int64_t>(), st));
-  HIPCHECK(exclusive_scan(s->r_matches.as<int64_t>(), nseg, s->moff.as<int64_t>(), scal + 3, s->scan_tmp.as<int64_t>(), st));
-  HIPCHECK(exclusive_scan(s->ents.as<int64_t>(), nseg, s->eoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), st));
-  int64_t tots[2] = {0, 0};
-  HIPCHECK(hipMemcpyAsync(tots, scal + 3, 16, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipStreamSynchronize(st));
+  // compaction into the CSR (counts scanned with the last attempt)
   s->g_matches = tots[0];
   s->g_entries = tots[1];
   const size_t nm = size_t(std::max<int64_t>(tots[0], 1)), ne = size_t(std::max<int64_t>(tots[1], 1));
