@@ -132,7 +132,7 @@ bool wave_ok(const DevProgram& D) {
 }
 
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
-constexpr NfaCaps kCaps{16, 64, 16, 32, 8, 16};
+constexpr NfaCaps kCaps{16, 64, 32, 32, 8, 16};
 constexpr int kMaxRetry = 8;                       // pool doublings before CEP_E_RUN_CAPACITY
 }  // namespace
 
