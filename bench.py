@@ -59,6 +59,8 @@ def parse(argv=None):
                     help="oracle threads for cpu_baseline (default: nproc, every CPU this process may run on)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-input", action="store_true", help="skip the PCIe-inclusive (host buffer) figure")
+    ap.add_argument("--processor-batch", type=lambda x: [int(v) for v in x.split(",") if v], default=[1 << 16, 1 << 20],
+                    help="stencil/chain: record counts per host batch for the processor-batch legs (comma list)")
     ap.add_argument("--carry-batches", type=int, default=10,
                     help="stencil/chain: also stream the batch through a carry session in this many batches")
     ap.add_argument("--gather-matches", action="store_true",
@@ -262,7 +264,13 @@ def main():
             line["config"]["live_run_hwm"] = sess.live_run_hwm()     # run-explosion high-water mark
             line["config"]["keys_on_cpu"] = 0                        # no CPU fallback: every key runs on the GPU
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and not args.no_host_input:
-            line["pcie_inclusive"] = _pcie_inclusive(sess, n, key, cols, stream, csum)
+            line["pcie_inclusive"], host = _pcie_inclusive(sess, n, key, cols, stream, csum)
+            # the processor's own batch sizes (CEPStream.query batch_size defaults to 1 << 16): host
+            # batches over PCIe, each collected, through a carry session
+            line["processor_batches"] = [
+                _carry_stream(pat, n, K, key, cols, stream, 0, n_matches, csum, value / world, reps=1, per=b,
+                              host=host, collect=True) for b in args.processor_batch]
+            del host
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and args.carry_batches > 1:
             line["carry_stream"] = _carry_stream(pat, n, K, key, cols, stream, args.carry_batches, n_matches, csum,
                                                  value / world)
@@ -295,30 +303,39 @@ def _pcie_inclusive(sess, n, key, cols, stream, csum, steps=3):
     _, c2 = sess.checksum()
     return {"value": n / dt, "unit": "events/s", "ms_per_step": dt * 1e3, "host_memory": "pinned",
             "bytes_per_step": int(hk.numel() * hk.element_size() + sum(c.numel() * c.element_size() for c in hc)),
-            "parity": c2 == csum}
+            "parity": c2 == csum}, (hk, hc)
 
 
-def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, reps=3):
-    """The same device-resident stream pushed through a CEP_SESSION_CARRY session (the
-    GpuCEPProcessor route) in `nb` consecutive batches: keys cut at batch boundaries continue from
-    their carried halos.  Parity: the batches' matches and checksums (over stream positions) add up
-    to the one-batch run.  Reported beside `value`, never as it."""
+def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, reps=3, per=None, host=None,
+                  collect=False):
+    """The same stream pushed through a CEP_SESSION_CARRY session (the GpuCEPProcessor route) in
+    consecutive batches (`nb` of them, or of `per` records): keys cut at batch boundaries continue
+    from their carried halos.  `host` = pinned host copies of (key, cols): every push stages its
+    batch over PCIe, as the JNI boundary hands it; `collect`: every batch's CSR is materialised on
+    the host (cep_collect), as the processor's flush does.  Parity: the batches' matches and
+    checksums (over stream positions) add up to the one-batch run.  Reported beside `value`, never
+    as it."""
     import torch
     from kcep import native as N
-    per = -(-n // nb)
-    per = -(-per // 4096) * 4096                     # 16-B aligned batch starts
+    if per is None:
+        per = -(-n // nb)
+        per = -(-per // 4096) * 4096                 # 16-B aligned batch starts
     bounds = list(range(0, n, per)) + [n]
     cs = N.Session(pat, per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K)
     cs.set_timing(False)
+    src_k, src_c = host if host is not None else (key, cols)
+    mem = N.MEM_HOST if host is not None else N.MEM_DEVICE
 
     def one_pass(check):
         tot_m, tot_c = 0, 0
         for a, b in zip(bounds[:-1], bounds[1:]):
-            cs.push(b - a, key.data_ptr() + 4 * a, [c.data_ptr() + c.element_size() * a for c in cols],
-                    mem=N.MEM_DEVICE, stream=stream.cuda_stream, flags=N.BATCH_OFFSETS_MONOTONE)
+            cs.push(b - a, src_k.data_ptr() + 4 * a, [c.data_ptr() + c.element_size() * a for c in src_c],
+                    mem=mem, stream=stream.cuda_stream, flags=N.BATCH_OFFSETS_MONOTONE)
             if check:
                 m, c = cs.checksum()
                 tot_m, tot_c = tot_m + m, (tot_c + c) & 0xFFFFFFFFFFFFFFFF
+            elif collect:
+                cs.collect()
         return tot_m, tot_c
 
     m, c = one_pass(True)
@@ -332,9 +349,18 @@ def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, r
         stream.synchronize()
         times.append(time.perf_counter() - t0)
     dt = min(times)
-    return {"value": n / dt, "unit": "events/s", "batches": len(bounds) - 1, "events_per_batch": per,
-            "ms_per_pass": dt * 1e3, "vs_resident": n / dt / resident, "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain"}.get(cs.path, "general"),
-            "parity": bool(m == n_matches and c == csum), "matches": int(m)}
+    nbat = len(bounds) - 1
+    out = {"value": n / dt, "unit": "events/s", "batches": nbat, "events_per_batch": per,
+           "ms_per_pass": dt * 1e3, "vs_resident": n / dt / resident,
+           "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain"}.get(cs.path, "general"),
+           "parity": bool(m == n_matches and c == csum), "matches": int(m)}
+    if host is not None or collect:
+        # per-batch cost above streaming the batch's records at the resident rate
+        out.update({"host_memory": "pinned" if host is not None else None, "collect_per_batch": collect,
+                    "us_per_batch": dt * 1e6 / nbat,
+                    "overhead_us_per_batch": (dt - n / resident) * 1e6 / nbat})
+    cs.close()
+    return out
 
 
 def _pmc_traffic(cfg, n):

@@ -153,7 +153,7 @@ typedef struct {
  * first (SharedVersionedBufferStoreImpl.peek :176-201), is
  *   entries [ent_off[m], ent_off[m+1]) : (ent_name[i], ent_record[i])
  * i.e. stage-name id and batch record index.  Sequence.Builder.build(true)
- * (Sequence.java:504-517) groups these by name in reverse order; helpers in
+ * (Sequence.java:210-223) groups these by name in reverse order; helpers in
  * kcep/sequence.py do it.  Matches are ordered by key (batch order), and per
  * key in emission order, which is the reference's per-key forward order. */
 typedef struct {
@@ -224,7 +224,8 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream);
  * device) so that a caller can chain work without a host sync. */
 const int64_t* cep_device_match_count(const cep_session* s);
 
-/* Waits for the last batch and materialises the host CSR. */
+/* Waits for the last batch and materialises the host CSR.  A second call before the next push
+ * returns the same CSR without touching the device. */
 int cep_collect(cep_session* s, cep_matches* out);
 
 /* Order-independent 64-bit checksum of the last batch's matches, computed on
@@ -255,6 +256,24 @@ int cep_state_clear(cep_session* s);
 int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len);
 /* Stream position the next batch's record 0 gets (0 for sessions without CEP_SESSION_CARRY). */
 int64_t cep_stream_position(const cep_session* s);
+/* Spill keys to the host, freeing their ids (the reference's NFAStore is an unbounded KV store,
+ * NFAStoreImpl.java:34-85; a session holds max_keys ids, so a host with more live keys keeps the cold
+ * ones' state itself).  Key keys[i]'s state becomes the self-contained single-key blob
+ * (*blobs)[offs[i] .. offs[i+1]) -- "KCST" or "KCSH" as cep_state_export writes it, empty if the key
+ * has no state -- and is dropped from the device, so the id starts afresh.  The blobs are
+ * library-owned, valid until the next cep_state_evict on the session.  offs has n + 1 entries. */
+int cep_state_evict(cep_session* s, const int32_t* keys, int64_t n, const uint8_t** blobs, int64_t* offs);
+/* Restores single-key blobs (from cep_state_evict, or a one-key cep_state_export) under the key ids
+ * keys[i] -- a spilled key re-admitted under whatever id is free.  Empty blobs are skipped. */
+int cep_state_import_keys(cep_session* s, const void* const* blobs, const size_t* lens, const int32_t* keys,
+                          int64_t n);
+/* The stream positions of every record a state blob (cep_state_export / cep_state_evict) still
+ * references -- the records a host must keep to build the Sequences of carried runs (the reference
+ * keeps them in its buffer store, MatchedEvent.java:29-34).  out == NULL: only *n. */
+int cep_state_positions(const void* blob, size_t len, int64_t* out, int64_t cap, int64_t* n);
+/* Changes cep_opts.max_key_words for the next batches: a host re-pushes the records of keys handed
+ * back with CEP_E_RUN_CAPACITY with the limit lifted (0 = only the device pool bounds a key). */
+int cep_session_set_max_key_words(cep_session* s, int64_t words);
 
 /* --- key-hash sharding across the GPUs of one node ---
  * The reference gets per-key independence from Kafka: the producer partitions records by key

@@ -8,6 +8,10 @@
  * Every shim is a thin call into the C-ABI: handles travel as jlong, errors as negative codes
  * with the message in cepLastError().  Host arrays are pinned only for the duration of the call
  * (GetPrimitiveArrayCritical); cep_push_batch stages them to the device and returns.
+ *
+ * Tested without a JVM: tests/test_jni_gpu.py compiles this file against tests/jni_stub/jni.h (a
+ * JNIEnv with exactly the functions used here, over plain C arrays) and drives it in the order
+ * GpuCEPProcessor.flush() calls it.
  */
 #include <jni.h>
 #include <stdint.h>
@@ -54,10 +58,13 @@ JNIEXPORT jlong JNICALL CLS(cepSessionOpen)(JNIEnv* env, jclass c, jlong pattern
   return rc ? -(jlong)rc : (jlong)(intptr_t)s;
 }
 
-/* cols: int[] / long[] / double[] per column type (1 / 2 / 3) */
+JNIEXPORT jint JNICALL CLS(cepSessionPath)(JNIEnv* env, jclass c, jlong session) { return cep_session_path(S(session)); }
+
+/* cols: int[] / long[] / double[] per column type (1 / 2 / 3); flags: cep_batch.flags
+   (CEP_BATCH_OFFSETS_MONOTONE once the caller applied the high-water mark itself) */
 JNIEXPORT jint JNICALL CLS(cepPushBatch)(JNIEnv* env, jclass c, jlong session, jint n, jintArray key,
                                          jintArray topic, jintArray partition, jlongArray offset, jlongArray ts,
-                                         jintArray col_types, jobjectArray cols) {
+                                         jintArray col_types, jobjectArray cols, jint flags) {
   const jsize nc = (*env)->GetArrayLength(env, cols);
   if (nc > 16) return CEP_E_ARG;
   jarray arrs[5 + 16];
@@ -76,11 +83,12 @@ JNIEXPORT jint JNICALL CLS(cepPushBatch)(JNIEnv* env, jclass c, jlong session, j
   b.n_cols = nc;
   b.mem = CEP_MEM_HOST;
   b.cols = (const void* const*)(ptrs + 5);
+  b.flags = (uint32_t)flags;
   int rc = cep_push_batch(S(session), &b, NULL);
   if (rc == CEP_OK) {                      /* the push is asynchronous: the host arrays must outlive it */
     cep_matches m;
-    rc = cep_collect(S(session), &m);      /* waits; the CSR stays library-owned until the next push */
-  }
+    rc = cep_collect(S(session), &m);      /* waits; the CSR stays library-owned until the next push, and */
+  }                                        /* cepCollect's cep_collect calls return it without device work */
   for (jsize i = 5 + nc - 1; i >= 0; i--) (*env)->ReleasePrimitiveArrayCritical(env, arrs[i], ptrs[i], JNI_ABORT);
   return rc;
 }
@@ -142,6 +150,70 @@ JNIEXPORT jint JNICALL CLS(cepStateImport)(JNIEnv* env, jclass c, jlong session,
   int rc = cep_state_import(S(session), p, (size_t)n);
   (*env)->ReleaseByteArrayElements(env, state, p, JNI_ABORT);
   return rc;
+}
+
+/* per key: its single-key blob (empty if it had no state); the keys' ids are free afterwards */
+JNIEXPORT jobjectArray JNICALL CLS(cepStateEvict)(JNIEnv* env, jclass c, jlong session, jintArray keys) {
+  const jsize n = (*env)->GetArrayLength(env, keys);
+  int64_t* offs = malloc(sizeof(int64_t) * (size_t)(n + 1));
+  jint* k = (*env)->GetIntArrayElements(env, keys, NULL);
+  const uint8_t* blobs = NULL;
+  int rc = offs ? cep_state_evict(S(session), (const int32_t*)k, n, &blobs, offs) : CEP_E_ARG;
+  (*env)->ReleaseIntArrayElements(env, keys, k, JNI_ABORT);
+  jobjectArray out = NULL;
+  if (rc == CEP_OK) {
+    out = (*env)->NewObjectArray(env, n, (*env)->FindClass(env, "[B"), NULL);
+    for (jsize i = 0; i < n; i++) {
+      const jsize len = (jsize)(offs[i + 1] - offs[i]);
+      jbyteArray b = (*env)->NewByteArray(env, len);
+      (*env)->SetByteArrayRegion(env, b, 0, len, (const jbyte*)(blobs + offs[i]));
+      (*env)->SetObjectArrayElement(env, out, i, b);
+    }
+  }
+  free(offs);
+  return out;
+}
+
+JNIEXPORT jint JNICALL CLS(cepStateImportKeys)(JNIEnv* env, jclass c, jlong session, jobjectArray blobs,
+                                               jintArray keys) {
+  const jsize n = (*env)->GetArrayLength(env, keys);
+  if ((*env)->GetArrayLength(env, blobs) != n) return CEP_E_ARG;
+  jbyteArray* arr = malloc(sizeof(jbyteArray) * (size_t)(n ? n : 1));
+  const void** ptrs = malloc(sizeof(void*) * (size_t)(n ? n : 1));
+  size_t* lens = malloc(sizeof(size_t) * (size_t)(n ? n : 1));
+  if (!arr || !ptrs || !lens) { free(arr); free((void*)ptrs); free(lens); return CEP_E_ARG; }
+  for (jsize i = 0; i < n; i++) {
+    arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, blobs, i);
+    lens[i] = (size_t)(*env)->GetArrayLength(env, arr[i]);
+    ptrs[i] = (*env)->GetByteArrayElements(env, arr[i], NULL);
+  }
+  jint* k = (*env)->GetIntArrayElements(env, keys, NULL);
+  int rc = cep_state_import_keys(S(session), ptrs, lens, (const int32_t*)k, n);
+  (*env)->ReleaseIntArrayElements(env, keys, k, JNI_ABORT);
+  for (jsize i = 0; i < n; i++) (*env)->ReleaseByteArrayElements(env, arr[i], (jbyte*)ptrs[i], JNI_ABORT);
+  free(arr); free((void*)ptrs); free(lens);
+  return rc;
+}
+
+JNIEXPORT jlongArray JNICALL CLS(cepStatePositions)(JNIEnv* env, jclass c, jbyteArray blob) {
+  const jsize len = (*env)->GetArrayLength(env, blob);
+  jbyte* p = (*env)->GetByteArrayElements(env, blob, NULL);
+  int64_t n = 0;
+  jlongArray out = NULL;
+  if (cep_state_positions(p, (size_t)len, NULL, 0, &n) == CEP_OK) {
+    int64_t* pos = malloc(sizeof(int64_t) * (size_t)(n ? n : 1));
+    if (pos && cep_state_positions(p, (size_t)len, pos, n, &n) == CEP_OK) {
+      out = (*env)->NewLongArray(env, (jsize)n);
+      (*env)->SetLongArrayRegion(env, out, 0, (jsize)n, (const jlong*)pos);
+    }
+    free(pos);
+  }
+  (*env)->ReleaseByteArrayElements(env, blob, p, JNI_ABORT);
+  return out;
+}
+
+JNIEXPORT jint JNICALL CLS(cepSetMaxKeyWords)(JNIEnv* env, jclass c, jlong session, jlong words) {
+  return cep_session_set_max_key_words(S(session), words);
 }
 
 JNIEXPORT void JNICALL CLS(cepSessionClose)(JNIEnv* env, jclass c, jlong session) { cep_session_close(S(session)); }

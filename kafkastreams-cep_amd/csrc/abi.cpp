@@ -193,6 +193,9 @@ struct cep_session {
   // ---- host CSR of the last collect ----
   std::vector<int64_t> match_record, ent_off, ent_record;
   std::vector<int32_t> match_key, ent_name, out_host;
+  bool collected = false;                  // the CSR above is the last batch's: a second collect re-uses it
+  cep_matches last{};
+  std::vector<uint8_t> evict_buf;          // cep_state_evict's blobs
 };
 
 namespace {
@@ -368,7 +371,9 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->e_code.clear();
   s->g_matches = s->g_entries = 0;
   HIPCHECK(hipEventRecord(s->ev0, st));
-  if (n == 0) {
+  if (n == 0) {                                   // cep_device_match_count reads scal[3]: zero it
+    if (s->scal.ensure(64)) return fail(CEP_E_HIP, "allocation failed");
+    HIPCHECK(hipMemsetAsync(s->scal.as<int64_t>() + 3, 0, 16, st));
     HIPCHECK(hipEventRecord(s->ev1, st));
     HIPCHECK(hipEventRecord(s->eb1, st));
     return CEP_OK;
@@ -477,7 +482,9 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->g_matches = s->g_entries = 0;
   s->nseg = 0;
   A.base = s->carry ? s->base : 0;
-  if (n == 0) {
+  if (n == 0) {                                   // cep_device_match_count reads scal[3]: zero it
+    if (s->scal.ensure(64)) return fail(CEP_E_HIP, "allocation failed");
+    HIPCHECK(hipMemsetAsync(s->scal.as<int64_t>() + 3, 0, 16, st));
     HIPCHECK(hipEventRecord(s->ev0, st));
     HIPCHECK(hipEventRecord(s->ev1, st));
     HIPCHECK(hipEventRecord(s->eb1, st));
@@ -884,6 +891,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   s->stream = st;
   s->n = b->n;
   s->pending = true;
+  s->collected = false;
   s->e_rec.clear();
   s->e_code.clear();
   if (s->timing) HIPCHECK(hipEventRecord(s->eb0, st));
@@ -950,6 +958,11 @@ int cep_collect(cep_session* s, cep_matches* o) {
   if (!s || !o) return fail(CEP_E_ARG, "null argument");
   RoctxRange range("cep_collect");
   memset(o, 0, sizeof *o);
+  if (s->collected) {                              // nothing pushed since: the host CSR is current
+    *o = s->last;
+    if (o->err) g_err = "the reference NFA raises an exception on this batch";
+    return CEP_OK;
+  }
   HIPCHECK(hipSetDevice(s->device));
   if (s->last_path == CEP_PATH_GENERAL || s->last_path == CEP_PATH_RUNS) {
     HIPCHECK(hipStreamSynchronize(s->stream));
@@ -1043,6 +1056,8 @@ int cep_collect(cep_session* s, cep_matches* o) {
   o->ent_name = s->ent_name.data();
   o->ent_record = s->ent_record.data();
   s->pending = false;
+  s->collected = true;
+  s->last = *o;
   return CEP_OK;
 }
 
@@ -1299,5 +1314,151 @@ int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len
 }
 
 int64_t cep_stream_position(const cep_session* s) { return s ? s->base : -1; }
+
+int cep_state_evict(cep_session* s, const int32_t* keys, int64_t n, const uint8_t** blobs, int64_t* offs) {
+  int rc = need_carry(s);
+  if (rc) return rc;
+  if (n < 0 || !blobs || !offs || (n > 0 && !keys)) return fail(CEP_E_ARG, "null argument");
+  for (int64_t i = 0; i < n; i++)
+    if (keys[i] < 0 || keys[i] >= s->opts.max_keys) return fail(CEP_E_ARG, "key id out of [0, max_keys)");
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  // one download of the key tables (and the carried pool), then one self-contained blob per key
+  std::vector<uint8_t>& out = s->evict_buf;
+  out.clear();
+  offs[0] = 0;
+  const uint32_t ver = 1;
+  auto header = [&](uint32_t magic, int32_t nk) {
+    const size_t at = out.size();
+    out.resize(at + 20);
+    memcpy(&out[at], &magic, 4); memcpy(&out[at + 4], &ver, 4); memcpy(&out[at + 8], &s->base, 8);
+    memcpy(&out[at + 16], &nk, 4);
+  };
+  if (halo_session(s)) {
+    const int km1 = s->pat->prog.stencil.k - 1;
+    const int64_t nk = s->opts.max_keys;
+    std::vector<HaloHdr> tab(static_cast<size_t>(nk));
+    std::vector<int64_t> pos(static_cast<size_t>(nk) * 2 * size_t(km1));
+    HIPCHECK(hipMemcpy(tab.data(), s->halo.p, tab.size() * sizeof(HaloHdr), hipMemcpyDeviceToHost));
+    if (km1) HIPCHECK(hipMemcpy(pos.data(), s->hpos.p, pos.size() * 8, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) {
+      HaloHdr& h = tab[size_t(keys[i])];
+      const int sl = halo_newest(h);
+      const int32_t cnt = h.cnt[sl];
+      if (h.stamp[sl] > 0 && cnt > 0) {
+        header(kHaloMagic, 1);
+        const size_t at = out.size();
+        out.resize(at + 16 + 8 * size_t(cnt));
+        memcpy(&out[at], &keys[i], 4); memcpy(&out[at + 4], &cnt, 4); memcpy(&out[at + 8], &h.masks[sl], 8);
+        memcpy(&out[at + 16], &pos[(2 * size_t(keys[i]) + size_t(sl)) * size_t(km1)], 8 * size_t(cnt));
+      }
+      h = HaloHdr{};                                 // no halo: the next batch starts the key afresh
+      offs[i + 1] = int64_t(out.size());
+    }
+    HIPCHECK(hipMemcpy(s->halo.p, tab.data(), tab.size() * sizeof(HaloHdr), hipMemcpyHostToDevice));
+  } else {
+    std::vector<int64_t> tab(size_t(s->opts.max_keys));
+    HIPCHECK(hipMemcpy(tab.data(), s->ctab.p, tab.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<int32_t> pool(size_t(s->cpool_used));
+    if (!pool.empty()) HIPCHECK(hipMemcpy(pool.data(), s->cpool.p, pool.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) {
+      int64_t& o = tab[size_t(keys[i])];
+      if (o >= 0) {
+        const int32_t w = pool[size_t(o) + CB_WORDS];
+        header(kStateMagic, 1);
+        const size_t at = out.size();
+        out.resize(at + 8 + 4 * size_t(w));
+        memcpy(&out[at], &keys[i], 4); memcpy(&out[at + 4], &w, 4);
+        memcpy(&out[at + 8], pool.data() + o, 4 * size_t(w));
+      }
+      o = -1;                                        // the blob's pool words are reclaimed by the next carry_gc
+      offs[i + 1] = int64_t(out.size());
+    }
+    HIPCHECK(hipMemcpy(s->ctab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+  }
+  *blobs = out.data();
+  return CEP_OK;
+}
+
+int cep_state_import_keys(cep_session* s, const void* const* blobs, const size_t* lens, const int32_t* keys,
+                          int64_t n) {
+  int rc = need_carry(s);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && (!blobs || !lens || !keys))) return fail(CEP_E_ARG, "null argument");
+  // one multi-key blob with the keys renumbered, then the ordinary import
+  std::vector<uint8_t> all(20);
+  const uint32_t magic = halo_session(s) ? kHaloMagic : kStateMagic, ver = 1;
+  int64_t base = 0;
+  int32_t nk = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const uint8_t* p = static_cast<const uint8_t*>(blobs[i]);
+    if (!p || lens[i] < 20) return fail(CEP_E_ARG, "bad state blob");
+    uint32_t m, v;
+    int64_t b;
+    int32_t cnt;
+    memcpy(&m, p, 4); memcpy(&v, p + 4, 4); memcpy(&b, p + 8, 8); memcpy(&cnt, p + 16, 4);
+    if (m != magic || v != 1 || cnt > 1) return fail(CEP_E_ARG, "cep_state_import_keys takes single-key blobs of this session's kind");
+    if (keys[i] < 0 || keys[i] >= s->opts.max_keys) return fail(CEP_E_ARG, "key id out of [0, max_keys)");
+    base = std::max(base, b);
+    if (cnt == 0) continue;
+    const size_t at = all.size();
+    all.insert(all.end(), p + 20, p + lens[i]);
+    memcpy(&all[at], &keys[i], 4);
+    nk++;
+  }
+  memcpy(&all[0], &magic, 4); memcpy(&all[4], &ver, 4); memcpy(&all[8], &base, 8); memcpy(&all[16], &nk, 4);
+  return cep_state_import(s, all.data(), all.size());
+}
+
+int cep_state_positions(const void* buf, size_t len, int64_t* out, int64_t cap, int64_t* n) {
+  if (!buf || !n || len < 20) return fail(CEP_E_ARG, "bad state blob");
+  const uint8_t* p = static_cast<const uint8_t*>(buf);
+  uint32_t magic;
+  int32_t nkeys;
+  memcpy(&magic, p, 4); memcpy(&nkeys, p + 16, 4);
+  if ((magic != kStateMagic && magic != kHaloMagic) || nkeys < 0) return fail(CEP_E_ARG, "bad state blob");
+  int64_t cnt = 0;
+  size_t at = 20;
+  auto put = [&](int64_t v) { if (out && cnt < cap) out[cnt] = v; cnt++; };
+  for (int32_t i = 0; i < nkeys; i++) {
+    if (at + 8 > len) return fail(CEP_E_ARG, "truncated state blob");
+    int32_t w;
+    memcpy(&w, p + at + 4, 4);
+    if (magic == kHaloMagic) {                       // key, records, masks, positions[records]
+      if (w < 0 || at + 16 + 8 * size_t(w) > len) return fail(CEP_E_ARG, "truncated state blob");
+      for (int32_t j = 0; j < w; j++) {
+        int64_t v;
+        memcpy(&v, p + at + 16 + 8 * size_t(j), 8);
+        put(v);
+      }
+      at += 16 + 8 * size_t(w);
+      continue;
+    }
+    if (w < CB_HDR || at + 8 + 4 * size_t(w) > len) return fail(CEP_E_ARG, "truncated state blob");
+    const int32_t* b = reinterpret_cast<const int32_t*>(p + at + 8);   // 4-byte aligned in every blob we write
+    int32_t hdr[CB_HDR];
+    memcpy(hdr, b, sizeof hdr);
+    const int32_t nev = hdr[CB_NEV];
+    if (nev > 0) {                                   // events: stream position (int64) first, carry_evw words each
+      const int64_t evw = 8 + 2 * int64_t(hdr[CB_NCOLS]);
+      const int64_t e0 = CB_HDR + 3 * int64_t(hdr[CB_NHWM]) + 4 * int64_t(hdr[CB_QLEN]);
+      if (e0 + nev * evw > w) return fail(CEP_E_ARG, "bad state blob");
+      for (int32_t e = 0; e < nev; e++) {
+        uint32_t lo, hi;
+        memcpy(&lo, b + e0 + e * evw, 4); memcpy(&hi, b + e0 + e * evw + 1, 4);
+        put(int64_t(uint64_t(lo) | (uint64_t(hi) << 32)));
+      }
+    }
+    at += 8 + 4 * size_t(w);
+  }
+  *n = cnt;
+  return out && cnt > cap ? fail(CEP_E_ARG, "output too small") : CEP_OK;
+}
+
+int cep_session_set_max_key_words(cep_session* s, int64_t words) {
+  if (!s || words < 0) return fail(CEP_E_ARG, "bad argument");
+  s->opts.max_key_words = words;
+  return CEP_OK;
+}
 
 }  // extern "C"

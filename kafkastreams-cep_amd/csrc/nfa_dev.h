@@ -1080,6 +1080,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
     if (A.last_attempt || l.cap_hit) {                                 // handed back per key
       A.res_err[seg] = CEP_E_RUN_CAPACITY;
       A.res_err_rec[seg] = A.base + l.seg0;
+      atomicOr(A.err_any, 1ull);                                       // the host reads res_err only then
     } else {
       atomicAdd(&A.flags[0], 1);
     }
@@ -1101,10 +1102,15 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
       if (l.overflow && (A.last_attempt || l.cap_hit)) {
         A.res_err[seg] = CEP_E_RUN_CAPACITY;
         A.res_err_rec[seg] = A.base + l.seg0;
+        atomicOr(A.err_any, 1ull);
         return false;
       }
       if (l.overflow) atomicAdd(&A.flags[0], 1);
       A.res_err[seg] = l.err;
+      if (l.err) {
+        A.res_err_rec[seg] = A.base + l.seg0;
+        atomicOr(A.err_any, 1ull);
+      }
       return false;
     }
   } else {

@@ -231,35 +231,55 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
 
 // end_of[j] = completing record of the run started at record j (flag[j] = 1), else flag 0
 // ... and, with A.segs, the run's consumed stages as segments (so runs_expand writes the traversal
-// without walking the run again)
+// without walking the run again).  Both are staged in LDS: a lane's segments while its run is open
+// (stored once, as two 16-B vectors, when the run completes -- and not at all when it dies), the
+// chunk's results until the wave has finished the chunk (then stored coalesced).  Stored as they
+// came, every segment word and every result was a partial-line write of its own.
 template <class Tab>
 __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, int64_t* __restrict__ flag,
                                               int32_t* __restrict__ end_of) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_seg[RT][RUNS_MAX_SEGS];
+  __shared__ int32_t s_end[RT / 64][RUNS_CHUNK];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
   const int64_t i0 = wave * RUNS_CHUNK, i1 = i0 + RUNS_CHUNK < A.n ? i0 + RUNS_CHUNK : A.n;
-  if (i0 >= A.n) return;
-  int64_t seg_item = -1;                                        // the lane's current start record
-  int seg_last = -1, seg_n = 0;
-  run_engine(
-      T, A, i0, i1, [&](int64_t i, int64_t* j, int64_t* stop) { *j = i; *stop = INT64_MAX; return true; },
-      [&](int64_t i, const RunResult& res) {
-        flag[i] = res.end >= 0 ? 1 : 0;
-        end_of[i] = int32_t(res.end);
-        if (res.fail_at >= 0) {
-          A.err_code[i] = res.err;
-          atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
-        }
-        if (A.segs && res.end >= 0 && seg_item == i && seg_n < RUNS_MAX_SEGS) A.segs[i * RUNS_MAX_SEGS + seg_n] = ~0u;
-      },
-      [&](int64_t i, int64_t r, int stage) {
-        if (!A.segs) return;
-        if (i != seg_item) { seg_item = i; seg_last = -1; seg_n = 0; }
-        if (stage == seg_last) return;
-        seg_last = stage;
-        const int64_t off = r - i;
-        if (seg_n >= RUNS_MAX_SEGS || off >= (int64_t(1) << 24)) { atomicOr(A.seg_over, 1ull); return; }
-        A.segs[i * RUNS_MAX_SEGS + seg_n++] = uint32_t(stage) << 24 | uint32_t(off);
-      });
+  uint32_t* const myseg = s_seg[threadIdx.x];
+  if (i0 < A.n) {
+    int64_t seg_item = -1;                                      // the lane's current start record
+    int seg_last = -1, seg_n = 0;
+    run_engine(
+        T, A, i0, i1, [&](int64_t i, int64_t* j, int64_t* stop) { *j = i; *stop = INT64_MAX; return true; },
+        [&](int64_t i, const RunResult& res) {
+          s_end[wv][i - i0] = int32_t(res.end);
+          if (res.fail_at >= 0) {
+            A.err_code[i] = res.err;
+            atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
+          }
+          if (A.segs && res.end >= 0) {
+            if (seg_item != i) seg_n = 0;
+            for (int q = seg_n; q < RUNS_MAX_SEGS; q++) myseg[q] = ~0u;   // terminator (and padding)
+            uint4* d = reinterpret_cast<uint4*>(A.segs + i * RUNS_MAX_SEGS);
+            const uint4* sp = reinterpret_cast<const uint4*>(myseg);
+#pragma unroll
+            for (int q = 0; q < RUNS_MAX_SEGS / 4; q++) d[q] = sp[q];
+          }
+        },
+        [&](int64_t i, int64_t r, int stage) {
+          if (!A.segs) return;
+          if (i != seg_item) { seg_item = i; seg_last = -1; seg_n = 0; }
+          if (stage == seg_last) return;
+          seg_last = stage;
+          const int64_t off = r - i;
+          if (seg_n >= RUNS_MAX_SEGS || off >= (int64_t(1) << 24)) { atomicOr(A.seg_over, 1ull); return; }
+          myseg[seg_n++] = uint32_t(stage) << 24 | uint32_t(off);
+        });
+  }
+  __syncthreads();                                              // (every wave reaches it)
+  for (int64_t k = lane; k < i1 - i0; k += 64) {
+    const int32_t e = s_end[wv][k];
+    flag[i0 + k] = e >= 0 ? 1 : 0;
+    end_of[i0 + k] = e;
+  }
 }
 
 struct WriteArgs {

@@ -72,7 +72,8 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels", "cep_live_run_hwm",
            "cep_batch_errors", "cep_session_set_timing",
            "cep_key_profile", "cep_key_hash", "cep_key_shard", "cep_shard_plan", "cep_partition", "cep_gather",
-           "cep_match_count_to"]
+           "cep_match_count_to", "cep_state_evict", "cep_state_import_keys", "cep_state_positions",
+           "cep_session_set_max_key_words"]
 
 _lib = None
 
@@ -134,6 +135,10 @@ def lib():
     L.cep_partition.argtypes = [P, C.c_int64, C.c_int32, P, C.c_int64, P, P, C.c_int32, P]
     L.cep_gather.argtypes = [P, C.c_int32, P, C.c_int64, P, C.c_int32, P]
     L.cep_match_count_to.argtypes = [P, P, P]
+    L.cep_state_evict.argtypes = [P, P, C.c_int64, C.POINTER(C.c_void_p), P]
+    L.cep_state_import_keys.argtypes = [P, P, P, P, C.c_int64]
+    L.cep_state_positions.argtypes = [P, C.c_size_t, P, C.c_int64, C.POINTER(C.c_int64)]
+    L.cep_session_set_max_key_words.argtypes = [P, C.c_int64]
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -143,6 +148,16 @@ def lib():
 def check(rc: int):
     if rc != CEP_OK:
         raise CepError(rc, lib().cep_last_error().decode())
+
+
+def state_positions(blob: bytes) -> np.ndarray:
+    """cep_state_positions: stream positions of the records a state blob still references."""
+    n = C.c_int64()
+    check(lib().cep_state_positions(blob, len(blob), None, 0, C.byref(n)))
+    out = np.zeros(n.value, np.int64)
+    if n.value:
+        check(lib().cep_state_positions(blob, len(blob), out.ctypes.data, n.value, C.byref(n)))
+    return out
 
 
 class CompiledPattern:
@@ -314,6 +329,29 @@ class Session:
 
     def state_clear(self):
         check(lib().cep_state_clear(self.h))
+
+    def state_evict(self, keys) -> list:
+        """cep_state_evict: the listed key ids' state as single-key blobs (b"" for a key without
+        state), dropped from the device so that the ids are free."""
+        k = np.ascontiguousarray(keys, np.int32)
+        offs = np.zeros(len(k) + 1, np.int64)
+        p = C.c_void_p()
+        check(lib().cep_state_evict(self.h, k.ctypes.data, len(k), C.byref(p), offs.ctypes.data))
+        if not len(k) or offs[-1] == 0:
+            return [b""] * len(k)
+        raw = C.string_at(p.value, int(offs[-1]))
+        return [raw[int(offs[i]):int(offs[i + 1])] for i in range(len(k))]
+
+    def state_import_keys(self, blobs, keys):
+        """cep_state_import_keys: single-key blobs restored under new key ids."""
+        k = np.ascontiguousarray(keys, np.int32)
+        bufs = [C.create_string_buffer(b, max(1, len(b))) for b in blobs]
+        ptrs = (C.c_void_p * max(1, len(bufs)))(*[C.cast(b, C.c_void_p) for b in bufs])
+        lens = (C.c_size_t * max(1, len(bufs)))(*[len(b) for b in blobs])
+        check(lib().cep_state_import_keys(self.h, ptrs, lens, k.ctypes.data, len(k)))
+
+    def set_max_key_words(self, words: int):
+        check(lib().cep_session_set_max_key_words(self.h, int(words)))
 
     def key_state(self, key: int):
         """(NFA.getRuns(), run-queue length) of a key, or None if it has no state yet."""

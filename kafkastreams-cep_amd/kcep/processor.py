@@ -19,7 +19,17 @@ registers) plays the role of the reference's three stores.
   topic, across batches.
 * **Keys and topics** are interned to dense ids (``key_id`` for the carry
   session, topic ids from the pattern's ``Schema`` so that ``withTopic`` filters
-  keep their ids).
+  keep their ids).  The session holds ``max_keys`` key ids; a batch that needs
+  more spills the least recently used keys' state to the host
+  (``cep_state_evict``) and re-admits a spilled key under a free id when it
+  returns (``cep_state_import_keys``), so the number of distinct keys over the
+  stream's life is unbounded, like the reference's ``NFAStore``
+  (``NFAStoreImpl.java:34-85``).
+* **Capacity hand-off.**  A key the device hands back with ``CEP_E_RUN_CAPACITY``
+  (over ``max_key_words``) keeps its state as of the batch start; its records of
+  the batch are pushed again with the per-key cap lifted, so every record is
+  processed (``:134-150``).  Only a key that outgrows the whole device pool fails
+  the task.
 * **Values** are decoded into the schema's typed columns by a
   ``kcep.ingest.ColumnDecoder``.
 * **Forward order.**  Each batch is stable-sorted by key for the device; the
@@ -92,7 +102,7 @@ class GpuCEPProcessor:
 
     def __init__(self, queryName: str, pattern: Union[Pattern, bytes], schema: Schema, decoder: ColumnDecoder,
                  batch_size: int = 1 << 16, max_keys: int = 1 << 20, device: int = 0,
-                 mode: int = N.MODE_PROCESSOR, prune_at: int = 1 << 20):
+                 mode: int = N.MODE_PROCESSOR, prune_at: int = 1 << 20, max_key_words: int = 0):
         if decoder.schema is not schema and decoder.schema.columns != schema.columns:
             raise ValueError("decoder and pattern use different schemas")
         self.queryName = queryName.lower().replace("\\s+", "")
@@ -100,19 +110,31 @@ class GpuCEPProcessor:
         self.decoder = decoder
         self.batch_size = int(batch_size)
         self.max_keys = int(max_keys)
+        self.max_key_words = int(max_key_words)
         self.device = device
         self.mode = mode
         ir = pattern if isinstance(pattern, (bytes, bytearray)) else pattern.to_ir(schema)
         self.compiled = N.CompiledPattern(bytes(ir))
         self.session: Optional[N.Session] = None
         self._forward: Optional[Callable[[Any, Sequence], None]] = None
+        # record key -> device key id.  The session holds max_keys ids; when a batch needs more, the
+        # least recently used keys are spilled to the host (cep_state_evict) and re-admitted under a
+        # free id when they come back (cep_state_import_keys): the reference's NFAStore is unbounded
+        # (NFAStoreImpl.java:34-85).
         self._keys: Dict[Any, int] = {}
-        self._pending: List[Tuple[int, tuple, int, int, int, int, Event]] = []
+        self._id_key: Dict[int, Any] = {}
+        self._free: List[int] = []
+        self._next_id = 0
+        self._used = np.zeros(0, np.int64)        # per key id: the flush that last used it (LRU)
+        self._flushes = 0
+        self._spilled: Dict[Any, Tuple[bytes, np.ndarray]] = {}   # key -> (single-key blob, positions)
+        self._pending: List[Tuple[Any, tuple, int, int, int, int, Event]] = []
         self._log: Dict[int, Event] = {}          # stream position -> Event (carried runs point back here)
         self._failed: Optional[Exception] = None
-        self._hwm: Dict[Tuple[int, int], int] = {}  # stencil sessions: (key id, topic id) -> high-water mark
+        self._hwm: Dict[Tuple[Any, int], int] = {}  # stencil sessions: (record key, topic id) -> high-water mark
         self._prune_at = max(int(prune_at), 2 * self.batch_size)   # _log size that triggers a prune
         self._prune_min = self._prune_at
+        self.capacity_reruns = 0                  # keys re-run with the per-key workspace cap lifted
 
     # ---- Processor API (CEPProcessor.init/process/punctuate/close, :88-170) ----
     def init(self, forward: Callable[[Any, Sequence], None], session=None):
@@ -121,21 +143,16 @@ class GpuCEPProcessor:
         check the host logic without a GPU)."""
         self._forward = forward
         self.session = session or N.Session(self.compiled, self.batch_size, mode=self.mode, device=self.device,
-                                            carry=True, max_keys=self.max_keys)
+                                            carry=True, max_keys=self.max_keys, max_key_words=self.max_key_words)
 
     def process(self, key, value, topic: str, partition: int, offset: int, timestamp: int):
         """One record with its ``ProcessorContext`` metadata."""
         self._check()
         if key is None or value is None:                  # :135-138
             return
-        kid = self._keys.get(key)
-        if kid is None:
-            if len(self._keys) >= self.max_keys:
-                raise N.CepError(11, f"more than max_keys={self.max_keys} distinct keys")
-            kid = self._keys[key] = len(self._keys)
         row = self.decoder.row(value)
         ev = Event(key, value, int(timestamp), topic, int(partition), int(offset))
-        self._pending.append((kid, row, self.schema.topic_id(topic), int(partition), int(offset), int(timestamp), ev))
+        self._pending.append((key, row, self.schema.topic_id(topic), int(partition), int(offset), int(timestamp), ev))
         if len(self._pending) >= self.batch_size:
             self.flush()
 
@@ -151,14 +168,99 @@ class GpuCEPProcessor:
                 self.session.close()
                 self.session = None
 
+    # ---- key ids ----
+    def _key_ids(self, recs) -> np.ndarray:
+        """Device key id of every record: interned keys keep theirs; new and spilled keys take free
+        ids, spilling the least recently used keys of earlier batches when none is left."""
+        self._flushes += 1
+        want = list(dict.fromkeys(r[0] for r in recs))    # distinct keys, first-arrival order
+        if len(want) > self.max_keys:
+            raise N.CepError(11, f"one batch holds {len(want)} distinct keys, more than max_keys={self.max_keys}")
+        new = [k for k in want if k not in self._keys]
+        short = len(new) - len(self._free) - (self.max_keys - self._next_id)
+        if short > 0:
+            self._spill(max(short, self.max_keys // 8), set(want))
+        admit_keys, admit_ids, admit_blobs = [], [], []
+        for k in new:
+            kid = self._free.pop() if self._free else self._take_id()
+            self._keys[k] = kid
+            self._id_key[kid] = k
+            sp = self._spilled.pop(k, None)
+            if sp is not None:
+                admit_keys.append(k)
+                admit_ids.append(kid)
+                admit_blobs.append(sp[0])
+        if admit_ids:
+            self.session.state_import_keys(admit_blobs, admit_ids)
+        ids = np.fromiter((self._keys[r[0]] for r in recs), np.int32, len(recs))
+        if len(self._used) < self._next_id:
+            self._used = np.concatenate([self._used, np.zeros(self._next_id - len(self._used), np.int64)])
+        self._used[ids] = self._flushes
+        return ids
+
+    def _take_id(self) -> int:
+        self._next_id += 1
+        return self._next_id - 1
+
+    def _spill(self, count: int, busy: set):
+        """Move the ``count`` least recently used keys not in this batch to the host."""
+        cand = [kid for kid in np.argsort(self._used[:self._next_id], kind="stable")
+                if int(kid) in self._id_key and self._id_key[int(kid)] not in busy][:count]
+        if not cand:
+            return
+        blobs = self.session.state_evict(cand)
+        for kid, blob in zip(cand, blobs):
+            kid = int(kid)
+            k = self._id_key.pop(kid)
+            del self._keys[k]
+            self._free.append(kid)
+            if blob:                                      # a key without state starts afresh anyway
+                self._spilled[k] = (blob, N.state_positions(blob))
+
     # ---- batching ----
+    def _run(self, recs, idx):
+        """One cep_push_batch of the records ``recs[i] for i in idx`` (arrival indices, ascending),
+        grouped by key id.  Returns ``(matches, errors)``: per match (arrival index of the completing
+        record, key id, traversal entries as (name id, stream position)) in emission order, and per
+        failing key (arrival index, code)."""
+        n = len(idx)
+        kid = self._kid[idx]
+        perm = np.asarray(idx, np.int64)[np.argsort(kid, kind="stable")]   # arrival index of batch position
+        sorted_recs = [recs[i] for i in perm]
+        cols = self.decoder.columns([r[1] for r in sorted_recs])
+        topic = np.fromiter((r[2] for r in sorted_recs), np.int32, n)
+        part = np.fromiter((r[3] for r in sorted_recs), np.int32, n)
+        off = np.fromiter((r[4] for r in sorted_recs), np.int64, n)
+        ts = np.fromiter((r[5] for r in sorted_recs), np.int64, n)
+        base = self.session.stream_position()
+        for i, r in enumerate(sorted_recs):
+            self._log[base + i] = r[6]
+        try:
+            self.session.push(n, self._kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts,
+                              flags=self._flags)
+            out = self.session.collect(raise_on_error=False)
+        except N.CepError as e:                           # no state was committed for this batch:
+            self._failed = e                              # the task fails, as the reference's does
+            raise
+        mrec = out["match_record"] - base                 # stream position -> batch position
+        matches = []
+        for m in range(len(mrec)):
+            a, b = int(out["ent_off"][m]), int(out["ent_off"][m + 1])
+            matches.append((int(perm[mrec[m]]), int(out["match_key"][m]),
+                            [(int(out["ent_name"][i]), int(out["ent_record"][i])) for i in range(a, b)]))
+        errors = []
+        if out["err"]:
+            erec, ecode = self.session.batch_errors()
+            errors = [(int(perm[r - base]), int(c)) for r, c in zip(erec, ecode)]
+        return matches, errors
+
     def flush(self) -> int:
         """Push the buffered records as one batch and forward its matches; returns how many."""
         self._check()
         if not self._pending:
             return 0
         recs, self._pending = self._pending, []
-        flags = 0
+        self._flags = 0
         if self.session.path in (N.PATH_STENCIL, N.PATH_CHAIN):
             # the stencil path carries only each key's last records: the high-water-mark rule
             # (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the
@@ -172,50 +274,45 @@ class GpuCEPProcessor:
                 self._hwm[hk] = r[4] + 1
                 kept.append(r)
             recs = kept
-            flags = N.BATCH_OFFSETS_MONOTONE
+            self._flags = N.BATCH_OFFSETS_MONOTONE
             if not recs:
                 return 0
-        n = len(recs)
-        kid = np.fromiter((r[0] for r in recs), np.int32, n)
-        perm = np.argsort(kid, kind="stable")             # the device wants the batch grouped by key
-        sorted_recs = [recs[i] for i in perm]
-        cols = self.decoder.columns([r[1] for r in sorted_recs])
-        topic = np.fromiter((r[2] for r in sorted_recs), np.int32, n)
-        part = np.fromiter((r[3] for r in sorted_recs), np.int32, n)
-        off = np.fromiter((r[4] for r in sorted_recs), np.int64, n)
-        ts = np.fromiter((r[5] for r in sorted_recs), np.int64, n)
-        base = self.session.stream_position()
-        for i, r in enumerate(sorted_recs):
-            self._log[base + i] = r[6]
-        try:
-            self.session.push(n, kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts, flags=flags)
-            out = self.session.collect(raise_on_error=False)
-        except N.CepError as e:                           # no state was committed for this batch:
-            self._failed = e                              # the task fails, as the reference's does
-            raise
-
-        mrec = out["match_record"] - base                 # stream position -> batch position
-        m_arrival = perm[mrec] if len(mrec) else np.zeros(0, np.int64)
-        order = np.argsort(m_arrival, kind="stable")
+        self._kid = self._key_ids(recs)
+        matches, errors = self._run(recs, np.arange(len(recs)))
+        # keys over the per-key workspace cap (CEP_E_RUN_CAPACITY) are handed back with their state as
+        # of the batch start: re-run exactly their records with the cap lifted, so that every record
+        # is processed, as the reference's process() does (CEPProcessor.java:134-150)
+        cap = {self._kid[a] for a, c in errors if c == 9}
+        if cap:
+            matches = [m for m in matches if m[1] not in cap]
+            errors = [e for e in errors if e[1] != 9]
+            idx = np.flatnonzero(np.isin(self._kid, np.fromiter(cap, np.int32, len(cap))))
+            self.session.set_max_key_words(0)
+            try:
+                m2, e2 = self._run(recs, idx)
+            finally:
+                self.session.set_max_key_words(self.max_key_words)
+            self.capacity_reruns += len(cap)
+            if any(c == 9 for _, c in e2):
+                self._failed = N.CepError(9, "a key outgrew the whole device pool", min(a for a, c in e2 if c == 9))
+                raise self._failed
+            matches += m2
+            errors += e2
+        matches.sort(key=lambda m: m[0])                  # arrival order of the completing record (stable)
         limit = err_code = None
-        if out["err"]:                                    # the first failure in ARRIVAL order (cep_batch_errors)
-            erec, ecode = self.session.batch_errors()
-            arr = perm[erec - base]
-            j = int(np.argmin(arr))
-            limit, err_code = int(arr[j]), int(ecode[j])
+        if errors:                                        # the first failure in ARRIVAL order (cep_batch_errors)
+            limit, err_code = min(errors)
         names = self.compiled.names
         sent = 0
-        for m in order:
-            if limit is not None and m_arrival[m] >= limit:
+        for a, _, ents in matches:
+            if limit is not None and a >= limit:
                 break
-            a, b = int(out["ent_off"][m]), int(out["ent_off"][m + 1])
-            ents = [(int(out["ent_name"][i]), int(out["ent_record"][i])) for i in range(a, b)]
             seq = sequence_from_traversal(ents, names, self._log.__getitem__)
-            self._forward(recs[m_arrival[m]][6].key, seq)
+            self._forward(recs[a][6].key, seq)
             sent += 1
-        if not out["err"] and len(self._log) >= self._prune_at:
+        if not errors and len(self._log) >= self._prune_at:
             self._prune()
-        if out["err"]:
+        if errors:
             self._failed = N.CepError(err_code, N.ERRORS.get(err_code, "exception") + " in process()", limit)
             raise self._failed
         return sent
@@ -223,8 +320,11 @@ class GpuCEPProcessor:
     def _prune(self):
         """Drop the records no live run can reach any more: the device's carried state lists, per
         key, the events its runs and buffer nodes still reference (``cep_state_export``), each with
-        its stream position.  Runs only when the log has doubled since the last prune."""
+        its stream position; spilled keys keep theirs.  Runs only when the log has doubled since the
+        last prune."""
         keep = carried_positions(self.session.state_export())
+        for _, pos in self._spilled.values():
+            keep.update(int(x) for x in pos)
         self._log = {p: ev for p, ev in self._log.items() if p in keep}
         self._prune_at = max(self._prune_min, 2 * len(self._log))
 
@@ -234,7 +334,9 @@ class GpuCEPProcessor:
         and the records carried runs may still reference."""
         self.flush()
         return {"state": self.session.state_export(), "keys": dict(self._keys), "log": dict(self._log),
-                "topics": dict(self.schema.topics), "hwm": dict(self._hwm)}
+                "topics": dict(self.schema.topics), "hwm": dict(self._hwm),
+                "spilled": {k: v[0] for k, v in self._spilled.items()}, "next_id": self._next_id,
+                "free": list(self._free)}
 
     def restore(self, snap: dict):
         self._check()
@@ -252,6 +354,11 @@ class GpuCEPProcessor:
         self.session.state_clear()
         self.session.state_import(snap["state"])
         self._keys = dict(snap["keys"])
+        self._id_key = {i: k for k, i in self._keys.items()}
+        self._next_id = int(snap.get("next_id", max(self._keys.values(), default=-1) + 1))
+        self._free = list(snap.get("free", []))
+        self._used = np.zeros(self._next_id, np.int64)
+        self._spilled = {k: (b, N.state_positions(b)) for k, b in snap.get("spilled", {}).items()}
         self._log = dict(snap["log"])
         self._hwm = dict(snap.get("hwm", {}))
 

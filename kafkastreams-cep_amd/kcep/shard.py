@@ -183,15 +183,21 @@ class CountExchange:
         self.offset = torch.zeros(slots, dtype=torch.int64, device=device)   # this rank's global match offset
         self.total = torch.zeros(slots, 2, dtype=torch.int64, device=device)  # node-wide (events, matches)
         self.side = torch.cuda.Stream(device=device)
+        self.done = [None] * slots       # per slot: the side-stream event of its last exchange
         self.posted = 0
 
     def post(self, session: "N.Session", n_events: int, stream) -> int:
-        """Enqueue the exchange of the session's last batch; returns its slot."""
+        """Enqueue the exchange of the session's last batch; returns its slot.  Everything the
+        slot's inputs need is ordered on ``stream`` (the launch stream), after the slot's previous
+        exchange has finished reading them."""
         import torch
         import torch.distributed as dist
         k = self.posted % self.slots
         self.posted += 1
-        self.mine[k, 0].fill_(int(n_events))
+        if self.done[k] is not None:     # the slot is reused: its last all-gather must have read it
+            stream.wait_event(self.done[k])
+        with torch.cuda.stream(stream):
+            self.mine[k, 0].fill_(int(n_events))
         session.match_count_to(self.mine[k, 1].data_ptr(), stream.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(stream)
@@ -201,6 +207,8 @@ class CountExchange:
             c = self.allc[k, :, 1]
             self.offset[k] = (torch.cumsum(c, 0) - c)[self.rank]
             self.total[k] = self.allc[k].sum(0)
+            self.done[k] = torch.cuda.Event()
+            self.done[k].record(self.side)
         return k
 
     def wait(self):

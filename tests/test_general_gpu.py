@@ -221,6 +221,31 @@ def test_over_capacity_key_is_handed_back_alone(lane_nfa):
 
 
 @pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
+def test_key_over_capacity_at_first_allocation(lane_nfa):
+    """A key whose very first workspace allocation is already over cep_opts.max_key_words (5000
+    records against 1<<17 words) must still be listed by cep_batch_errors with CEP_E_RUN_CAPACITY
+    at its first record -- key_begin raises the batch's error flag, so the host reads the per-key
+    errors -- while every other key matches the oracle."""
+    rng = np.random.default_rng(5)
+    lens = [12] * 40
+    lens[7] = 5000
+    key = np.repeat(np.arange(40, dtype=np.int32), lens)
+    val = rng.integers(0, 4, len(key)).astype(np.int32)
+    ir = PL.any_any().to_ir(PL.I32)
+    want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
+    s = N.Session(N.CompiledPattern(ir), len(key), force_path=N.PATH_GENERAL, max_key_words=1 << 17,
+                  lane_nfa=lane_nfa)
+    s.push(len(key), key, [val])
+    out = s.collect(raise_on_error=False)
+    rec, code = s.batch_errors()
+    first7 = int(np.searchsorted(key, 7))
+    assert list(code) == [9] and list(rec) == [first7]
+    assert out["err"] == 9
+    got = product_matches(s, out)
+    assert got == [m for m in want if m[1] != 7]
+
+
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
 def test_c4_heavy_keys(lane_nfa):
     """C4 (skip-till-any times(3) + zeroOrMore) keys long enough that one record's run queue holds
     several rounds of 64 runs on the wave kernel; every match, in order, as the oracle's."""

@@ -1,0 +1,51 @@
+"""The JNI shim (jni/kcep_jni.c) without a GPU: compiled unchanged against tests/jni_stub/jni.h, it
+exports one symbol per ``native`` method of java/GpuCEPProcessor.java, and its host-only calls
+(pattern compile, stage names, blob positions) work through a mock JNIEnv with every pinned array
+released."""
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+
+from jni_twin import JniLib, LIB, NATIVES, PFX
+import patterns_lib as PL
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def jl():
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} missing: build it with `make -C tests/jni_stub` (__graft_entry__.build does)")
+    return JniLib()
+
+
+def test_java_natives_match_the_shim(jl):
+    src = open(os.path.join(ROOT, "java", "GpuCEPProcessor.java")).read()
+    java = re.findall(r"private static native [\w\[\]]+ (\w+)\(", src)
+    assert sorted(java) == sorted(NATIVES)
+    c = open(os.path.join(ROOT, "jni", "kcep_jni.c")).read()
+    assert sorted(re.findall(r"JNICALL CLS\((\w+)\)", c)) == sorted(NATIVES)
+    for n in NATIVES:
+        assert hasattr(jl.L, PFX + n)
+
+
+def test_compile_and_stage_names_through_the_shim(jl):
+    ir = PL.c5_optional().to_ir(PL.I32)
+    p = jl.cepCompile(ir)
+    assert p > 0
+    names = jl.cepStageNames(p)
+    assert names[0] == "$final" and len(names) >= 4
+    jl.cepPatternFree(p)
+    assert jl.cepCompile(b"\x00\x01") < 0 and jl.cepLastError()
+    assert jl.pins() == 0
+
+
+def test_state_positions_through_the_shim(jl):
+    # a KCSH blob (stencil carry): two keys with 2 and 1 carried records
+    blob = struct.pack("<IIqi", 0x4853434B, 1, 10, 2)
+    blob += struct.pack("<iiQqq", 3, 2, 0, 7, 9) + struct.pack("<iiQq", 5, 1, 0, 8)
+    assert list(jl.cepStatePositions(blob)) == [7, 9, 8]
+    assert jl.pins() == 0
