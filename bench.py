@@ -271,7 +271,7 @@ def main():
                 _carry_stream(pat, n, K, key, cols, stream, 0, n_matches, csum, value / world, reps=1, per=b,
                               host=host, collect=True) for b in args.processor_batch]
             del host
-        if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and args.carry_batches > 1:
+        if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS) and args.carry_batches > 1:
             line["carry_stream"] = _carry_stream(pat, n, K, key, cols, stream, args.carry_batches, n_matches, csum,
                                                  value / world)
         if world == 1 and not args.no_cpu_baseline:
@@ -352,7 +352,7 @@ def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, r
     nbat = len(bounds) - 1
     out = {"value": n / dt, "unit": "events/s", "batches": nbat, "events_per_batch": per,
            "ms_per_pass": dt * 1e3, "vs_resident": n / dt / resident,
-           "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain"}.get(cs.path, "general"),
+           "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain", N.PATH_RUNS: "runs"}.get(cs.path, "general"),
            "parity": bool(m == n_matches and c == csum), "matches": int(m)}
     if host is not None or collect:
         # per-batch cost above streaming the batch's records at the resident rate

@@ -100,11 +100,12 @@ typedef struct {
                                 one stopped.  Record positions in cep_matches are then stream positions
                                 (records pushed before the batch + index in the batch).  Strict fixed-length
                                 patterns (with or without optional() stages) stay on the stencil / chain path,
-                                which carries only each key's last K-1
-                                records and then takes batches without null records (valid) and with
-                                per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE; the host applies the
-                                high-water-mark rule); every other pattern carries its full NFA state on the
-                                general path. */
+                                which carries only each key's last K-1 records; patterns of the
+                                deterministic-runs path stay on it and carry each key's records from its oldest
+                                still-open run on (the runs are simulated again over them).  Both then take
+                                batches without null records (valid) and with per-key increasing offsets
+                                (CEP_BATCH_OFFSETS_MONOTONE; the host applies the high-water-mark rule); every
+                                other pattern carries its full NFA state on the general path. */
 
 #define CEP_SESSION_INTERPRET 2  /* runs path: use the built-in kernels, which interpret the pattern's predicates
                                     and folds, instead of kernels compiled for the pattern at cep_session_open

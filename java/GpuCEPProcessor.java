@@ -72,7 +72,7 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     private static native String cepLastError();
 
     private static final int CEP_MODE_PROCESSOR = 1, CEP_SESSION_CARRY = 1, CEP_E_RUN_CAPACITY = 9;
-    private static final int CEP_PATH_STENCIL = 1, CEP_PATH_CHAIN = 3, CEP_BATCH_OFFSETS_MONOTONE = 1;
+    private static final int CEP_PATH_STENCIL = 1, CEP_PATH_CHAIN = 3, CEP_PATH_RUNS = 4, CEP_BATCH_OFFSETS_MONOTONE = 1;
 
     private final String queryName;
     private final byte[] ir;
@@ -274,11 +274,12 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         List<Event<K, V>> recs = new ArrayList<>(pending);
         pending.clear();
         int flags = 0;
-        if (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN) {
-            // the stencil / chain paths carry only each key's last K-1 records: the high-water-mark
-            // rule (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the
-            // batch is declared clean.  A strict fixed-length pattern never throws, so every admitted
-            // record is processed and moves the mark.
+        if (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN || path == CEP_PATH_RUNS) {
+            // the stencil / chain / runs paths carry each key's records (its last K-1, or those from
+            // its oldest open run on), not its NFA: the high-water-mark rule
+            // (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the batch
+            // is declared clean.  Every admitted record is processed and moves the mark (a record that
+            // throws fails the task anyway).
             List<Event<K, V>> kept = new ArrayList<>(recs.size());
             for (Event<K, V> e : recs) {
                 Map<Integer, Long> hw = highWater.computeIfAbsent(e.key(), k -> new HashMap<>());

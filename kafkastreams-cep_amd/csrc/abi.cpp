@@ -193,6 +193,10 @@ struct cep_session {
   // ---- host CSR of the last collect ----
   std::vector<int64_t> match_record, ent_off, ent_record;
   std::vector<int32_t> match_key, ent_name, out_host;
+  // ---- carried tails of the runs path (CEP_SESSION_CARRY, runs.hip) ----
+  DBuf rtab, rpool, rpool2, rtop, e_key, e_topic, e_part, e_seg, e_off, e_ts, e_pos, rc_a, rc_b, rc_c, rc_d, gc_len, gc_off;
+  DBuf e_cols[16];
+  int64_t rpool_cap = 0, rpool_used = 0;   // tail records (5 + ncols int64 words each)
   bool collected = false;                  // the CSR above is the last batch's: a second collect re-uses it
   cep_matches last{};
   std::vector<uint8_t> evict_buf;          // cep_state_evict's blobs
@@ -359,8 +363,41 @@ int stage_inputs(cep_session* s, const cep_batch* b, hipStream_t st, NfaArgs& A)
 
 // Deterministic strict runs (runs.hip): one lane per start record, completed runs
 // ordered by (completing record, start), traversals written into the general CSR.
+int tail_rw(const cep_session* s) { return 5 + int(s->pat->prog.coltypes.size()); }
+bool tail_session(const cep_session* s) { return s->carry && s->path == CEP_PATH_RUNS; }
+
+// the tail pool with room for `more` records beyond the used ones (compacted / grown when short)
+int tail_reserve(cep_session* s, int64_t more, hipStream_t st) {
+  if (s->rpool_used + more <= s->rpool_cap) return CEP_OK;
+  const int RW = tail_rw(s);
+  const int64_t nk = s->opts.max_keys;
+  const int64_t cap = std::max<int64_t>(2 * (s->rpool_used + more), int64_t(1) << 16);
+  if (s->rpool2.ensure(size_t(cap) * RW * 8) || s->gc_len.ensure(size_t(nk + 1) * 8) || s->gc_off.ensure(size_t(nk + 1) * 8) ||
+      s->scan_tmp.ensure(size_t(nk / 1024 + 4) * 8))
+    return fail(CEP_E_HIP, "tail pool allocation failed");
+  if (s->rpool_used > 0)
+    HIPCHECK(runs_carry_gc(s->rtab.as<int64_t>(), nk, RW, s->rpool.as<int64_t>(), s->rpool2.as<int64_t>(),
+                           s->gc_len.as<int64_t>(), s->gc_off.as<int64_t>(), s->rtop.as<int64_t>(), s->scan_tmp.as<int64_t>(),
+                           st));
+  else
+    HIPCHECK(hipMemsetAsync(s->rtop.p, 0, 8, st));
+  int64_t live = 0;
+  HIPCHECK(hipMemcpyAsync(&live, s->rtop.p, 8, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  std::swap(s->rpool, s->rpool2);
+  s->rpool2.release();
+  s->rpool_cap = cap;
+  s->rpool_used = live;
+  return CEP_OK;
+}
+
+// Deterministic strict runs (runs.hip): one lane per start record, completed runs
+// ordered by (completing record, start), traversals written into the general CSR.
+// Carry sessions prefix every key's records with its carried tail (runs.hip) and keep the tails of
+// the runs still open at the batch end.
 int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
-  const int64_t n = b->n;
+  const int64_t nb = b->n;                        // the batch's records
+  int64_t n = nb;                                 // records simulated (carry: plus the keys' tails)
   NfaArgs in{};
   int rc = stage_inputs(s, b, st, in);
   if (rc) return rc;
@@ -378,8 +415,56 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     HIPCHECK(hipEventRecord(s->eb1, st));
     return CEP_OK;
   }
+  const bool rcarry = tail_session(s);
+  RcExt X{};
+  const int32_t* bkey = in.key;                   // the batch's own key column (segments index it)
+  if (rcarry) {
+    const Program& PP = s->pat->prog;
+    if (s->flag.ensure(size_t(nb) * 8) || s->idx.ensure(size_t(nb) * 8) || s->seg.ensure(size_t(nb + 1) * 8) ||
+        s->scan_tmp.ensure(size_t(nb / 1024 + 4) * 8) || s->rc_a.ensure(size_t(nb + 2) * 8) ||
+        s->rc_b.ensure(size_t(nb + 2) * 8) || s->ctl.ensure(64))
+      return fail(CEP_E_HIP, "allocation failed");
+    int64_t* scal = s->scal.as<int64_t>();
+    HIPCHECK(nfa_segments(in.key, nb, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
+                          s->scan_tmp.as<int64_t>(), st));
+    HIPCHECK(hipMemsetAsync(scal + 1, 0, 8, st));
+    HIPCHECK(carry_keycheck_launch(nb, scal, in.key, s->seg.as<int64_t>(), int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
+                                   s->kstamp.as<int32_t>(), ++s->batch_no, reinterpret_cast<unsigned long long*>(scal + 1), st));
+    RcIn B{};
+    B.key = in.key; B.topic = in.topic; B.partition = in.partition; B.offset = in.offset; B.ts = in.ts;
+    for (int c = 0; c < 16; c++) B.cols[c] = in.cols[c];
+    HIPCHECK(runs_carry_build(B, nb, s->base, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
+                              s->rtab.as<int64_t>(), s->rpool.as<int64_t>(), s->rc_a.as<int64_t>(), s->rc_b.as<int64_t>(),
+                              scal + 5, s->scan_tmp.as<int64_t>(), X, st, true));
+    int64_t h[6];
+    HIPCHECK(hipMemcpyAsync(h, scal, sizeof h, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (h[1] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    if (h[1] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+    n = nb + h[5];
+    if (n >= (int64_t(1) << 31)) return fail(CEP_E_RUN_CAPACITY, "carried tails make the batch exceed 2^31 records");
+    const size_t e4 = size_t(n) * 4, e8 = size_t(n) * 8;
+    if (s->e_key.ensure(e4) || s->e_topic.ensure(e4) || s->e_part.ensure(e4) || s->e_seg.ensure(e4) ||
+        s->e_off.ensure(e8) || s->e_ts.ensure(e8) || s->e_pos.ensure(e8))
+      return fail(CEP_E_HIP, "allocation failed");
+    X.key = s->e_key.as<int32_t>(); X.topic = s->e_topic.as<int32_t>(); X.partition = s->e_part.as<int32_t>();
+    X.seg = s->e_seg.as<int32_t>(); X.offset = s->e_off.as<int64_t>(); X.ts = s->e_ts.as<int64_t>();
+    X.pos = s->e_pos.as<int64_t>();
+    X.ncols = int32_t(PP.coltypes.size());
+    for (int c = 0; c < X.ncols; c++) {
+      X.coltype[c] = PP.coltypes[c];
+      if (s->e_cols[c].ensure(size_t(n) * type_size(PP.coltypes[c]))) return fail(CEP_E_HIP, "allocation failed");
+      X.cols[c] = s->e_cols[c].p;
+    }
+    HIPCHECK(runs_carry_build(B, nb, s->base, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
+                              s->rtab.as<int64_t>(), s->rpool.as<int64_t>(), s->rc_a.as<int64_t>(), s->rc_b.as<int64_t>(),
+                              scal + 5, s->scan_tmp.as<int64_t>(), X, st, false));
+    in.key = X.key; in.topic = X.topic; in.partition = X.partition; in.offset = X.offset; in.ts = X.ts;
+    for (int c = 0; c < X.ncols; c++) in.cols[c] = X.cols[c];
+    if ((rc = tail_reserve(s, n, st))) return rc;    // room for the new tails (at most every record)
+  }
   if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
-      s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 2) * 8) ||
+      s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 4) * 8) ||
       s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->r_endof.ensure(size_t(n) * 4) ||
       s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) || s->r_blk.ensure(size_t(n / 256 + 2) * 16))
     return fail(CEP_E_HIP, "allocation failed");
@@ -389,6 +474,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   for (int c = 0; c < 16; c++) A.cols[c] = in.cols[c];
   A.n = n;
   A.base = 0;
+  A.pos = rcarry ? X.pos : nullptr;               // carry: stream positions; runs ending in a tail are old
+  A.emit_from = s->base;
   unsigned long long* ctl = s->ctl.as<unsigned long long>();
   A.nmatch = ctl;
   A.err_min = ctl + 1;
@@ -408,18 +495,34 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->r_endof.as<int32_t>(), n,
                                s->rk.as<unsigned long long>(), s->r_blk.as<int64_t>(), s->r_blk.as<int64_t>() + nblk,
                                reinterpret_cast<int64_t*>(ctl + 2), s->scan_tmp.as<int64_t>(), st));
+  if (rcarry) {                                    // the keys' new tails: from their oldest still-open start
+    if (s->rc_c.ensure(size_t(nb + 2) * 8) || s->rc_d.ensure(size_t(nb + 2) * 8))
+      return fail(CEP_E_HIP, "allocation failed");
+    HIPCHECK(runs_carry_tails(X, n, nb, scal0, s->seg.as<int64_t>(), bkey, s->rc_b.as<int64_t>(), s->r_endof.as<int32_t>(),
+                              reinterpret_cast<unsigned long long*>(s->rc_a.as<int64_t>()), s->rc_c.as<int64_t>(),
+                              s->rc_d.as<int64_t>(), scal0 + 6, s->scan_tmp.as<int64_t>(), s->rtop.as<int64_t>(),
+                              s->rpool.as<int64_t>(), s->rtab.as<int64_t>(), st));
+  }
   // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow
   unsigned long long res[4];
+  int64_t top = 0;
   HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(&res[0], scal0 + 3, 8, hipMemcpyDeviceToHost, st));
+  if (rcarry) HIPCHECK(hipMemcpyAsync(&top, s->rtop.p, 8, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
+  if (rcarry) {
+    s->rpool_used = top;
+    s->base += nb;
+  }
   const int64_t nm = int64_t(res[0]), ne = int64_t(res[2]);
   if (nm > n) return fail(CEP_E_RUN_CAPACITY, "more completed runs than records");
   if (res[1] != ~0ull) {                           // the reference's first exception
-    const int64_t at = int64_t(res[1] >> 31), j = int64_t(res[1] & 0x7FFFFFFFull);
+    int64_t at = int64_t(res[1] >> 31);
+    const int64_t j = int64_t(res[1] & 0x7FFFFFFFull);
     int32_t code = 0;
     HIPCHECK(hipMemcpy(&code, s->r_errcode.as<int32_t>() + j, 4, hipMemcpyDeviceToHost));
     if (code == CEP_E_UNSUPPORTED) return fail(CEP_E_UNSUPPORTED, "sequence condition on the runs path");
+    if (rcarry) HIPCHECK(hipMemcpy(&at, X.pos + at, 8, hipMemcpyDeviceToHost));   // its stream position
     s->g_err = code;
     s->g_err_rec = at;
     s->e_rec.push_back(at);                        // the runs path keeps only the first exception
@@ -431,7 +534,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   HIPCHECK(runs_sort(nullptr, nullptr, nm, bits, nullptr, &tmp_bytes, st));
   const size_t nmb = size_t(std::max<int64_t>(nm, 1)), neb = size_t(std::max<int64_t>(ne, 1));
   if (s->rk_tmp.ensure(std::max<size_t>(tmp_bytes, 16)) || s->r_len.ensure(nmb * 8) || s->r_entoff.ensure(nmb * 8) ||
-      s->scan_tmp.ensure(size_t(nm / 1024 + 2) * 8) || s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) ||
+      s->scan_tmp.ensure(size_t(nm / 1024 + 4) * 8) || s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) ||
       s->o_entoff.ensure(nmb * 8) || s->o_name.ensure(neb * 4) || s->o_entrec.ensure(neb * 8))
     return fail(CEP_E_HIP, "allocation failed");
   if (nm > 0)
@@ -719,10 +822,6 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   const bool carry = opts->flags & CEP_SESSION_CARRY;
   if (carry && (opts->max_keys <= 0 || opts->max_keys > INT32_MAX))
     return fail(CEP_E_ARG, "carry sessions need max_keys (dense key ids in [0, max_keys))");
-  if (carry && path == CEP_PATH_RUNS) {          // (runs: not carried yet)
-    if (opts->force_path) return fail(CEP_E_UNSUPPORTED, "carried state runs on the stencil, chain and general paths");
-    path = CEP_PATH_GENERAL;
-  }
   if (carry && !P.general_ok)
     return fail(CEP_E_UNSUPPORTED, "pattern cannot be lowered to the device NFA: " + P.general_why);
   HIPCHECK(hipSetDevice(opts->device));
@@ -766,6 +865,13 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
         s->hpos.ensure(size_t(opts->max_keys) * 2 * size_t(std::max(1, P.stencil.k - 1)) * 8) ||
         hipMemset(s->halo.p, 0, size_t(opts->max_keys) * sizeof(HaloHdr)) || hipMemset(s->hflags.p, 0, 8))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
+  } else if (carry && path == CEP_PATH_RUNS) {    // per key a carried tail, none yet (runs.hip)
+    s->carry = true;
+    if (s->rtab.ensure(size_t(opts->max_keys) * 16) || s->rtop.ensure(8) || s->kstamp.ensure(size_t(opts->max_keys) * 4) ||
+        hipMemset(s->rtab.p, 0, size_t(opts->max_keys) * 16) || hipMemset(s->rtop.p, 0, 8) ||
+        hipMemset(s->kstamp.p, 0, size_t(opts->max_keys) * 4))
+      return cleanup(fail(CEP_E_HIP, "device allocation failed"));
+    if (tail_reserve(s, std::min<int64_t>(cap, int64_t(1) << 20), nullptr)) return cleanup(CEP_E_HIP);
   } else if (carry) {                            // NFAStore: no key has state yet
     s->carry = true;
     s->cpool_words = std::max<int64_t>(int64_t(1) << 20, opts->max_keys * 64);
@@ -796,9 +902,12 @@ void cep_session_close(cep_session* s) {
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
                   &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_segs, &s->r_blk, &s->r_len, &s->r_entoff,
-                  &s->r_errcode, &s->r_endof, &s->r_prof})
+                  &s->r_errcode, &s->r_endof, &s->r_prof, &s->rtab, &s->rpool, &s->rpool2, &s->rtop, &s->e_key,
+                  &s->e_topic, &s->e_part, &s->e_seg, &s->e_off, &s->e_ts, &s->e_pos, &s->rc_a, &s->rc_b, &s->rc_c,
+                  &s->rc_d, &s->gc_len, &s->gc_off})
     b->release();
   for (auto& c : s->h_cols) c.release();
+  for (auto& c : s->e_cols) c.release();
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->eb0) (void)hipEventDestroy(s->eb0);
@@ -909,6 +1018,9 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   }
   if (s->carry && (s->path == CEP_PATH_STENCIL || s->path == CEP_PATH_CHAIN))   // the halo cannot be carried through the general path
     return fail(CEP_E_UNSUPPORTED, "a stencil carry session takes batches without null records (valid) and with "
+                                   "per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE)");
+  if (s->carry && s->path == CEP_PATH_RUNS)      // nor the runs path's carried tails
+    return fail(CEP_E_UNSUPPORTED, "a runs carry session takes batches without null records (valid) and with "
                                    "per-key increasing offsets (CEP_BATCH_OFFSETS_MONOTONE)");
   if (!P.general_ok)
     return fail(CEP_E_UNSUPPORTED, "batch needs the general NFA path, which this pattern cannot use: " + P.general_why);
@@ -1191,6 +1303,87 @@ int halo_import(cep_session* s, const uint8_t* p, size_t len) {
   return CEP_OK;
 }
 
+// runs carry sessions: "KCSR", version 1, int64 next stream position, int32 key count, then per key with
+// a tail: int32 key id, int32 records, int32 words per record (5 + ncols), int32 0, then the records
+// (runs.hip tail records: stream position first)
+constexpr uint32_t kTailMagic = 0x5253434Bu;   // "KCSR"
+int tail_download(cep_session* s, std::vector<int64_t>& tab, std::vector<int64_t>& pool) {
+  tab.resize(size_t(s->opts.max_keys) * 2);
+  pool.resize(size_t(s->rpool_used) * size_t(tail_rw(s)));
+  HIPCHECK(hipMemcpy(tab.data(), s->rtab.p, tab.size() * 8, hipMemcpyDeviceToHost));
+  if (!pool.empty()) HIPCHECK(hipMemcpy(pool.data(), s->rpool.p, pool.size() * 8, hipMemcpyDeviceToHost));
+  return CEP_OK;
+}
+// appends key k's tail entry (key, records, words) to out; returns its record count
+int64_t tail_entry(const cep_session* s, const std::vector<int64_t>& tab, const std::vector<int64_t>& pool, int32_t k,
+                   std::vector<uint8_t>& out) {
+  const int64_t L = tab[2 * size_t(k) + 1];
+  if (L <= 0) return 0;
+  const size_t RW = size_t(tail_rw(s)), at = out.size();
+  const int32_t cnt = int32_t(L), rw = int32_t(RW), zero = 0;
+  out.resize(at + 16 + size_t(L) * RW * 8);
+  memcpy(&out[at], &k, 4); memcpy(&out[at + 4], &cnt, 4); memcpy(&out[at + 8], &rw, 4); memcpy(&out[at + 12], &zero, 4);
+  memcpy(&out[at + 16], pool.data() + size_t(tab[2 * size_t(k)]) * RW, size_t(L) * RW * 8);
+  return L;
+}
+int tail_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed) {
+  std::vector<int64_t> tab, pool;
+  int rc = tail_download(s, tab, pool);
+  if (rc) return rc;
+  std::vector<uint8_t> out(20);
+  int32_t nkeys = 0;
+  for (int32_t k = key_lo; k < key_hi; k++) nkeys += tail_entry(s, tab, pool, k, out) > 0;
+  const uint32_t ver = 1;
+  memcpy(&out[0], &kTailMagic, 4); memcpy(&out[4], &ver, 4); memcpy(&out[8], &s->base, 8); memcpy(&out[16], &nkeys, 4);
+  *needed = out.size();
+  if (!buf) return CEP_OK;
+  if (cap < out.size()) return fail(CEP_E_ARG, "export buffer too small");
+  memcpy(buf, out.data(), out.size());
+  return CEP_OK;
+}
+int tail_import(cep_session* s, const uint8_t* p, size_t len) {
+  int64_t base;
+  int32_t nkeys;
+  memcpy(&base, p + 8, 8); memcpy(&nkeys, p + 16, 4);
+  const size_t RW = size_t(tail_rw(s));
+  std::vector<std::pair<int32_t, size_t>> ents;
+  size_t at = 20, recs = 0;
+  for (int32_t i = 0; i < nkeys; i++) {
+    if (at + 16 > len) return fail(CEP_E_ARG, "truncated state blob");
+    int32_t k, cnt, rw;
+    memcpy(&k, p + at, 4); memcpy(&cnt, p + at + 4, 4); memcpy(&rw, p + at + 8, 4);
+    if (rw != int32_t(RW)) return fail(CEP_E_ARG, "state blob does not match this pattern");
+    if (k < 0 || k >= s->opts.max_keys || cnt <= 0 || at + 16 + size_t(cnt) * RW * 8 > len)
+      return fail(CEP_E_ARG, "bad key entry in the state blob");
+    ents.push_back({k, at});
+    recs += size_t(cnt);
+    at += 16 + size_t(cnt) * RW * 8;
+  }
+  HIPCHECK(hipSetDevice(s->device));
+  if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
+  int rc = tail_reserve(s, int64_t(recs), s->stream);
+  if (rc) return rc;
+  std::vector<int64_t> tab(size_t(s->opts.max_keys) * 2);
+  HIPCHECK(hipMemcpy(tab.data(), s->rtab.p, tab.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<int64_t> words(recs * RW);
+  int64_t w0 = 0;
+  for (auto& e : ents) {
+    int32_t cnt;
+    memcpy(&cnt, p + e.second + 4, 4);
+    memcpy(words.data() + size_t(w0) * RW, p + e.second + 16, size_t(cnt) * RW * 8);
+    tab[2 * size_t(e.first)] = s->rpool_used + w0;
+    tab[2 * size_t(e.first) + 1] = cnt;
+    w0 += cnt;
+  }
+  if (recs) HIPCHECK(hipMemcpy(s->rpool.as<int64_t>() + size_t(s->rpool_used) * RW, words.data(), words.size() * 8,
+                               hipMemcpyHostToDevice));
+  HIPCHECK(hipMemcpy(s->rtab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+  s->rpool_used += int64_t(recs);
+  HIPCHECK(hipMemcpy(s->rtop.p, &s->rpool_used, 8, hipMemcpyHostToDevice));
+  s->base = std::max(s->base, base);
+  return CEP_OK;
+}
+
 int cep_state_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, size_t cap, size_t* needed) {
   int rc = need_carry(s);
   if (rc) return rc;
@@ -1200,6 +1393,7 @@ int cep_state_export(cep_session* s, int32_t key_lo, int32_t key_hi, void* buf, 
   key_lo = std::max<int32_t>(key_lo, 0);
   key_hi = int32_t(std::min<int64_t>(key_hi, s->opts.max_keys));
   if (halo_session(s)) return halo_export(s, key_lo, key_hi, buf, cap, needed);
+  if (tail_session(s)) return tail_export(s, key_lo, key_hi, buf, cap, needed);
   std::vector<int64_t> tab(size_t(std::max(0, key_hi - key_lo)));
   if (!tab.empty()) HIPCHECK(hipMemcpy(tab.data(), s->ctab.as<int64_t>() + key_lo, tab.size() * 8, hipMemcpyDeviceToHost));
   std::vector<int32_t> pool(size_t(s->cpool_used));
@@ -1237,6 +1431,10 @@ int cep_state_import(cep_session* s, const void* buf, size_t len) {
   if (halo_session(s)) {
     if (magic != kHaloMagic || ver != 1 || nkeys < 0) return fail(CEP_E_ARG, "bad state blob (stencil sessions take KCSH)");
     return halo_import(s, p, len);
+  }
+  if (tail_session(s)) {
+    if (magic != kTailMagic || ver != 1 || nkeys < 0) return fail(CEP_E_ARG, "bad state blob (runs sessions take KCSR)");
+    return tail_import(s, p, len);
   }
   if (magic != kStateMagic || ver != 1 || nkeys < 0) return fail(CEP_E_ARG, "bad state blob");
   const DevProgram& D = s->pat->prog.dev;
@@ -1290,6 +1488,12 @@ int cep_state_clear(cep_session* s) {
     s->halo_stamp = 0;
     return CEP_OK;
   }
+  if (tail_session(s)) {
+    HIPCHECK(hipMemset(s->rtab.p, 0, size_t(s->opts.max_keys) * 16));
+    HIPCHECK(hipMemset(s->rtop.p, 0, 8));
+    s->rpool_used = 0;
+    return CEP_OK;
+  }
   HIPCHECK(hipMemset(s->ctab.p, 0xFF, size_t(s->opts.max_keys) * 8));
   s->cpool_used = 0;
   return CEP_OK;
@@ -1301,6 +1505,8 @@ int cep_key_state(cep_session* s, int32_t key, int64_t* runs, int64_t* queue_len
   if (!runs || !queue_len || key < 0 || key >= s->opts.max_keys) return fail(CEP_E_ARG, "bad argument");
   if (halo_session(s))
     return fail(CEP_E_UNSUPPORTED, "a stencil carry session keeps each key's last records, not its NFA runs");
+  if (tail_session(s))
+    return fail(CEP_E_UNSUPPORTED, "a runs carry session keeps each key's records from its oldest open run, not its NFA queue");
   HIPCHECK(hipSetDevice(s->device));
   if (s->stream) HIPCHECK(hipStreamSynchronize(s->stream));
   int64_t off = -1;
@@ -1356,6 +1562,19 @@ int cep_state_evict(cep_session* s, const int32_t* keys, int64_t n, const uint8_
       offs[i + 1] = int64_t(out.size());
     }
     HIPCHECK(hipMemcpy(s->halo.p, tab.data(), tab.size() * sizeof(HaloHdr), hipMemcpyHostToDevice));
+  } else if (tail_session(s)) {
+    std::vector<int64_t> tab, pool;
+    int rc2 = tail_download(s, tab, pool);
+    if (rc2) return rc2;
+    for (int64_t i = 0; i < n; i++) {
+      if (tab[2 * size_t(keys[i]) + 1] > 0) {
+        header(kTailMagic, 1);
+        tail_entry(s, tab, pool, keys[i], out);
+      }
+      tab[2 * size_t(keys[i]) + 1] = 0;              // (the pool records are reclaimed by the next compaction)
+      offs[i + 1] = int64_t(out.size());
+    }
+    HIPCHECK(hipMemcpy(s->rtab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
   } else {
     std::vector<int64_t> tab(size_t(s->opts.max_keys));
     HIPCHECK(hipMemcpy(tab.data(), s->ctab.p, tab.size() * 8, hipMemcpyDeviceToHost));
@@ -1387,7 +1606,7 @@ int cep_state_import_keys(cep_session* s, const void* const* blobs, const size_t
   if (n < 0 || (n > 0 && (!blobs || !lens || !keys))) return fail(CEP_E_ARG, "null argument");
   // one multi-key blob with the keys renumbered, then the ordinary import
   std::vector<uint8_t> all(20);
-  const uint32_t magic = halo_session(s) ? kHaloMagic : kStateMagic, ver = 1;
+  const uint32_t magic = halo_session(s) ? kHaloMagic : tail_session(s) ? kTailMagic : kStateMagic, ver = 1;
   int64_t base = 0;
   int32_t nk = 0;
   for (int64_t i = 0; i < n; i++) {
@@ -1416,7 +1635,7 @@ int cep_state_positions(const void* buf, size_t len, int64_t* out, int64_t cap, 
   uint32_t magic;
   int32_t nkeys;
   memcpy(&magic, p, 4); memcpy(&nkeys, p + 16, 4);
-  if ((magic != kStateMagic && magic != kHaloMagic) || nkeys < 0) return fail(CEP_E_ARG, "bad state blob");
+  if ((magic != kStateMagic && magic != kHaloMagic && magic != kTailMagic) || nkeys < 0) return fail(CEP_E_ARG, "bad state blob");
   int64_t cnt = 0;
   size_t at = 20;
   auto put = [&](int64_t v) { if (out && cnt < cap) out[cnt] = v; cnt++; };
@@ -1424,6 +1643,19 @@ int cep_state_positions(const void* buf, size_t len, int64_t* out, int64_t cap, 
     if (at + 8 > len) return fail(CEP_E_ARG, "truncated state blob");
     int32_t w;
     memcpy(&w, p + at + 4, 4);
+    if (magic == kTailMagic) {                       // key, records, words per record, 0, records (pos first)
+      int32_t rw;
+      if (at + 16 > len) return fail(CEP_E_ARG, "truncated state blob");
+      memcpy(&rw, p + at + 8, 4);
+      if (w <= 0 || rw < 5 || at + 16 + size_t(w) * size_t(rw) * 8 > len) return fail(CEP_E_ARG, "truncated state blob");
+      for (int32_t j = 0; j < w; j++) {
+        int64_t v;
+        memcpy(&v, p + at + 16 + size_t(j) * size_t(rw) * 8, 8);
+        put(v);
+      }
+      at += 16 + size_t(w) * size_t(rw) * 8;
+      continue;
+    }
     if (magic == kHaloMagic) {                       // key, records, masks, positions[records]
       if (w < 0 || at + 16 + 8 * size_t(w) > len) return fail(CEP_E_ARG, "truncated state blob");
       for (int32_t j = 0; j < w; j++) {

@@ -348,6 +348,12 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // LDS arena words of the wave kernel's key workspace (KCEP_WAVE_ARENA, tuning only)
   const char* aenv = getenv("KCEP_WAVE_ARENA");
   if (aenv) o += "#define WAVE_ARENA " + std::to_string(std::min(8192, std::max(4, atoi(aenv)))) + "\n";
+  // LDS words per lane of the wave kernel's private run lists / logs (KCEP_WAVE_PRIV, tuning only; 0: pool)
+  const char* penv = getenv("KCEP_WAVE_PRIV");
+  if (penv) {
+    const int pw = atoi(penv);
+    o += "#define WAVE_PRIV " + std::to_string(pw <= 0 ? 0 : std::min(64, std::max(12, (pw + 3) & ~3))) + "\n";
+  }
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
        "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
   kcep::nfa_kernel_body(A);

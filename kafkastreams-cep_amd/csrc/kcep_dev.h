@@ -176,6 +176,10 @@ struct RunsArgs {
   // terminated by ~0u when shorter (a run's consumed stages never increase, runs.hip); null: off
   uint32_t* segs;
   unsigned long long* seg_over;   // set when a run needs more segments or an offset >= 2^24
+  // carry sessions (runs.hip, carried tails): stream position of every record (null: base + index);
+  // runs ending or failing at a position < emit_from were handled by an earlier batch (not emitted)
+  const int64_t* pos;
+  int64_t emit_from;
 };
 constexpr int RUNS_MAX_SEGS = 8;
 

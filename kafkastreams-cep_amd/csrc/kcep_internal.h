@@ -1,6 +1,7 @@
 // kcep_internal.h — compiled-pattern representation shared by the host
 // compiler (compile.cpp) and the HIP kernels (stencil.hip, nfa.hip).
 #pragma once
+#include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include "kcep_dev.h"
 
@@ -173,5 +174,34 @@ struct StencilLaunch {
 // compile.cpp
 int lower_general(Program& P, std::string& why);
 int compile_ir(const uint8_t* ir, size_t len, Program& out, std::string& err);
+
+// ---- carried tails of the runs path (CEP_SESSION_CARRY, runs.hip) ----
+// the batch's columns as runs_carry_build reads them (device pointers; optional ones may be null)
+struct RcIn {
+  const int32_t* key;
+  const int32_t* topic;
+  const int32_t* partition;
+  const int64_t* offset;
+  const int64_t* ts;
+  const void* cols[16];
+};
+// the extended batch: each key's carried tail, then its records of the batch; seg = batch segment
+struct RcExt {
+  int32_t *key, *topic, *partition, *seg;
+  int64_t *offset, *ts, *pos;
+  void* cols[16];
+  int32_t coltype[16];
+  int32_t ncols;
+};
+hipError_t runs_carry_build(const RcIn& B, int64_t n, int64_t base, const int64_t* seg_flag, const int64_t* seg_idx,
+                            const int64_t* seg_start, const int64_t* nseg, const int64_t* rtab, const int64_t* rpool,
+                            int64_t* tlen, int64_t* toff, int64_t* total, int64_t* scan_tmp, const RcExt& X,
+                            hipStream_t st, bool lens_only);
+hipError_t runs_carry_tails(const RcExt& X, int64_t ext_n, int64_t n, const int64_t* nseg, const int64_t* seg_start,
+                            const int32_t* key, const int64_t* toff, const int32_t* end_of, unsigned long long* tstart,
+                            int64_t* newlen, int64_t* noff, int64_t* new_total, int64_t* scan_tmp, int64_t* top,
+                            int64_t* rpool, int64_t* rtab, hipStream_t st);
+hipError_t runs_carry_gc(int64_t* rtab, int64_t nkeys, int RW, const int64_t* src, int64_t* dst, int64_t* len,
+                         int64_t* off, int64_t* total, int64_t* scan_tmp, hipStream_t st);
 
 }  // namespace kcep

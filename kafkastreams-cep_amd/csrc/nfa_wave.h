@@ -34,6 +34,9 @@ constexpr int WAVE = 64;
 #ifndef WAVE_ARENA
 #define WAVE_ARENA 2048                    // LDS words per key workspace (KCEP_WAVE_ARENA A/B: 0 = pool only)
 #endif
+#ifndef WAVE_PRIV
+#define WAVE_PRIV 16                       // LDS words per lane for its private run list + operation log
+#endif                                     // (KCEP_WAVE_PRIV A/B; 0 = in the pool)
 
 // the key's shared workspace descriptor (LDS); lanes keep register copies in their Lane
 struct WaveShared {
@@ -383,13 +386,23 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   l.rec_out_top = 0; l.rec_nmatch = 0;
   l.slm = 0; l.sle = 0; l.flen = 0; l.tlen = 0;
   ws_to_lane(l, w);
-  // private run lists and operation logs
+  // private run lists and operation logs: written by every evaluation and read back by the commit
+  // and the queue placement, so they start in LDS (a lane's list that outgrows its slice moves to the
+  // pool like any other array)
   __shared__ int32_t* s_priv;
   const int q0 = 2;
+#if WAVE_PRIV > 0
+  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
+  constexpr int priv_stride = WAVE_PRIV, log0 = (WAVE_PRIV - 4 * q0) / WL;
+  static_assert(WAVE_PRIV % 4 == 0 && log0 >= 1, "WAVE_PRIV: room for the run list and one log entry");
+  if (lane == 0) s_priv = s_priv_lds;
+#else
+  constexpr int priv_stride = 4 * (q0 + q0 * WL / 4 + 4), log0 = q0;
   if (lane == 0) {
-    s_priv = pool_alloc(l, int64_t(WAVE) * 4 * (q0 + q0 * WL / 4 + 4));
+    s_priv = pool_alloc(l, int64_t(WAVE) * priv_stride);
     if (!s_priv) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
   }
+#endif
   __syncthreads();
   const auto& P = KCEP_PROG(l);
   const int ns = P.nslots;
@@ -403,11 +416,11 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   int64_t evals = 0;
   const uint64_t t0 = A.profile ? wall_clock64() : 0;
   if (!w.overflow) {
-    int32_t* pv = s_priv + int64_t(lane) * 4 * (q0 + q0 * WL / 4 + 4);
+    int32_t* pv = s_priv + int64_t(lane) * priv_stride;
     l.tq = pv;
     l.tq_cap = q0;
     l.log = pv + 4 * q0;
-    l.log_cap = q0;
+    l.log_cap = log0;
   }
   l.wtop = &w.heap_top;
   for (int i = 0; i < l.L && !w.err && !w.overflow; i++) {

@@ -22,6 +22,8 @@
 
 #include <string.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "../../include/kcep.h"
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(256) void runs_compact(const int64_t* __restrict__ 
 // 256 consecutive matches and writes their entries as one contiguous range, thread-strided (coalesced
 // stores); an entry finds its match by a binary search over the workgroup's entry offsets in LDS.
 __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
-                                                   const uint32_t* __restrict__ segs,
+                                                   const int64_t* __restrict__ pos, const uint32_t* __restrict__ segs,
                                                    const unsigned long long* __restrict__ sorted, int64_t nm,
                                                    const int64_t* __restrict__ ent_off, int64_t ne, int64_t base,
                                                    int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
     s_at[tid] = at;
     s_j[tid] = j;
     s_e[tid] = e;
-    match_record[m] = base + e;
+    match_record[m] = pos ? pos[e] : base + e;
     match_key[m] = key[j];
     ent_off_out[m] = at;
 #pragma unroll
@@ -106,13 +108,149 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
       if (w == ~0u) break;
     }
     ent_name[x] = P->st[stage].name;
-    ent_record[x] = base + j + o;
+    ent_record[x] = pos ? pos[j + o] : base + j + o;
   }
 }
 
 __global__ void runs_lengths(const unsigned long long* __restrict__ sorted, int64_t nm, int64_t* __restrict__ len) {
   const int64_t m = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (m < nm) len[m] = int64_t(sorted[m] >> 31) - int64_t(sorted[m] & 0x7FFFFFFFull) + 1;
+}
+
+// ---- carried tails (CEP_SESSION_CARRY on the runs path) ----
+// A run here is a function of its start record and the key's following records, so a key's open
+// runs are carried as the key's records from its oldest open run's start on (its "tail", stream
+// positions and every field a predicate or fold can read): the next batch of the key is prefixed
+// with them and every run is simulated again from its start, which reproduces its stage and fold
+// registers exactly.  Runs that end or fail inside the tail were emitted / raised by the earlier
+// batch (RunsArgs.emit_from).  Tail records are int64 words: pos, offset, ts, key | topic << 32,
+// partition, then the columns' bits.
+__device__ __forceinline__ int64_t col_bits(const void* c, int type, int64_t i) {
+  return type == T_I32 ? int64_t(static_cast<const int32_t*>(c)[i]) : static_cast<const int64_t*>(c)[i];
+}
+__device__ __forceinline__ void col_put(void* c, int type, int64_t i, int64_t v) {
+  if (type == T_I32) static_cast<int32_t*>(c)[i] = int32_t(v);
+  else static_cast<int64_t*>(c)[i] = v;
+}
+
+// per batch segment: its key's carried tail length (0 beyond the segment count)
+__global__ void rc_tail_len(const int64_t* __restrict__ nseg, const int64_t* __restrict__ seg_start,
+                            const int32_t* __restrict__ key, const int64_t* __restrict__ rtab, int64_t nmax,
+                            int64_t* __restrict__ tlen) {
+  const int64_t sg = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (sg >= nmax) return;
+  tlen[sg] = sg < *nseg ? rtab[2 * int64_t(key[seg_start[sg]]) + 1] : 0;
+}
+
+// the batch's records into the extended batch, after their key's tail
+__global__ void rc_build_new(RcExt X, int64_t n, const int64_t* __restrict__ seg_flag, const int64_t* __restrict__ seg_idx,
+                             const int64_t* __restrict__ toff, const int64_t* __restrict__ tlen, int64_t base,
+                             RcIn B) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t sg = seg_idx[i] + seg_flag[i] - 1;
+  const int64_t e = i + toff[sg] + tlen[sg];
+  X.key[e] = B.key[i];
+  X.topic[e] = B.topic ? B.topic[i] : 0;
+  X.partition[e] = B.partition ? B.partition[i] : 0;
+  X.pos[e] = base + i;
+  X.offset[e] = B.offset ? B.offset[i] : base + i;
+  X.ts[e] = B.ts ? B.ts[i] : base + i;
+  X.seg[e] = int32_t(sg);
+  for (int c = 0; c < X.ncols; c++) col_put(X.cols[c], X.coltype[c], e, col_bits(B.cols[c], X.coltype[c], i));
+}
+
+// the carried tails into the extended batch (one thread per segment: tails are short)
+__global__ void rc_build_tail(RcExt X, int64_t nmax, const int64_t* __restrict__ nseg, const int64_t* __restrict__ seg_start,
+                              const int32_t* __restrict__ key, const int64_t* __restrict__ rtab,
+                              const int64_t* __restrict__ rpool, const int64_t* __restrict__ toff,
+                              const int64_t* __restrict__ tlen) {
+  const int64_t sg = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (sg >= nmax || sg >= *nseg) return;
+  const int64_t T = tlen[sg];
+  if (!T) return;
+  const int RW = 5 + X.ncols;
+  const int64_t* src = rpool + rtab[2 * int64_t(key[seg_start[sg]])] * RW;
+  const int64_t e0 = seg_start[sg] + toff[sg];
+  for (int64_t t = 0; t < T; t++, src += RW) {
+    const int64_t e = e0 + t;
+    X.pos[e] = src[0];
+    X.offset[e] = src[1];
+    X.ts[e] = src[2];
+    X.key[e] = int32_t(uint64_t(src[3]));
+    X.topic[e] = int32_t(uint64_t(src[3]) >> 32);
+    X.partition[e] = int32_t(src[4]);
+    X.seg[e] = int32_t(sg);
+    for (int c = 0; c < X.ncols; c++) col_put(X.cols[c], X.coltype[c], e, src[5 + c]);
+  }
+}
+
+// per segment: the first start whose run is still open (runs_sim's end_of == -2)
+__global__ void rc_open_min(const int32_t* __restrict__ end_of, const int32_t* __restrict__ seg, int64_t n,
+                            unsigned long long* __restrict__ tstart) {
+  const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (j < n && end_of[j] == -2) atomicMin(&tstart[seg[j]], (unsigned long long)j);
+}
+
+__global__ void rc_new_len(int64_t nmax, const int64_t* __restrict__ nseg, const int64_t* __restrict__ seg_start,
+                           const int64_t* __restrict__ toff, const unsigned long long* __restrict__ tstart,
+                           int64_t* __restrict__ newlen) {
+  const int64_t sg = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (sg >= nmax) return;
+  int64_t L = 0;
+  if (sg < *nseg) {
+    const int64_t end = seg_start[sg + 1] + toff[sg + 1];          // the segment's end in the extended batch
+    const unsigned long long t = tstart[sg];
+    if (int64_t(t) >= 0 && int64_t(t) < end) L = end - int64_t(t);
+  }
+  newlen[sg] = L;
+}
+
+// the new tails appended to the pool (at *top + noff), the key table updated
+__global__ void rc_tail_write(RcExt X, int64_t nmax, const int64_t* __restrict__ nseg,
+                              const int64_t* __restrict__ seg_start, const int32_t* __restrict__ key,
+                              const int64_t* __restrict__ toff, const unsigned long long* __restrict__ tstart,
+                              const int64_t* __restrict__ newlen, const int64_t* __restrict__ noff,
+                              const int64_t* __restrict__ top, int64_t* __restrict__ rpool, int64_t* __restrict__ rtab) {
+  const int64_t sg = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (sg >= nmax || sg >= *nseg) return;
+  const int64_t k = key[seg_start[sg]];
+  const int64_t L = newlen[sg];
+  if (!L) { rtab[2 * k + 1] = 0; return; }
+  const int RW = 5 + X.ncols;
+  const int64_t at = *top + noff[sg];
+  int64_t* d = rpool + at * RW;
+  const int64_t j0 = int64_t(tstart[sg]);
+  for (int64_t t = 0; t < L; t++, d += RW) {
+    const int64_t e = j0 + t;
+    d[0] = X.pos[e];
+    d[1] = X.offset[e];
+    d[2] = X.ts[e];
+    d[3] = int64_t(uint64_t(uint32_t(X.key[e])) | (uint64_t(uint32_t(X.topic[e])) << 32));
+    d[4] = X.partition[e];
+    for (int c = 0; c < X.ncols; c++) d[5 + c] = col_bits(X.cols[c], X.coltype[c], e);
+  }
+  rtab[2 * k] = at;
+  rtab[2 * k + 1] = L;
+}
+
+__global__ void rc_top_add(int64_t* __restrict__ top, const int64_t* __restrict__ add) { *top += *add; }
+
+// compaction of the tail pool: every key's tail copied to `dst` at the exclusive prefix of the lengths
+__global__ void rc_gc_len(const int64_t* __restrict__ rtab, int64_t nkeys, int64_t* __restrict__ len) {
+  const int64_t k = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (k < nkeys) len[k] = rtab[2 * k + 1];
+}
+__global__ void rc_gc_copy(int64_t* __restrict__ rtab, int64_t nkeys, const int64_t* __restrict__ off, int RW,
+                           const int64_t* __restrict__ src, int64_t* __restrict__ dst) {
+  const int64_t k = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (k >= nkeys) return;
+  const int64_t L = rtab[2 * k + 1];
+  if (!L) return;
+  const int64_t* a = src + rtab[2 * k] * RW;
+  int64_t* b = dst + off[k] * RW;
+  for (int64_t w = 0; w < L * RW; w++) b[w] = a[w];
+  rtab[2 * k] = off[k];
 }
 
 }  // namespace
@@ -159,8 +297,53 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
                               int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st) {
   if (nm <= 0) return hipSuccess;
-  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.segs, sorted, nm,
+  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, sorted, nm,
                      ent_off, ne, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
+  return hipGetLastError();
+}
+
+static unsigned blocks256(int64_t n) { return unsigned((std::max<int64_t>(n, 1) + 255) / 256); }
+
+// the extended batch of a runs carry session: every batch segment prefixed by its key's tail.
+// seg_flag / seg_idx / seg_start / nseg: nfa_segments of the batch; nmax >= segment count (the batch
+// size); tlen / toff: n + 1 entries of scratch; total: the tails' record count (device)
+hipError_t runs_carry_build(const RcIn& B, int64_t n, int64_t base, const int64_t* seg_flag, const int64_t* seg_idx,
+                            const int64_t* seg_start, const int64_t* nseg, const int64_t* rtab, const int64_t* rpool,
+                            int64_t* tlen, int64_t* toff, int64_t* total, int64_t* scan_tmp, const RcExt& X,
+                            hipStream_t st, bool lens_only) {
+  if (lens_only) {
+    hipLaunchKernelGGL(rc_tail_len, dim3(blocks256(n + 1)), dim3(256), 0, st, nseg, seg_start, B.key, rtab, n + 1, tlen);
+    return exclusive_scan(tlen, n + 1, toff, total, scan_tmp, st);
+  }
+  hipLaunchKernelGGL(rc_build_new, dim3(blocks256(n)), dim3(256), 0, st, X, n, seg_flag, seg_idx, toff, tlen, base, B);
+  hipLaunchKernelGGL(rc_build_tail, dim3(blocks256(n)), dim3(256), 0, st, X, n, nseg, seg_start, B.key, rtab, rpool, toff,
+                     tlen);
+  return hipGetLastError();
+}
+
+// after runs_sim over the extended batch (ext_n records): the keys' new tails
+hipError_t runs_carry_tails(const RcExt& X, int64_t ext_n, int64_t n, const int64_t* nseg, const int64_t* seg_start,
+                            const int32_t* key, const int64_t* toff, const int32_t* end_of, unsigned long long* tstart,
+                            int64_t* newlen, int64_t* noff, int64_t* new_total, int64_t* scan_tmp, int64_t* top,
+                            int64_t* rpool, int64_t* rtab, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(tstart, 0x7F, size_t(n + 1) * 8, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(rc_open_min, dim3(blocks256(ext_n)), dim3(256), 0, st, end_of, X.seg, ext_n, tstart);
+  hipLaunchKernelGGL(rc_new_len, dim3(blocks256(n + 1)), dim3(256), 0, st, n + 1, nseg, seg_start, toff, tstart, newlen);
+  if ((e = exclusive_scan(newlen, n + 1, noff, new_total, scan_tmp, st)) != hipSuccess) return e;
+  hipLaunchKernelGGL(rc_tail_write, dim3(blocks256(n)), dim3(256), 0, st, X, n, nseg, seg_start, key, toff, tstart, newlen,
+                     noff, top, rpool, rtab);
+  hipLaunchKernelGGL(rc_top_add, dim3(1), dim3(1), 0, st, top, new_total);
+  return hipGetLastError();
+}
+
+// compaction of the tail pool into dst (len / off: nkeys + 1 entries of scratch; *total: live records)
+hipError_t runs_carry_gc(int64_t* rtab, int64_t nkeys, int RW, const int64_t* src, int64_t* dst, int64_t* len,
+                         int64_t* off, int64_t* total, int64_t* scan_tmp, hipStream_t st) {
+  hipLaunchKernelGGL(rc_gc_len, dim3(blocks256(nkeys)), dim3(256), 0, st, rtab, nkeys, len);
+  hipError_t e = exclusive_scan(len, nkeys, off, total, scan_tmp, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(rc_gc_copy, dim3(blocks256(nkeys)), dim3(256), 0, st, rtab, nkeys, off, RW, src, dst);
   return hipGetLastError();
 }
 

@@ -56,8 +56,8 @@ struct RunEnv {
     return static_cast<const int64_t*>(c)[g];
   }
   __device__ __forceinline__ int64_t key() { return A.key[g]; }
-  __device__ __forceinline__ int64_t ts() { return A.ts ? A.ts[g] : A.base + g; }
-  __device__ __forceinline__ int64_t off() { return A.offset ? A.offset[g] : A.base + g; }
+  __device__ __forceinline__ int64_t ts() { return A.ts ? A.ts[g] : A.pos ? A.pos[g] : A.base + g; }
+  __device__ __forceinline__ int64_t off() { return A.offset ? A.offset[g] : A.pos ? A.pos[g] : A.base + g; }
   __device__ __forceinline__ int64_t part() { return A.partition ? A.partition[g] : 0; }
   __device__ __forceinline__ int32_t topic() { return A.topic ? A.topic[g] : 0; }
   __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) {
@@ -92,6 +92,7 @@ struct RunResult {
   int64_t end;        // record where the run consumed its last stage, -1 none
   int64_t fail_at;    // record whose evaluation raised, -1 none
   int err;
+  bool open;          // the run consumed its key's last record of the batch and waits for the next
 };
 
 // item(i, &j, &stop): start record and last record to walk of item i (false: skip)
@@ -103,7 +104,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
   RunState rs;
 #pragma unroll
   for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
-  RunResult res{-1, -1, 0};
+  RunResult res{-1, -1, 0, false};
   bool alive = false;
   int64_t idx = -1, r = 0, stop = 0;
   int ps = -1, cur = -1;
@@ -136,7 +137,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
           ps = P.begin;                                      // the begin run's evaluation on record j
           cur = -1;
           load_record(j, &k);
-          res = RunResult{-1, -1, 0};
+          res = RunResult{-1, -1, 0, false};
 #pragma unroll
           for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
         }
@@ -218,6 +219,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
         int32_t kr = k + 1;
         if (r < A.n && r <= stop) load_record(r, &kr);
         ps = kr == k ? cur : -2;
+        if (ps == -2 && r <= stop) res.open = true;                // out of the key's records, not dead
       } else if (ps != -2) {
         ps = -2;                                                   // (a recursion that consumed nothing)
       }
@@ -250,12 +252,15 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
     run_engine(
         T, A, i0, i1, [&](int64_t i, int64_t* j, int64_t* stop) { *j = i; *stop = INT64_MAX; return true; },
         [&](int64_t i, const RunResult& res) {
-          s_end[wv][i - i0] = int32_t(res.end);
-          if (res.fail_at >= 0) {
+          // carry: a run that ended in the carried records was emitted by an earlier batch; -2 marks a
+          // run still open at its key's last record (its start begins the key's next carried tail)
+          const bool old_end = A.pos && res.end >= 0 && A.pos[res.end] < A.emit_from;
+          s_end[wv][i - i0] = old_end ? -1 : res.open ? -2 : int32_t(res.end);
+          if (res.fail_at >= 0 && !(A.pos && A.pos[res.fail_at] < A.emit_from)) {
             A.err_code[i] = res.err;
             atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
           }
-          if (A.segs && res.end >= 0) {
+          if (A.segs && res.end >= 0 && !old_end) {
             if (seg_item != i) seg_n = 0;
             for (int q = seg_n; q < RUNS_MAX_SEGS; q++) myseg[q] = ~0u;   // terminator (and padding)
             uint4* d = reinterpret_cast<uint4*>(A.segs + i * RUNS_MAX_SEGS);
@@ -278,7 +283,7 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
   for (int64_t k = lane; k < i1 - i0; k += 64) {
     const int32_t e = s_end[wv][k];
     flag[i0 + k] = e >= 0 ? 1 : 0;
-    end_of[i0 + k] = e;
+    end_of[i0 + k] = e;                                         // (-2: open, carried)
   }
 }
 
@@ -297,7 +302,7 @@ struct WriteArgs {
 template <class Tab>
 __device__ __forceinline__ void put_entry(const Tab& T, const WriteArgs& W, int64_t at, int stage, int64_t r) {
   W.ent_name[at] = T.prog().st[stage].name;
-  W.ent_record[at] = W.R.base + r;
+  W.ent_record[at] = W.R.pos ? W.R.pos[r] : W.R.base + r;
 }
 
 // re-walk each completed run: traversal order is final stage first (peek :176-201)
@@ -312,7 +317,7 @@ __device__ __forceinline__ void runs_write_body(const Tab& T, const WriteArgs& W
         const unsigned long long kv = W.sorted[m];
         *j = int64_t(kv & 0x7FFFFFFFull);
         *stop = int64_t(kv >> 31);
-        W.match_record[m] = W.R.base + *stop;
+        W.match_record[m] = W.R.pos ? W.R.pos[*stop] : W.R.base + *stop;
         W.match_key[m] = W.R.key[*j];
         W.ent_off_out[m] = W.ent_off[m];
         return true;

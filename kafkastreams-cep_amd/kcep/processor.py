@@ -261,11 +261,12 @@ class GpuCEPProcessor:
             return 0
         recs, self._pending = self._pending, []
         self._flags = 0
-        if self.session.path in (N.PATH_STENCIL, N.PATH_CHAIN):
-            # the stencil path carries only each key's last records: the high-water-mark rule
+        if self.session.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS):
+            # the stencil / chain / runs paths carry each key's records (its last K-1, or those
+            # from its oldest open run on), not its NFA: the high-water-mark rule
             # (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the
-            # batch handed over has increasing offsets per key and topic.  A strict fixed-length
-            # pattern never throws, so every admitted record is processed and moves the mark.
+            # batch handed over has increasing offsets per key and topic.  Every admitted record is
+            # processed and moves the mark (a record that throws fails the task anyway).
             kept = []
             for r in recs:
                 hk = (r[0], r[2])
@@ -322,7 +323,7 @@ class GpuCEPProcessor:
         key, the events its runs and buffer nodes still reference (``cep_state_export``), each with
         its stream position; spilled keys keep theirs.  Runs only when the log has doubled since the
         last prune."""
-        keep = carried_positions(self.session.state_export())
+        keep = set(int(x) for x in N.state_positions(self.session.state_export()))
         for _, pos in self._spilled.values():
             keep.update(int(x) for x in pos)
         self._log = {p: ev for p, ev in self._log.items() if p in keep}

@@ -27,7 +27,7 @@ NATIVES = ["cepCompile", "cepStageNames", "cepSessionOpen", "cepSessionPath", "c
            "cepLastError"]
 
 CEP_MODE_PROCESSOR, CEP_SESSION_CARRY, CEP_E_RUN_CAPACITY = 1, 1, 9
-CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_BATCH_OFFSETS_MONOTONE = 1, 3, 1
+CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS, CEP_BATCH_OFFSETS_MONOTONE = 1, 3, 4, 1
 
 
 class JniLib:
@@ -293,7 +293,7 @@ class JavaTwin:
             return
         recs, self.pending = self.pending, []
         flags = 0
-        if self.path in (CEP_PATH_STENCIL, CEP_PATH_CHAIN):
+        if self.path in (CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS):
             kept = []
             for r in recs:
                 hw = self.high_water.setdefault(r[0], {})

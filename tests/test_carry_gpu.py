@@ -102,8 +102,10 @@ def test_stream_in_batches(name, mk, vmax, gen, mode, nbatch, lane_nfa):
     assert oerr is None and gerr is None
     assert len(want) > 0
     assert got == want
-    if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):     # carries each key's last records, not its runs
-        assert name == ("c2_strict" if sess.path == N.PATH_STENCIL else "c5_optional")
+    if name == "c3_stock":                              # a runs-path pattern stays on the runs kernels
+        assert sess.path == N.PATH_RUNS
+    if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS):   # carries each key's records, not its queue
+        assert name == {N.PATH_STENCIL: "c2_strict", N.PATH_CHAIN: "c5_optional", N.PATH_RUNS: "c3_stock"}[sess.path]
         return
     for k in np.unique(key):                            # NFA.getRuns() and queue length per key
         assert sess.key_state(int(k)) == r.state(int(k)), int(k)
@@ -316,3 +318,75 @@ def test_chain_carry_c5_random_cuts_and_export():
     s3.state_import(blob)
     part2, _, _ = run_carry(ir, key, [val], bounds[half:], sess=s3)
     assert part1 + part2 == whole
+
+
+# ---- the runs path's carried tails (runs.hip): each key's records from its oldest open run on ----
+
+def c3_stream(seed, n_keys, per_key):
+    rng = np.random.default_rng(seed)
+    key = np.repeat(np.arange(n_keys, dtype=np.int32), rng.poisson(per_key, n_keys) + 1)
+    rng.shuffle(key)
+    val = (100 + np.cumsum(rng.integers(-5, 6, len(key)))).astype(np.int32)
+    return key, val
+
+
+@pytest.mark.parametrize("cuts", [1, 2, 5, 64])
+def test_runs_carry_cut_anywhere(cuts):
+    """C3's pattern (stock oneOrMore + sum/count folds) on the runs path of a carry session, the
+    stream cut into batches of `cuts` records (1: record at a time): open runs -- with their fold
+    registers -- continue across every cut, as the reference's NFAStore/AggregatesStore keep them
+    (CEPProcessor.java:111-124, 144-147; AggregatesStoreImpl.java:55-75)."""
+    key, val = c3_stream(cuts, 60 if cuts < 5 else 200, 12 if cuts < 5 else 30)
+    bounds, order = batches_of(key, list(range(cuts, len(key), cuts)))
+    key, val = key[order], val[order]
+    ir = PL.c3_stock().to_ir(PL.I32)
+    want, _, oerr = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    got, sess, gerr = run_carry(ir, key, [val], bounds)
+    assert sess.path == N.PATH_RUNS
+    assert oerr is None and gerr is None
+    assert len(want) > 0 and got == want
+
+
+def test_runs_carry_long_open_run_and_export_import():
+    """A oneOrMore run that stays open over many batches (rising prices keep avg < v), then a
+    mid-stream checkpoint (cep_state_export "KCSR") restored into a fresh session: the rest of the
+    stream matches as one uninterrupted run, and cep_state_positions lists the carried records."""
+    from kcep import native as NN
+    n_keys = 8
+    rng = np.random.default_rng(3)
+    key = np.tile(np.arange(n_keys, dtype=np.int32), 150)
+    val = (100 + np.arange(len(key)) // n_keys + rng.integers(0, 2, len(key))).astype(np.int32)  # slow rise
+    val[len(val) * 3 // 4:] -= 40                                            # then a drop closes the runs
+    ir = PL.c3_stock().to_ir(PL.I32)
+    want, _, _ = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    bounds = list(range(0, len(key), 16)) + [len(key)]
+    order = np.concatenate([a + np.argsort(key[a:b], kind="stable") for a, b in zip(bounds[:-1], bounds[1:])])
+    key, val = key[order], val[order]
+    want, _, _ = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    half = len(bounds) // 2
+    got, s1, _ = run_carry(ir, key, [val], bounds[:half + 1], max_keys=n_keys)
+    blob = s1.state_export()
+    assert blob[:4] == b"KCSR"
+    pos = NN.state_positions(blob)
+    assert len(pos) > 0 and pos.max() < bounds[half]
+    s2 = N.Session(N.CompiledPattern(ir), 16, carry=True, max_keys=n_keys)
+    s2.state_import(blob)
+    assert s2.stream_position() == bounds[half]
+    rest = [b - bounds[half] for b in bounds[half:]]
+    got2, _, _ = run_carry(ir, key[bounds[half]:], [val[bounds[half]:]], rest, sess=s2)
+    assert len(want) > 0 and got + got2 == want
+
+
+def test_runs_carry_rejects_unclean_batches():
+    """Like the stencil carry: null records or unflagged offsets cannot be taken by the runs kernels
+    (the host applies CEPProcessor's filters first)."""
+    ir = PL.c3_stock().to_ir(PL.I32)
+    s = N.Session(N.CompiledPattern(ir), 8, carry=True, max_keys=4)
+    assert s.path == N.PATH_RUNS
+    key = np.array([0, 0, 1, 1], np.int32)
+    val = np.array([100, 101, 102, 103], np.int32)
+    with pytest.raises(N.CepError) as ei:
+        s.push(4, key, [val], offset=np.arange(4, dtype=np.int64))
+    assert ei.value.code == 12
+    s.push(4, key, [val], offset=np.arange(4, dtype=np.int64), flags=N.BATCH_OFFSETS_MONOTONE)
+    s.collect()

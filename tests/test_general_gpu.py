@@ -225,13 +225,15 @@ def test_key_over_capacity_at_first_allocation(lane_nfa):
     """A key whose very first workspace allocation is already over cep_opts.max_key_words (5000
     records against 1<<17 words) must still be listed by cep_batch_errors with CEP_E_RUN_CAPACITY
     at its first record -- key_begin raises the batch's error flag, so the host reads the per-key
-    errors -- while every other key matches the oracle."""
+    errors -- while every other key matches the oracle.  (The strict A->B->C pattern on the general
+    path: a long key is cheap for the oracle.)"""
+    from kcep import synth
     rng = np.random.default_rng(5)
     lens = [12] * 40
     lens[7] = 5000
     key = np.repeat(np.arange(40, dtype=np.int32), lens)
     val = rng.integers(0, 4, len(key)).astype(np.int32)
-    ir = PL.any_any().to_ir(PL.I32)
+    ir = synth.c2_pattern().to_ir(PL.I32)
     want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
     s = N.Session(N.CompiledPattern(ir), len(key), force_path=N.PATH_GENERAL, max_key_words=1 << 17,
                   lane_nfa=lane_nfa)
