@@ -63,6 +63,10 @@ def parse(argv=None):
                     help="stencil/chain: record counts per host batch for the processor-batch legs (comma list)")
     ap.add_argument("--carry-batches", type=int, default=10,
                     help="stencil/chain: also stream the batch through a carry session in this many batches")
+    ap.add_argument("--force-path", choices=["stencil", "chain", "runs", "general"], default=None,
+                    help="run the workload on this path (e.g. C3 on the general NFA), not the fastest exact one")
+    ap.add_argument("--lane-nfa", action="store_true",
+                    help="general path: one lane per key (CEP_SESSION_LANE_NFA) instead of the wave kernel")
     ap.add_argument("--gather-matches", action="store_true",
                     help="N > 1: after the timed steps, gather every rank's matches to rank 0 (12 B/match) and "
                          "time it")
@@ -153,8 +157,10 @@ def main():
         exchange = S.CountExchange(dev)
 
     pat = N.CompiledPattern(ir)
-    sess = N.Session(pat, n, mode=N.MODE_PROCESSOR, device=local)
-    if args.config == "c2":
+    force = {"stencil": N.PATH_STENCIL, "chain": N.PATH_CHAIN, "runs": N.PATH_RUNS,
+             "general": N.PATH_GENERAL}.get(args.force_path, 0)
+    sess = N.Session(pat, n, mode=N.MODE_PROCESSOR, device=local, force_path=force, lane_nfa=args.lane_nfa)
+    if args.config == "c2" and not force:
         assert sess.path == N.PATH_STENCIL
 
     def step():
@@ -245,7 +251,8 @@ def main():
                        "matches_per_gpu": int(n_matches), "matches_total": int(tot_matches),
                        "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain", N.PATH_RUNS: "runs"}.get(sess.path, "general"),
                        "parallelism": f"key-hash sharded x{world}" if world > 1 else "1 GPU",
-                       "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in"},
+                       "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in",
+                       "forced_path": args.force_path, "lane_nfa": bool(args.lane_nfa)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
                          "kernel": roof_kernel, "kernel_ms": roof_ms, "algo_bytes_per_launch": algo_bytes},

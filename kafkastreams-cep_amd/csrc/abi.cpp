@@ -120,15 +120,23 @@ uint64_t mix64(uint64_t x) {
 
 // The wave kernel (nfa_wave.h) evaluates a record's runs in parallel: it needs a pattern whose
 // evaluations read nothing but the record -- every edge predicate event-only, no folds, no states.
-bool wave_ok(const DevProgram& D) {
-  if (D.nstates || D.ndefined) return false;
+// the wave kernel takes every pattern: rounds whose runs share a sequence that one of them folds into
+// (or that read a partial sequence after a run of the round died) are evaluated again sequentially
+// (nfa_wave.h).  KCEP_NFA_WAVE_AGG=0 keeps patterns with aggregates / SequenceMatchers on the lane kernel.
+bool wave_stateful(const DevProgram& D) {
+  if (D.nstates || D.ndefined) return true;
   for (int s = 0; s < D.nstages; s++) {
     const DevStage& t = D.st[s];
-    if (t.nfolds) return false;
+    if (t.nfolds) return true;
     for (int e = 0; e < t.nedges; e++)
-      if (t.pred[e] >= 0 && t.sl[e] < 0) return false;
+      if (t.pred[e] >= 0 && t.sl[e] < 0) return true;
   }
-  return true;
+  return false;
+}
+bool wave_ok(const DevProgram& D) {
+  const char* v = getenv("KCEP_NFA_WAVE_AGG");
+  const bool agg_on = !(v && v[0] == '0');
+  return agg_on || !wave_stateful(D);
 }
 
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
@@ -647,6 +655,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.err_any = ctl + 4;
   // key segments per wave (KCEP_NFA_SPREAD: experiments; fewer keys per wave diverge less but leave
   // the chip emptier -- tools/c4_profile.py)
+  A.wave_agg = (wave_stateful(D) ? 1 : 0) | (P.has_seq ? 2 : 0);
   const char* spread_env = getenv("KCEP_NFA_SPREAD");
   A.spread = spread_env ? std::min(64, std::max(1, atoi(spread_env))) : 64;
   if (s->opts.flags & CEP_SESSION_PROFILE) {

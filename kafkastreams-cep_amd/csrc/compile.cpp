@@ -842,6 +842,11 @@ int compile_ir(const uint8_t* ir, size_t len, Program& P, std::string& err) {
   analyse_stencil(P);
   P.general_ok = lower_general(P, P.general_why) == CEP_OK;
   analyse_runs(P);
+  P.has_seq = false;
+  for (const auto& pd : P.pats) {
+    P.has_seq = P.has_seq || uses_seq(pd.pred);
+    for (const auto& f : pd.folds) P.has_seq = P.has_seq || uses_seq(f.expr);
+  }
   return CEP_OK;
 }
 

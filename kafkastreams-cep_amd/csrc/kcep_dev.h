@@ -149,6 +149,8 @@ struct NfaArgs {
                                   // [3] live-run high-water mark over the batch's keys
   int64_t* profile;               // CEP_SESSION_PROFILE: NFA_PROFILE_W words per segment (nfa_dev.h)
   int32_t spread;                 // key segments per wave (1..64)
+  int32_t wave_agg;               // wave kernel: bit 0 the pattern folds / reads / copies aggregates (rounds
+                                  // check for runs sharing a sequence), bit 1 it has SequenceMatchers
   int32_t last_attempt;           // 1: no pool regrowth follows -- an overflowing key reports CEP_E_RUN_CAPACITY
   const int32_t* wave_seg;        // wave kernel: the segment of each workgroup (nullptr: workgroup = segment)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY

@@ -115,6 +115,7 @@ struct Program {
   bool stencil_ok = false;
   std::string stencil_why;           // reason the stencil path does not apply
   bool runs_ok = false;              // deterministic strict runs (compile.cpp analyse_runs)
+  bool has_seq = false;              // some predicate or fold is a SequenceMatcher (OP_SEQ_*)
   std::string runs_why;
   StencilProgram stencil{};
 };

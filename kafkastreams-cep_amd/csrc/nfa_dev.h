@@ -81,6 +81,7 @@ struct Lane {
   int32_t arena_used;             // wave kernel: LDS arena words key_begin took (-1: workspace in the pool)
   int32_t nph;                 // wave: run-counter increments of this lane's run (seq placeholders)
   int32_t wgrow;               // wave: the shared heap was too small (grow it and re-run the round)
+  int32_t ov_own;              // wave: this evaluation wrote an aggregate of its run's own sequence
   unsigned long long* wpool;   // wave: the key's pool words, in LDS (every lane allocates for the key)
 #ifdef KCEP_PHASES
   uint64_t ph[11];             // profiling kernels only: clocks in evaluate / predicates / buffer puts+branch /
@@ -232,7 +233,7 @@ __device__ __forceinline__ bool add_pred(Lane& l, int32_t* nd, int ver, int pslo
 // wave mode: a buffer operation is logged (WL words: kind | cur sid << 8 | prev sid << 16, event, prev
 // event, version) and applied in queue order after the round (nfa_wave.h)
 constexpr int WL = 4;
-enum : int32_t { WOP_PUT5 = 1, WOP_PUT3 = 2, WOP_BRANCH = 3 };
+enum : int32_t { WOP_PUT5 = 1, WOP_PUT3 = 2, WOP_BRANCH = 3, WOP_AGG = 4 };
 __device__ __forceinline__ void wlog(Lane& l, int kind, int sid, int psid, int ev, int pev, int ver) {
   if (l.log_n >= l.log_cap) {
     int32_t capw = l.log_cap * WL;
@@ -337,6 +338,45 @@ __device__ __forceinline__ int32_t* agg(Lane& l, int state, int seq) {
   return l.aggs + (int64_t(seq) * ns + state) * 3;
 }
 
+// AggregatesStore.find / put (AggregatesStoreImpl.java:55-75) for the evaluating run.  Wave mode: the
+// round evaluates against the aggregates as they were before it; a lane's writes are logged (WOP_AGG:
+// state, boxed type, sequence -- a placeholder for a sequence created in the round -- and the value)
+// and read back by the same lane first, then applied in queue order after the round (nfa_wave.h).
+__device__ __forceinline__ bool agg_read(Lane& l, int state, int seq, int32_t& tag, int64_t& v) {
+  if (l.wave) {
+    for (int k = l.log_n - 1; k >= 0; k--) {
+      const int32_t* o = l.log + k * WL;
+      if ((o[0] & 0xFF) == WOP_AGG && ((o[0] >> 8) & 0xFF) == state && o[1] == seq) {
+        tag = (o[0] >> 16) & 0xFF;
+        v = int64_t(uint32_t(o[2])) | (int64_t(o[3]) << 32);
+        return true;
+      }
+    }
+    if (seq < 0 || seq >= l.seqcap) { tag = 0; v = 0; return true; }   // a row not grown yet: every state null
+    const int32_t* e = l.aggs + (int64_t(seq) * KCEP_PROG(l).nstates + state) * 3;
+    tag = e[0];
+    v = int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32);
+    return true;
+  }
+  const int32_t* e = agg(l, state, seq);
+  if (!e) return false;
+  tag = e[0];
+  v = int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32);
+  return true;
+}
+__device__ __forceinline__ bool agg_write(Lane& l, int state, int seq, int32_t tag, int64_t v) {
+  const int32_t lo = int32_t(uint32_t(uint64_t(v))), hi = int32_t(uint32_t(uint64_t(v) >> 32));
+  if (l.wave) {
+    const int n0 = l.log_n;
+    wlog(l, WOP_AGG, state, tag, seq, lo, hi);
+    return l.log_n > n0;
+  }
+  int32_t* e = agg(l, state, seq);
+  if (!e) return false;
+  e[0] = tag; e[1] = lo; e[2] = hi;
+  return true;
+}
+
 // ---- event fields: local event e (carried below C) ----
 __device__ __forceinline__ int64_t cw64(const int32_t* p) { return int64_t(uint32_t(p[0])) | (int64_t(p[1]) << 32); }
 __device__ __forceinline__ const int32_t* cev_of(const Lane& l, int e) { return l.cev + int64_t(e) * l.evw; }
@@ -377,14 +417,25 @@ struct Ctx {
   int64_t curr;
 };
 
+// scratch for a partial sequence's walk: above the heap top (wave mode: drawn from the shared heap,
+// since the other lanes allocate concurrently)
+__device__ __forceinline__ int32_t* seq_scratch(Lane& l) {
+  const int need = 2 * l.nev + 2;
+  if (l.wave) {
+    const int at = heap_alloc(l, need);
+    return at < 0 ? nullptr : l.heap + at;
+  }
+  if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need))
+    return nullptr;
+  return l.heap + l.heap_top;
+}
+
 // SequenceMatcher: average of a column over buffer.get(Matched(prev, prevEvent), version)
 // (SequenceMatcher.java:21-26), with Sequence's per-stage TreeSet de-duplication.
 __device__ __forceinline__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t& out) {
   if (c.prev_sid < 0 || c.pev < 0) { l.err = CEP_E_NPE; return false; }
-  const int need = 2 * l.nev + 2;
-  if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need))
-    return false;
-  int32_t* tmp = l.heap + l.heap_top;                // scratch: the walk visits at most one node per event
+  int32_t* tmp = seq_scratch(l);                     // the walk visits at most one node per event
+  if (!tmp) return false;
   const int cnt = buf_peek(l, c.prev_sid, c.pev, c.ver, false, tmp, l.nev + 1);
   if (cnt < 0) return false;
   const int t = KCEP_PROG(l).coltype[col];
@@ -418,10 +469,8 @@ __device__ __forceinline__ int ev_cmp(const Lane& l, int a, int b) {
 }
 __device__ __forceinline__ bool seq_agg(Lane& l, const Ctx& c, int kind, int col, int stage, int64_t& out) {
   if (c.prev_sid < 0 || c.pev < 0) { l.err = CEP_E_NPE; return false; }
-  const int need = 2 * l.nev + 2;
-  if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need))
-    return false;
-  int32_t* tmp = l.heap + l.heap_top;
+  int32_t* tmp = seq_scratch(l);
+  if (!tmp) return false;
   const int cnt = buf_peek(l, c.prev_sid, c.pev, c.ver, false, tmp, l.nev + 1);
   if (cnt < 0) return false;
   const auto& P = KCEP_PROG(l);
@@ -477,13 +526,7 @@ struct LaneEnv {
   __device__ __forceinline__ int64_t off() { return b_off(l, l.g); }
   __device__ __forceinline__ int64_t part() { return b_part(l, l.g); }
   __device__ __forceinline__ int32_t topic() { return b_topic(l, l.g); }
-  __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) {
-    const int32_t* e = agg(l, idx, c.seq);
-    if (!e) return false;
-    tag = e[0];
-    v = int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32);
-    return true;
-  }
+  __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) { return agg_read(l, idx, c.seq, tag, v); }
   __device__ __forceinline__ bool seq_avg(int col, int64_t& v) { return kcep::seq_avg(l, c, col, v); }
   __device__ __forceinline__ bool seq_agg(int kind, int col, int stage, int64_t& v) {
     return kcep::seq_agg(l, c, kind, col, stage, v);
@@ -668,12 +711,10 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
         if (!push_t(l, mk_run(f.prev_sid, f.cur_sid, nv, last, nseq, true, false))) return false;
         for (int k = 0; k < KCEP_PROG(l).ndefined; k++) {                    // AggregatesStoreImpl.branch
           const int st = KCEP_PROG(l).defined[k];
-          const int32_t* src = agg(l, st, seq);
-          if (!src) return false;
-          const int32_t s0 = src[0], s1 = src[1], s2 = src[2];      // (agg() may move the table)
-          int32_t* dst = agg(l, st, nseq);
-          if (!dst) return false;
-          if (s0) { dst[0] = s0; dst[1] = s1; dst[2] = s2; }
+          int32_t t;
+          int64_t v;
+          if (!agg_read(l, st, seq, t, v)) return false;
+          if (t && !agg_write(l, st, nseq, t, v)) return false;           // (a new sequence's row is null)
         }
         if (!pb) {
           KPH_BEGIN(l, 2);
@@ -688,15 +729,14 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
     if (f.consumed && f.cur_eps == EPS_NONE) {                       // evaluateAggregates :319-321, :362-369
       const DevStage& s = stg(l, f.cur_sid);
       for (int k = 0; k < s.nfolds; k++) {
-        int32_t* e = agg(l, s.fold_state[k], seq);
-        if (!e) return false;
-        Ctx c{seq, -1, -1, ver, true, e[0], int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32)};
+        int32_t ct;
+        int64_t cv;
+        if (!agg_read(l, s.fold_state[k], seq, ct, cv)) return false;
+        Ctx c{seq, -1, -1, ver, true, ct, cv};
         int64_t v;
         if (!run_code(l, s.fold_code[k], c, v)) return false;
-        e = agg(l, s.fold_state[k], seq);
-        e[0] = s.fold_type[k];
-        e[1] = int32_t(uint32_t(uint64_t(v)));
-        e[2] = int32_t(uint32_t(uint64_t(v) >> 32));
+        if (!agg_write(l, s.fold_state[k], seq, s.fold_type[k], v)) return false;
+        l.ov_own = 1;
       }
     }
     const int csid = r_sid(f.cs), ceps = r_eps(f.cs);

@@ -40,8 +40,8 @@ constexpr int WAVE = 64;
 
 // the key's shared workspace descriptor (LDS); lanes keep register copies in their Lane
 struct WaveShared {
-  int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm;
-  int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs;
+  int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm, *aggs;
+  int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs, seqcap;
   int64_t nmatch;
   unsigned long long pool_words;   // the key's pool words (every lane allocates for the key)
   int32_t err, overflow, cap_hit;
@@ -50,18 +50,21 @@ struct WaveShared {
   int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
   int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
   int32_t *arena, arena_used;      // the key's LDS arena and its bump pointer (re-allocations go there first)
+  int32_t cseq[WAVE], cown[WAVE];  // stateful patterns: each lane's run sequence / whether it wrote it
   // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
   int32_t ms_slot[WAVE], ms_e[WAVE], ms_pv[WAVE], ms_cnt[WAVE], ms_done[WAVE], ms_err[WAVE];
 };
 
 __device__ __forceinline__ void ws_to_lane(Lane& l, const WaveShared& w) {
   l.nodes = w.nodes; l.heap = w.heap; l.qa = w.qa; l.qb = w.qb; l.fq = w.fq; l.out = w.out; l.hwm = w.hwm;
+  l.aggs = w.aggs; l.seqcap = w.seqcap;
   l.heapcap = w.heapcap; l.heap_top = w.heap_top; l.qa_cap = w.qa_cap; l.qb_cap = w.qb_cap; l.fq_cap = w.fq_cap;
   l.qlen = w.qlen; l.outcap = w.outcap; l.out_top = w.out_top; l.nhwm = w.nhwm; l.runs = w.runs;
   l.nmatch = w.nmatch; l.err = w.err; l.overflow = w.overflow; l.cap_hit = w.cap_hit;
 }
 __device__ __forceinline__ void lane_to_ws(WaveShared& w, const Lane& l) {
   w.nodes = l.nodes; w.heap = l.heap; w.qa = l.qa; w.qb = l.qb; w.fq = l.fq; w.out = l.out; w.hwm = l.hwm;
+  w.aggs = l.aggs; w.seqcap = l.seqcap;
   w.heapcap = l.heapcap; w.heap_top = l.heap_top; w.qa_cap = l.qa_cap; w.qb_cap = l.qb_cap; w.fq_cap = l.fq_cap;
   w.qlen = l.qlen; w.outcap = l.outcap; w.out_top = l.out_top; w.nhwm = l.nhwm; w.runs = l.runs;
   w.nmatch = l.nmatch; w.err = l.err; w.overflow = l.overflow; w.cap_hit = l.cap_hit;
@@ -153,7 +156,7 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
   __syncthreads();
   auto survives = [&](const int32_t* o, int gi) {
     const int kind = o[0] & 0xFF;
-    if (kind == WOP_BRANCH) return false;
+    if (kind == WOP_BRANCH || kind == WOP_AGG) return false;
     const int lp = w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)];
     return kind == WOP_PUT3 ? gi == lp : gi > lp;
   };
@@ -335,6 +338,60 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
   return true;
 }
 
+// Stateful patterns: the round's aggregate writes (WOP_AGG log entries; wave_agg bit 0) in queue
+// order.  Without a conflict (wave_round_conflict) no two lanes write one (sequence, state) -- a lane
+// writes its own run's sequence and sequences it created -- so every lane applies its own entries,
+// placeholders numbered as the run words are (rb).  The table first grows to the largest sequence.
+__device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared& w, int lane, int rb) {
+  const int ns = KCEP_PROG(l).nstates;
+  auto real = [&](int sq) { return sq < -1 ? rb + (-sq - 2) + 1 : sq; };
+  int need = -1;
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if ((o[0] & 0xFF) == WOP_AGG) { const int sq = real(o[1]); need = sq > need ? sq : need; }
+  }
+  for (int d = 32; d > 0; d >>= 1) { const int x = __shfl_xor(need, d); need = x > need ? x : need; }
+  if (need < 0) return true;
+  if (need >= w.seqcap) {
+    int32_t capw = w.seqcap * ns * 3;
+    const int64_t used = int64_t(capw);
+    int32_t* na = wave_regrow(l, w, w.aggs, capw, used, (int64_t(need) + 1) * ns * 3, lane);
+    if (!na) return false;
+    for (int64_t i = used + lane; i < capw; i += WAVE) na[i] = 0;       // the new rows: every state null
+    __syncthreads();
+    if (lane == 0) { w.aggs = na; w.seqcap = capw / (ns * 3); }
+    __syncthreads();
+  }
+  l.aggs = w.aggs;
+  l.seqcap = w.seqcap;
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if ((o[0] & 0xFF) != WOP_AGG) continue;
+    int32_t* e = l.aggs + (int64_t(real(o[1])) * ns + ((o[0] >> 8) & 0xFF)) * 3;
+    e[0] = (o[0] >> 16) & 0xFF; e[1] = o[2]; e[2] = o[3];
+  }
+  __syncthreads();
+  return true;
+}
+
+// A round whose parallel evaluation may differ from the reference's queue-order one: two runs of the
+// round share a run sequence (AggregatesStore rows are per sequence, AggregatesStoreImpl.java:55-75)
+// and one of them wrote it -- the later run would have read the earlier one's fold (NFA.java:319-321,
+// 362-369) -- or, with SequenceMatchers, a run died before others read partial sequences (its
+// removePattern, NFA.java:142-143, changes the buffer they walk).
+__device__ __forceinline__ bool wave_round_conflict(const Lane& l, WaveShared& w, int lane, bool act, int seq,
+                                                    uint64_t dmask) {
+  if ((l.A->wave_agg & 2) && dmask) return true;
+  if (!(l.A->wave_agg & 1)) return false;
+  w.cseq[lane] = act ? seq : INT32_MIN;
+  w.cown[lane] = act && l.ov_own;
+  __syncthreads();
+  bool c = false;
+  for (int j = 0; j < lane && act; j++) c = c || (w.cseq[j] == seq && (w.cown[j] || l.ov_own));
+  __syncthreads();
+  return __ballot(c) != 0;
+}
+
 // profiling kernels (KCEP_PHASES): lane 0's clocks per phase of the record loop -- record setup,
 // evaluation rounds, buffer commit, run numbering + queue placement, matchConstruction
 #ifdef KCEP_PHASES
@@ -379,8 +436,6 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   l.cev = reinterpret_cast<const int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.cev), 0));
   l.tq = reinterpret_cast<int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.tq), 0));
   l.tq_cap = __shfl(l.tq_cap, 0);
-  l.aggs = reinterpret_cast<int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.aggs), 0));
-  l.seqcap = __shfl(l.seqcap, 0);
   l.runs_delta = __shfl(l.runs_delta, 0);
   l.pool_words = 0;
   l.rec_out_top = 0; l.rec_nmatch = 0;
@@ -454,15 +509,40 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         run = Run{x.x, x.y, x.z, x.w};
       }
       const int top0 = w.heap_top;
-      bool good = true;
+      const int nact = n - base < WAVE ? n - base : WAVE;
+      bool good = true, seqd = false;
+      int jj = 0;                                              // sequential mode: the lane evaluating
+      uint64_t emask = 0, dmask = 0;
+      bool err_lane = false;
       KWP_MARK(t_ev);
-      for (;;) {                                               // evaluate; re-run if the heap was short
-        l.heap = w.heap; l.heapcap = w.heapcap;
-        l.tlen = 0; l.log_n = 0; l.nph = 0; l.err = 0; l.overflow = 0; l.wgrow = 0;
-        l.wave = 1;
+      for (;;) {
+        // one evaluation pass: every lane its run with logged side effects (parallel), or -- for a
+        // stateful round that conflicts (wave_round_conflict) -- lane jj alone with the lane kernel's
+        // immediate ones, on the key's shared state, lanes in queue order (one call site of evaluate)
+        const bool me = seqd ? lane == jj : act;
+        if (seqd) {
+          __syncthreads();
+          if (me) ws_to_lane(l, w);
+        } else {
+          l.heap = w.heap; l.heapcap = w.heapcap;
+        }
+        if (me || !seqd) { l.tlen = 0; l.log_n = 0; l.nph = 0; l.err = 0; l.overflow = 0; l.wgrow = 0; l.ov_own = 0; }
+        l.wave = seqd ? 0 : 1;
         good = true;
-        if (act) good = evaluate(l, run, fr);
+        if (me) good = evaluate(l, run, fr);
         l.wave = 0;
+        if (seqd) {
+          if (me) {
+            if (good && l.tlen == 0) buf_peek(l, r_sid(run), run.ev, run.ver, true, nullptr, 0);   // removePattern
+            const int e = l.err, o = l.overflow;
+            lane_to_ws(w, l);
+            if (e) w.err = e;
+            if (o) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
+          }
+          __syncthreads();
+          if (w.err || w.overflow || ++jj >= nact) break;
+          continue;
+        }
         const bool grow = __ballot(l.wgrow) != 0;
         const bool pool_out = __ballot(l.overflow && !l.wgrow) != 0;
         if (pool_out) {                                        // a private list could not grow
@@ -471,22 +551,35 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
           if (lane == 0 && ch) w.cap_hit = 1;
           break;
         }
-        if (!grow) break;
-        __syncthreads();
-        if (lane == 0) w.heap_top = top0;
-        __syncthreads();
-        if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, lane)) break;
+        if (grow) {
+          __syncthreads();
+          if (lane == 0) w.heap_top = top0;
+          __syncthreads();
+          if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, lane)) break;
+          continue;
+        }
+        err_lane = act && !good && l.err;
+        const bool dead = act && good && l.tlen == 0;
+        emask = __ballot(err_lane);
+        dmask = __ballot(dead);
+        // a conflict is checked before the errors: a run may throw on a state an earlier run of the
+        // round would have folded first
+        if (A.wave_agg && wave_round_conflict(l, w, lane, act, run.seq, dmask)) {
+          seqd = true;
+          l.tlen = 0; l.log_n = 0; l.nph = 0;                  // the parallel pass is discarded
+          continue;
+        }
+        break;
       }
       __syncthreads();
       KWP_ADD(1, t_ev);
       if (w.overflow) break;
       // commit in queue order
       KWP_MARK(t_cm);
-      const bool err_lane = act && !good && l.err;
-      const bool dead = act && good && l.tlen == 0;
-      const uint64_t emask = __ballot(err_lane), dmask = __ballot(dead);
-      const int nact = n - base < WAVE ? n - base : WAVE;
-      if (!emask && !dmask) {
+      if (seqd) {                                              // (committed as evaluated)
+        ws_to_lane(l, w);
+        if (w.err) { KWP_ADD(2, t_cm); break; }
+      } else if (!emask && !dmask) {
         const int e = wave_commit_parallel(l, w, lane, r, nact);
         if (lane == 0 && e) w.err = e;
         __syncthreads();
@@ -505,7 +598,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
               const int kind = o[0] & 0xFF, sid = (o[0] >> 8) & 0xFF, psid = (o[0] >> 16) & 0xFF;
               if (kind == WOP_PUT5) buf_put5(l, sid, o[1], psid, o[2], o[3]);
               else if (kind == WOP_PUT3) buf_put3(l, sid, o[1], o[3]);
-              else buf_branch(l, sid, o[1], o[3]);
+              else if (kind == WOP_BRANCH) buf_branch(l, sid, o[1], o[3]);
             }
             if (l.err || l.overflow) break;
             if ((emask >> j) & 1) { l.err = w.errc[j]; break; }
@@ -525,6 +618,10 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       KWP_MARK(t_pl);
       int nrun = 0;
       const int rb = w.runs + wave_excl_scan(l.nph, lane, nrun);
+      if ((A.wave_agg & 1) && !seqd && !wave_apply_aggs(l, w, lane, rb)) {   // the round's folds and copies
+        if (lane == 0) w.overflow = 1;
+        break;
+      }
       int nf = 0, nq = 0;
       for (int t = 0; t < l.tlen; t++) {
         int4* y = reinterpret_cast<int4*>(l.tq) + t;

@@ -170,14 +170,15 @@ __global__ void rc_build_tail(RcExt X, int64_t nmax, const int64_t* __restrict__
   const int64_t T = tlen[sg];
   if (!T) return;
   const int RW = 5 + X.ncols;
-  const int64_t* src = rpool + rtab[2 * int64_t(key[seg_start[sg]])] * RW;
+  const int32_t k = key[seg_start[sg]];
+  const int64_t* src = rpool + rtab[2 * int64_t(k)] * RW;
   const int64_t e0 = seg_start[sg] + toff[sg];
   for (int64_t t = 0; t < T; t++, src += RW) {
     const int64_t e = e0 + t;
     X.pos[e] = src[0];
     X.offset[e] = src[1];
     X.ts[e] = src[2];
-    X.key[e] = int32_t(uint64_t(src[3]));
+    X.key[e] = k;                                  // the key's current id (a spilled key may come back under another)
     X.topic[e] = int32_t(uint64_t(src[3]) >> 32);
     X.partition[e] = int32_t(src[4]);
     X.seg[e] = int32_t(sg);
