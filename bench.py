@@ -65,8 +65,9 @@ def parse(argv=None):
                     help="stencil/chain: also stream the batch through a carry session in this many batches")
     ap.add_argument("--force-path", choices=["stencil", "chain", "runs", "general"], default=None,
                     help="run the workload on this path (e.g. C3 on the general NFA), not the fastest exact one")
-    ap.add_argument("--lane-nfa", action="store_true",
-                    help="general path: one lane per key (CEP_SESSION_LANE_NFA) instead of the wave kernel")
+    ap.add_argument("--nfa-kernel", choices=["auto", "wave", "lane"], default="auto",
+                    help="general path: one key per wave (CEP_SESSION_WAVE_NFA) or per lane (CEP_SESSION_LANE_NFA); "
+                         "auto: the library's choice")
     ap.add_argument("--gather-matches", action="store_true",
                     help="N > 1: after the timed steps, gather every rank's matches to rank 0 (12 B/match) and "
                          "time it")
@@ -159,7 +160,8 @@ def main():
     pat = N.CompiledPattern(ir)
     force = {"stencil": N.PATH_STENCIL, "chain": N.PATH_CHAIN, "runs": N.PATH_RUNS,
              "general": N.PATH_GENERAL}.get(args.force_path, 0)
-    sess = N.Session(pat, n, mode=N.MODE_PROCESSOR, device=local, force_path=force, lane_nfa=args.lane_nfa)
+    sess = N.Session(pat, n, mode=N.MODE_PROCESSOR, device=local, force_path=force,
+                     lane_nfa={"auto": None, "wave": False, "lane": True}[args.nfa_kernel])
     if args.config == "c2" and not force:
         assert sess.path == N.PATH_STENCIL
 
@@ -252,7 +254,7 @@ def main():
                        "path": {N.PATH_STENCIL: "stencil", N.PATH_CHAIN: "chain", N.PATH_RUNS: "runs"}.get(sess.path, "general"),
                        "parallelism": f"key-hash sharded x{world}" if world > 1 else "1 GPU",
                        "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in",
-                       "forced_path": args.force_path, "lane_nfa": bool(args.lane_nfa)},
+                       "forced_path": args.force_path, "nfa_kernel": args.nfa_kernel},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
                          "kernel": roof_kernel, "kernel_ms": roof_ms, "algo_bytes_per_launch": algo_bytes},

@@ -114,9 +114,11 @@ typedef struct {
 #define CEP_SESSION_PROFILE 4    /* general path: record per key segment its live-run high-water mark, run
                                     evaluations and kernel cycles (cep_key_profile) */
 
-#define CEP_SESSION_LANE_NFA 8    /* general path: always one lane per key segment.  By default a pattern whose
-                                    evaluations read only the current record (no folds, no state reads, no
-                                    SequenceMatcher) runs one key per wave with one queued run per lane */
+#define CEP_SESSION_LANE_NFA 8    /* general path: always one lane per key segment (nfa_kernel) */
+#define CEP_SESSION_WAVE_NFA 16   /* general path: always one key per wave with one queued run per lane
+                                    (nfa_wave).  By default the wave kernel runs patterns whose keys' runs
+                                    can multiply (a skip-till-next / skip-till-any stage) and the lane kernel
+                                    the strict ones */
 
 #define CEP_MEM_HOST 0
 #define CEP_MEM_DEVICE 1

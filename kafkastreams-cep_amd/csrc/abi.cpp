@@ -123,16 +123,6 @@ uint64_t mix64(uint64_t x) {
 // the wave kernel takes every pattern: rounds whose runs share a sequence that one of them folds into
 // (or that read a partial sequence after a run of the round died) are evaluated again sequentially
 // (nfa_wave.h).  KCEP_NFA_WAVE_AGG=0 keeps patterns with aggregates / SequenceMatchers on the lane kernel.
-bool wave_stateful(const DevProgram& D) {
-  if (D.nstates || D.ndefined) return true;
-  for (int s = 0; s < D.nstages; s++) {
-    const DevStage& t = D.st[s];
-    if (t.nfolds) return true;
-    for (int e = 0; e < t.nedges; e++)
-      if (t.pred[e] >= 0 && t.sl[e] < 0) return true;
-  }
-  return false;
-}
 bool wave_ok(const DevProgram& D) {
   const char* v = getenv("KCEP_NFA_WAVE_AGG");
   const bool agg_on = !(v && v[0] == '0');
@@ -891,8 +881,20 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   }
   if (hipEventCreate(&s->ev0) || hipEventCreate(&s->ev1) || hipEventCreate(&s->eb0) || hipEventCreate(&s->eb1))
     return cleanup(fail(CEP_E_HIP, "event create failed"));
-  const char* env_wave = getenv("KCEP_NFA_WAVE");      // 0: the lane kernel for every pattern (A/B runs)
-  s->wave = P.general_ok && wave_ok(P.dev) && !(opts->flags & CEP_SESSION_LANE_NFA) && !(env_wave && !strcmp(env_wave, "0"));
+  // general path kernel: one key per wave (nfa_wave.h) where a key's live runs can multiply -- a stage
+  // with an IGNORE edge (skip-till-next / skip-till-any, the C4 run explosion) -- else one key per
+  // lane: keys of strict patterns hold a few runs, and a wave round costs a light key more than a
+  // lane's walk (C3 on the general path: 342 vs 107 ms, profiles/r03_ab_c3_general_wave_lane.log).
+  // CEP_SESSION_LANE_NFA / CEP_SESSION_WAVE_NFA or KCEP_NFA_WAVE=0/1 choose explicitly.
+  bool grows = false;
+  for (const auto& st : P.stages)
+    for (const auto& e : st.edges) grows = grows || e.op == E_IGNORE;
+  const char* env_wave = getenv("KCEP_NFA_WAVE");
+  bool wave = grows;
+  if (opts->flags & CEP_SESSION_LANE_NFA) wave = false;
+  else if (opts->flags & CEP_SESSION_WAVE_NFA) wave = true;
+  else if (env_wave) wave = env_wave[0] == '1';
+  s->wave = P.general_ok && wave && wave_ok(P.dev);
   const char* env_jit = getenv("KCEP_JIT");
   s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
   if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels

@@ -105,8 +105,8 @@ ExprP parse_expr(Reader& r, Program& P, int depth) {
       if (e->col >= int(P.coltypes.size()) || e->ct < SEQ_SUM || e->ct > SEQ_LAST) { r.bad = true; return nullptr; }
       const uint8_t ctype = P.coltypes[e->col];
       if ((e->ct == SEQ_FIRST || e->ct == SEQ_LAST) && isnull) { r.bad = true; return nullptr; }
-      if (e->ct == SEQ_SUM && ctype == T_F64) { r.bad = true; return nullptr; }   // (DoubleStream.sum: compensated)
-      e->t = e->ct == SEQ_COUNT || e->ct == SEQ_SUM ? T_I64 : ctype;
+      // sum over a double column: DoubleStream.sum, compensated (nfa_dev.h jsum_*), a double
+      e->t = e->ct == SEQ_COUNT ? T_I64 : e->ct == SEQ_SUM ? (ctype == T_F64 ? T_F64 : T_I64) : ctype;
       break;
     }
     case OP_NOT:
@@ -848,6 +848,19 @@ int compile_ir(const uint8_t* ir, size_t len, Program& P, std::string& err) {
     for (const auto& f : pd.folds) P.has_seq = P.has_seq || uses_seq(f.expr);
   }
   return CEP_OK;
+}
+
+// a pattern whose evaluations read or write more than the current record: aggregates (folds, defined
+// states, state reads) or partial sequences -- the wave kernel's stateful round machinery (nfa_wave.h)
+bool wave_stateful(const DevProgram& D) {
+  if (D.nstates || D.ndefined) return true;
+  for (int s = 0; s < D.nstages; s++) {
+    const DevStage& t = D.st[s];
+    if (t.nfolds) return true;
+    for (int e = 0; e < t.nedges; e++)
+      if (t.pred[e] >= 0 && t.sl[e] < 0) return true;
+  }
+  return false;
 }
 
 }  // namespace kcep

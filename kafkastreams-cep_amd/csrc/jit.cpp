@@ -359,7 +359,7 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   kcep::nfa_kernel_body(A);
 }
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()" + std::to_string(wave_occ) + R"())) void kcep_nfa_wave(kcep::NfaArgs A) {
-  kcep::nfa_wave_body(A);
+  kcep::nfa_wave_body<)" + std::string(wave_stateful(P.dev) || P.has_seq ? "true" : "false") + R"(>(A);
 }
 )";
   return o;

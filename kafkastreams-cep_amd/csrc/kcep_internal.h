@@ -174,6 +174,7 @@ struct StencilLaunch {
 
 // compile.cpp
 int lower_general(Program& P, std::string& why);
+bool wave_stateful(const DevProgram& D);
 int compile_ir(const uint8_t* ir, size_t len, Program& out, std::string& err);
 
 // ---- carried tails of the runs path (CEP_SESSION_CARRY, runs.hip) ----

@@ -53,7 +53,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nf
 
 // one key per wave, one queued run per lane (nfa_wave.h); patterns without aggregates
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_kernel(NfaArgs A) {
-  nfa_wave_body(A);
+  nfa_wave_body<false>(A);
+}
+// ... and patterns with aggregates or SequenceMatchers
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_agg_kernel(NfaArgs A) {
+  nfa_wave_body<true>(A);
 }
 
 // ---- segments, scans, output compaction, carry commit ----
@@ -154,7 +158,8 @@ hipError_t nfa_wave_launch(const NfaArgs& A, int64_t nwg, hipStream_t st, hipFun
     void* args[] = {&a};
     return hipModuleLaunchKernel(jf, unsigned(nwg), 1, 1, 64, 1, 1, 0, st, args, nullptr);
   }
-  hipLaunchKernelGGL(nfa_wave_kernel, dim3(unsigned(nwg)), dim3(64), 0, st, A);
+  if (A.wave_agg) hipLaunchKernelGGL(nfa_wave_agg_kernel, dim3(unsigned(nwg)), dim3(64), 0, st, A);
+  else hipLaunchKernelGGL(nfa_wave_kernel, dim3(unsigned(nwg)), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 

@@ -430,6 +430,53 @@ __device__ __forceinline__ int32_t* seq_scratch(Lane& l) {
   return l.heap + l.heap_top;
 }
 
+// Java 8's compensated double summation (Collectors.sumWithCompensation / computeFinalSum, used by
+// DoubleStream.sum / average and DoubleSummaryStatistics): Kahan sum + simple sum, finished as
+// sum + compensation (JDK 8), or the simple sum when that is NaN and the simple sum infinite.  The
+// build has -ffp-contract=off, so no step is fused.
+struct JSum {
+  double s = 0, c = 0, simple = 0;
+  __device__ __forceinline__ void add(double d) {
+    const double tmp = d - c;
+    const double velvel = s + tmp;
+    c = (velvel - s) - tmp;
+    s = velvel;
+    simple += d;
+  }
+  __device__ __forceinline__ double final_sum() const {
+    const double tmp = s + c;
+    return (tmp != tmp && __builtin_isinf(simple)) ? simple : tmp;
+  }
+};
+__device__ __forceinline__ int ev_cmp(const Lane& l, int a, int b);
+// the partial sequence's events in Sequence order -- what a stream over it visits (Sequence.java
+// build(true) :210-223: stages in reverse first-seen order of the walk, each stage's events a TreeSet
+// ascending by Event.compareTo, duplicates dropped); stage != SEQ_ANY_STAGE: that stage's only.
+// tmp: the walk's (slot, event) pairs.  Only the compensated double sums depend on this order.
+template <class F>
+__device__ __forceinline__ void seq_visit(const Lane& l, const int32_t* tmp, int cnt, int stage, F&& f) {
+  const auto& P = KCEP_PROG(l);
+  for (int gi = cnt - 1; gi >= 0; gi--) {
+    const int nm = P.slot_name[tmp[2 * gi]];
+    bool first = true;
+    for (int j = 0; j < gi && first; j++) first = P.slot_name[tmp[2 * j]] != nm;
+    if (!first || (stage != SEQ_ANY_STAGE && nm != stage)) continue;
+    int last = -1;
+    for (;;) {                                     // the next event of the stage's TreeSet
+      int pick = -1;
+      for (int i = 0; i < cnt; i++) {
+        if (P.slot_name[tmp[2 * i]] != nm) continue;
+        const int e = tmp[2 * i + 1];
+        if (last >= 0 && ev_cmp(l, e, last) <= 0) continue;
+        if (pick < 0 || ev_cmp(l, e, pick) < 0) pick = e;
+      }
+      if (pick < 0) break;
+      f(pick);
+      last = pick;
+    }
+  }
+}
+
 // SequenceMatcher: average of a column over buffer.get(Matched(prev, prevEvent), version)
 // (SequenceMatcher.java:21-26), with Sequence's per-stage TreeSet de-duplication.
 __device__ __forceinline__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t& out) {
@@ -440,18 +487,21 @@ __device__ __forceinline__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t&
   if (cnt < 0) return false;
   const int t = KCEP_PROG(l).coltype[col];
   int64_t isum = 0;
-  double fsum = 0;
+  JSum js;
   int64_t n = 0;
-  for (int i = 0; i < cnt; i++) {
-    bool dup = false;
-    for (int j = 0; j < i && !dup; j++)
-      dup = KCEP_PROG(l).slot_name[tmp[2 * j]] == KCEP_PROG(l).slot_name[tmp[2 * i]] && ev_same(l, tmp[2 * j + 1], tmp[2 * i + 1]);
-    if (dup) continue;
-    const int64_t v = ev_field(l, col, t, tmp[2 * i + 1]);
-    if (t == T_F64) fsum += as_f(v); else isum += v;
-    n++;
+  if (t == T_F64) {                                // DoubleStream.average: compensated, in Sequence order
+    seq_visit(l, tmp, cnt, SEQ_ANY_STAGE, [&](int e) { js.add(as_f(ev_field(l, col, t, e))); n++; });
+  } else {
+    for (int i = 0; i < cnt; i++) {
+      bool dup = false;
+      for (int j = 0; j < i && !dup; j++)
+        dup = KCEP_PROG(l).slot_name[tmp[2 * j]] == KCEP_PROG(l).slot_name[tmp[2 * i]] && ev_same(l, tmp[2 * j + 1], tmp[2 * i + 1]);
+      if (dup) continue;
+      isum += ev_field(l, col, t, tmp[2 * i + 1]);
+      n++;
+    }
   }
-  const double avg = n ? (t == T_F64 ? fsum : double(isum)) / double(n) : 0.0;
+  const double avg = n ? (t == T_F64 ? js.final_sum() : double(isum)) / double(n) : 0.0;
   out = as_b(avg);
   return true;
 }
@@ -475,6 +525,14 @@ __device__ __forceinline__ bool seq_agg(Lane& l, const Ctx& c, int kind, int col
   if (cnt < 0) return false;
   const auto& P = KCEP_PROG(l);
   const int t = P.coltype[col];
+  if (kind == SEQ_SUM && t == T_F64) {             // DoubleStream.sum: compensated, in Sequence order
+    JSum js;
+    int64_t m = 0;
+    seq_visit(l, tmp, cnt, stage, [&](int e) { js.add(as_f(ev_field(l, col, t, e))); m++; });
+    if (m == 0 && stage != SEQ_ANY_STAGE) { l.err = CEP_E_NPE; return false; }
+    out = as_b(js.final_sum());
+    return true;
+  }
   int64_t n = 0, acc = 0;
   int pick = -1;                                   // FIRST / LAST: the event chosen so far
   for (int i = 0; i < cnt; i++) {

@@ -50,7 +50,6 @@ struct WaveShared {
   int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
   int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
   int32_t *arena, arena_used;      // the key's LDS arena and its bump pointer (re-allocations go there first)
-  int32_t cseq[WAVE], cown[WAVE];  // stateful patterns: each lane's run sequence / whether it wrote it
   // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
   int32_t ms_slot[WAVE], ms_e[WAVE], ms_pv[WAVE], ms_cnt[WAVE], ms_done[WAVE], ms_err[WAVE];
 };
@@ -379,15 +378,16 @@ __device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared& w, int lane
 // and one of them wrote it -- the later run would have read the earlier one's fold (NFA.java:319-321,
 // 362-369) -- or, with SequenceMatchers, a run died before others read partial sequences (its
 // removePattern, NFA.java:142-143, changes the buffer they walk).
-__device__ __forceinline__ bool wave_round_conflict(const Lane& l, WaveShared& w, int lane, bool act, int seq,
+// conf: 2 x WAVE words of LDS (each lane's run sequence, whether it wrote it)
+__device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf, int lane, bool act, int seq,
                                                     uint64_t dmask) {
   if ((l.A->wave_agg & 2) && dmask) return true;
   if (!(l.A->wave_agg & 1)) return false;
-  w.cseq[lane] = act ? seq : INT32_MIN;
-  w.cown[lane] = act && l.ov_own;
+  conf[lane] = act ? seq : INT32_MIN;
+  conf[WAVE + lane] = act && l.ov_own;
   __syncthreads();
   bool c = false;
-  for (int j = 0; j < lane && act; j++) c = c || (w.cseq[j] == seq && (w.cown[j] || l.ov_own));
+  for (int j = 0; j < lane && act; j++) c = c || (conf[j] == seq && (conf[WAVE + j] || l.ov_own));
   __syncthreads();
   return __ballot(c) != 0;
 }
@@ -402,8 +402,13 @@ __device__ __forceinline__ bool wave_round_conflict(const Lane& l, WaveShared& w
 #define KWP_ADD(i, t)
 #endif
 
+// AGG: the pattern reads or writes aggregates / reads partial sequences (DevProgram, abi.cpp
+// wave_stateful): the round machinery for them (conflict checks, the sequential re-evaluation,
+// applying the logged aggregate writes) is compiled in only then.
+template <bool AGG>
 __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   __shared__ WaveShared w;
+  __shared__ int32_t s_conf[AGG ? 2 * WAVE : 1];
   const int lane = threadIdx.x;
   const int seg = A.wave_seg ? A.wave_seg[blockIdx.x] : int(blockIdx.x);
   if (seg >= A.nseg) return;
@@ -564,7 +569,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         dmask = __ballot(dead);
         // a conflict is checked before the errors: a run may throw on a state an earlier run of the
         // round would have folded first
-        if (A.wave_agg && wave_round_conflict(l, w, lane, act, run.seq, dmask)) {
+        if (AGG && A.wave_agg && wave_round_conflict(l, s_conf, lane, act, run.seq, dmask)) {
           seqd = true;
           l.tlen = 0; l.log_n = 0; l.nph = 0;                  // the parallel pass is discarded
           continue;
@@ -618,7 +623,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       KWP_MARK(t_pl);
       int nrun = 0;
       const int rb = w.runs + wave_excl_scan(l.nph, lane, nrun);
-      if ((A.wave_agg & 1) && !seqd && !wave_apply_aggs(l, w, lane, rb)) {   // the round's folds and copies
+      if (AGG && (A.wave_agg & 1) && !seqd && !wave_apply_aggs(l, w, lane, rb)) {   // the round's folds and copies
         if (lane == 0) w.overflow = 1;
         break;
       }

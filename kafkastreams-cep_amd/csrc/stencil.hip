@@ -82,6 +82,39 @@ __global__ __launch_bounds__(1024) void tile_scan(const int64_t* __restrict__ cn
   if (tid == 1023) *total = run;
 }
 
+// small batches (processor flushes): the scan and the gather in one workgroup, one launch instead of
+// two -- the prefix of <= 1024 super-tile counts in LDS, then each wave copies super-tiles' slots
+constexpr int SMALL_FINISH = 1024;
+__global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __restrict__ slots,
+                                                             const int64_t* __restrict__ cnt, int64_t nt, int k,
+                                                             int32_t* __restrict__ out, int64_t out_cap, int sub,
+                                                             int64_t* __restrict__ total) {
+  __shared__ int64_t s_pre[SMALL_FINISH + 1];
+  __shared__ int64_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t c = tid < nt ? cnt[tid] : 0;
+  int64_t incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  int64_t run = incl - c;
+  for (int w = 0; w < wid; w++) run += s_w[w];
+  s_pre[tid] = run;
+  if (tid == 1023) { s_pre[SMALL_FINISH] = run + c; *total = run + c; }
+  __syncthreads();
+  for (int64_t t = wid; t < nt; t += 16) {                 // one wave per super-tile
+    const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
+    if (pre + m > out_cap) continue;
+    const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
+    int32_t* dst = out + pre * k;
+    for (int64_t w = lane; w < m * k; w += 64) dst[w] = src[w];
+  }
+}
+
 static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
   if (L.chain && L.k != 3 && L.k != 4) return hipErrorInvalidValue;   // an optional stage needs k >= 3; chain k <= 4
   switch (L.k) {
@@ -113,6 +146,11 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e == hipSuccess) e = stencil_count(L, st);
   if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
+  if (nsuper <= SMALL_FINISH) {
+    hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
+                       L.out_cap, sub, L.total);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total);
   hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre, L.k,
                      L.out, L.out_cap, sub);

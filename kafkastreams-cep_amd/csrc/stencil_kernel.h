@@ -30,8 +30,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "kcep_internal.h"
@@ -750,151 +748,10 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 }
 
 
-// ---- the plain stencil (no carry, no optional stage) with one wave per super-tile ----
-// The workgroup kernel above stages every tile through LDS to hand each thread 16 consecutive
-// records, with two barriers per tile.  Without carried halos and chain runs the window a record
-// needs is only the K-1 records before it, so a wave can work on its lane-contiguous 16-B vectors
-// directly: records q*256 + 4*lane .. +3 of a 1024-record wave-tile, the up to 7 earlier records
-// from the two lanes below (lane 0 and 1: lanes 62/63 of the previous vector row) by cross-lane
-// shuffles.  No LDS image, no barrier: a wave streams its super-tile (SUB x 4096 records) with the
-// next wave-tile's loads in flight while it tests the current one, and writes its matches in record
-// order straight into the super-tile's slot (the offsets of a row's hits by ballot + mbcnt).  The
-// slot / count layout is the workgroup kernel's, so tile_scan and stencil_gather are shared.
-constexpr int SW_WT = 1024;                      // records per wave-tile (64 lanes x 16)
-
-__device__ __forceinline__ v4i shfl4(const v4i& x, int src) {
-  return v4i{__shfl(x[0], src), __shfl(x[1], src), __shfl(x[2], src), __shfl(x[3], src)};
-}
-
-template <int K, class VT, bool TOPIC, int SUB>
-__global__ __launch_bounds__(64) void stencil_wave_kernel(const int32_t* __restrict__ key, const VT* __restrict__ val,
-                                                          const int32_t* __restrict__ topic, int64_t n,
-                                                          const StencilProgram* __restrict__ P, int32_t* __restrict__ out,
-                                                          int64_t* __restrict__ tile_count, int64_t ntiles) {
-  __shared__ uint8_t s_tab[64];
-  __shared__ uint8_t s_lut[256];
-  __shared__ uint8_t s_nan[4];
-  const int lane = threadIdx.x;
-  s_tab[lane] = P->table[lane];
-#pragma unroll
-  for (int i = 0; i < 4; i++) s_lut[lane + 64 * i] = P->lut[lane + 64 * i];
-  if (lane < 4) s_nan[lane] = P->nan_mask[lane];
-  const int64_t tile0 = int64_t(blockIdx.x) * SUB;
-  int64_t base = tile0 * ST_TILE;
-  const int64_t end = (tile0 + SUB) * ST_TILE < n ? (tile0 + SUB) * ST_TILE : n;
-  const int nwt = int((end - base + SW_WT - 1) / SW_WT);
-  Chunk<VT, TOPIC> cur;
-  load_chunk<VT, TOPIC, 256>(cur, key, val, topic, base, n, lane);
-  // the previous vector row of lanes 62 / 63: the 8 records before the super-tile
-  v4i pk = v4i{INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN};
-  uint32_t pm = 0;
-  VT hv[4];
-  int32_t ht[4] = {0, 0, 0, 0};
-  const bool hl = lane >= 62 && base > 0;
-  if (hl) {
-    const int64_t g = base - 4 * (64 - lane);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      pk[i] = key[g + i];
-      hv[i] = val[g + i];
-      if constexpr (TOPIC) ht[i] = topic[g + i];
-    }
-  }
-  __syncthreads();                                 // the tables (one wave: no wait)
-  if (hl) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) pm |= mask_of<VT, TOPIC>(P, s_tab, s_nan, hv[i], ht[i]) << (8 * i);
-  }
-  int32_t* const slot = out + tile0 * int64_t(ST_TILE) * K;
-  int64_t o = 0;                                   // matches written so far (wave-uniform)
-  const int src1 = (lane + 63) & 63, src2 = (lane + 62) & 63;
-  for (int t = 0; t < nwt; t++) {
-    uint32_t packed[4];
-    masks_of_chunk<VT, TOPIC>(cur, P, s_tab, s_nan, packed, s_lut);
-    v4i kk[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      kk[q] = cur.k[q];
-      const int64_t left = n - (base + q * 256 + 4 * lane);   // records >= n match nothing
-      if (left < 4) packed[q] &= left <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - left)));
-    }
-    if (t + 1 < nwt) load_chunk<VT, TOPIC, 256>(cur, key, val, topic, base + SW_WT, n, lane);   // in flight
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const v4i prk = q == 0 ? pk : kk[q - 1];     // this lane's vector of the previous row
-      const uint32_t prm = q == 0 ? pm : packed[q - 1];
-      int32_t wk[12];
-      uint64_t wm = uint64_t(packed[q]) << 32;     // window masks, record w at byte w - 4 (w >= 4)
-      const v4i n1 = shfl4(lane == 63 ? prk : kk[q], src1);
-      const uint32_t m1 = __shfl(lane == 63 ? prm : packed[q], src1);
-      wm |= m1;
-#pragma unroll
-      for (int i = 0; i < 4; i++) { wk[4 + i] = n1[i]; wk[8 + i] = kk[q][i]; wk[i] = INT32_MIN; }
-      uint32_t m2 = 0;
-      if constexpr (K > 5) {
-        const v4i n2 = shfl4(lane >= 62 ? prk : kk[q], src2);
-        m2 = __shfl(lane >= 62 ? prm : packed[q], src2);
-#pragma unroll
-        for (int i = 0; i < 4; i++) wk[i] = n2[i];
-      }
-      uint32_t h4 = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        bool ok = true;
-#pragma unroll
-        for (int s = 0; s < K; s++) {
-          const int w = 8 + i - (K - 1) + s;       // window position of stage s's record
-          const uint32_t mb = w >= 4 ? uint32_t(wm >> (8 * (w - 4))) : (m2 >> (8 * w));
-          ok = ok && ((mb >> s) & 1) && wk[w] == wk[8 + i];
-        }
-        h4 |= uint32_t(ok) << i;
-      }
-      // this row's hits in record order (lane-major, then the 4 records of a lane)
-      uint32_t before = 0, tot = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint64_t b = __ballot((h4 >> i) & 1);
-        before += __builtin_amdgcn_mbcnt_hi(uint32_t(b >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(b), 0u));
-        tot += uint32_t(__popcll(b));
-      }
-      if (h4) {
-        int64_t idx = o + before;
-        const int32_t r0 = int32_t(base + q * 256 + 4 * lane);   // < 2^31 (checked by the launcher)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          if ((h4 >> i) & 1) {
-            int32_t* d = slot + idx * K;
-#pragma unroll
-            for (int s = 0; s < K; s++) d[s] = r0 + i - (K - 1) + s;
-            idx++;
-          }
-        }
-      }
-      o += tot;
-    }
-    pk = kk[3];
-    pm = packed[3];
-    base += SW_WT;
-  }
-  if (lane == 0) tile_count[blockIdx.x] = o;
-}
-
-// KCEP_STENCIL=wg: the workgroup kernel for plain stencil batches too (A/B)
-inline bool stencil_use_wave() {
-  static const bool wave = [] {
-    const char* e = getenv("KCEP_STENCIL");
-    return !(e && e[0] == 'w' && e[1] == 'g');
-  }();
-  return wave;
-}
-
 template <int K, class VT, bool TP, bool CH, int SUB>
 inline void launch_kts(const StencilLaunch& L, int64_t ntiles, hipStream_t st) {
   const int64_t nsuper = (ntiles + SUB - 1) / SUB;
-  if (!CH && !L.carry.hdr && stencil_use_wave())
-    hipLaunchKernelGGL((stencil_wave_kernel<K, VT, TP, SUB>), dim3(unsigned(nsuper)), dim3(64), 0, st, L.key,
-                       static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles);
-  else if (L.carry.hdr)
+  if (L.carry.hdr)
     hipLaunchKernelGGL((stencil_kernel<K, VT, TP, CH, true, SUB>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
                        L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles,
                        L.carry);

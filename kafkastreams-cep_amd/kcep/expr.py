@@ -560,10 +560,8 @@ def bind(e: Expr, schema) -> Expr:
         if e.kind == SEQ_COUNT:
             return SeqAgg(SEQ_COUNT, 0, T_I64, e.stage)
         col, t = schema.resolve(e.name)
-        if e.kind == SEQ_SUM:
-            if type_code(t) == T_F64:
-                raise TypeError("sum over a double column is DoubleStream.sum (compensated): not lowered")
-            t = T_I64
+        if e.kind == SEQ_SUM:                       # LongStream.sum, or DoubleStream.sum (compensated)
+            t = T_F64 if type_code(t) == T_F64 else T_I64
         return SeqAgg(e.kind, col, t, e.stage)
     if isinstance(e, Bin):
         return Bin(e.op, bind(e.a, schema), bind(e.b, schema))

@@ -29,6 +29,7 @@ SESSION_CARRY = 1
 SESSION_INTERPRET = 2
 SESSION_PROFILE = 4
 SESSION_LANE_NFA = 8
+SESSION_WAVE_NFA = 16
 
 
 class CepError(RuntimeError):
@@ -135,10 +136,11 @@ def lib():
     L.cep_partition.argtypes = [P, C.c_int64, C.c_int32, P, C.c_int64, P, P, C.c_int32, P]
     L.cep_gather.argtypes = [P, C.c_int32, P, C.c_int64, P, C.c_int32, P]
     L.cep_match_count_to.argtypes = [P, P, P]
-    L.cep_state_evict.argtypes = [P, P, C.c_int64, C.POINTER(C.c_void_p), P]
-    L.cep_state_import_keys.argtypes = [P, P, P, P, C.c_int64]
-    L.cep_state_positions.argtypes = [P, C.c_size_t, P, C.c_int64, C.POINTER(C.c_int64)]
-    L.cep_session_set_max_key_words.argtypes = [P, C.c_int64]
+    if hasattr(L, "cep_state_evict"):       # (KCEP_LIB A/B runs may load an older build)
+        L.cep_state_evict.argtypes = [P, P, C.c_int64, C.POINTER(C.c_void_p), P]
+        L.cep_state_import_keys.argtypes = [P, P, P, P, C.c_int64]
+        L.cep_state_positions.argtypes = [P, C.c_size_t, P, C.c_int64, C.POINTER(C.c_int64)]
+        L.cep_session_set_max_key_words.argtypes = [P, C.c_int64]
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -213,7 +215,7 @@ class Session:
     """One ``cep_session`` (one stream task's processor on one GPU)."""
 
     def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0,
-                 carry=False, max_keys=0, interpret=False, profile=False, max_key_words=0, lane_nfa=False):
+                 carry=False, max_keys=0, interpret=False, profile=False, max_key_words=0, lane_nfa=None):
         """``carry=True``: every key's NFA state continues across batches (CEP_SESSION_CARRY);
         key ids must then be dense in [0, max_keys) and record positions are stream positions.
         ``interpret=True``: the built-in interpreting kernels instead of kernels compiled for the
@@ -222,8 +224,10 @@ class Session:
         (``batch_errors`` lists it with RunCapacity), every other key completes."""
         self.pattern = pattern
         self.h = C.c_void_p()
+        # lane_nfa: None = the library's choice, True = one key per lane, False = one key per wave
         flags = ((SESSION_CARRY if carry else 0) | (SESSION_INTERPRET if interpret else 0) |
-                 (SESSION_PROFILE if profile else 0) | (SESSION_LANE_NFA if lane_nfa else 0))
+                 (SESSION_PROFILE if profile else 0) | (SESSION_LANE_NFA if lane_nfa else 0) |
+                 (SESSION_WAVE_NFA if lane_nfa is False else 0))
         o = Opts(device, mode, force_path, flags, max_events, max_keys, 0.0, max_key_words)
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)

@@ -260,8 +260,9 @@ static Expr* rd_expr(orc_pattern* p, Rd* r, int depth) {
       }
       if (e->col >= p->ncols || e->ct < SEQ_SUM || e->ct > SEQ_LAST) { r->bad = 1; return NULL; }
       if ((e->ct == SEQ_FIRST || e->ct == SEQ_LAST) && isnull) { r->bad = 1; return NULL; }
-      if (e->ct == SEQ_SUM && p->coltype[e->col] == T_F64) { r->bad = 1; return NULL; }
-      e->t = (e->ct == SEQ_SUM || e->ct == SEQ_COUNT) ? T_I64 : p->coltype[e->col];
+      /* sum over a double column: DoubleStream.sum (compensated, below) stays a double */
+      e->t = e->ct == SEQ_COUNT ? T_I64 : e->ct == SEQ_SUM ? (p->coltype[e->col] == T_F64 ? T_F64 : T_I64)
+                                                          : p->coltype[e->col];
       break;
     }
     case OP_NOT:
@@ -861,6 +862,23 @@ static int read_col(const orc_batch* b, const orc_pattern* p, int col, int64_t r
   return ORC_OK;
 }
 
+/* Java 8's compensated double summation (Collectors.sumWithCompensation / computeFinalSum, which
+   DoubleStream.sum and DoubleStream.average / DoubleSummaryStatistics use): a Kahan sum plus the
+   simple sum, finished as sum + compensation (JDK 8 adds the compensation term), the simple sum
+   when that is NaN and the simple sum is infinite.  Values in Sequence order. */
+typedef struct { double s, c, simple; } JSum;
+static void jsum_add(JSum* j, double d) {
+  const double tmp = d - j->c;
+  const double velvel = j->s + tmp;
+  j->c = (velvel - j->s) - tmp;
+  j->s = velvel;
+  j->simple += d;
+}
+static double jsum_final(const JSum* j) {
+  const double tmp = j->s + j->c;
+  return isnan(tmp) && isinf(j->simple) ? j->simple : tmp;
+}
+
 static int seq_avg(EC* c, int col, Val* out) {
   /* SequenceMatcher.accept (SequenceMatcher.java:21-26): buffer.get(Matched.from(prev, prevEvent), version) */
   orc_run* R = c->R;
@@ -870,12 +888,12 @@ static int seq_avg(EC* c, int col, Val* out) {
   if (rc) return rc;
   int64_t gb, ge;
   materialise(R, eb, ee, &gb, &ge);
-  double sum = 0; int64_t cnt = 0; int64_t isum = 0;
+  JSum js = {0, 0, 0}; int64_t cnt = 0; int64_t isum = 0;
   for (int64_t g = gb; g < ge; g++)
     for (int64_t i = 0; i < R->grp_cnt.a[g]; i++) {
       Val v; rc = read_col(R->b, R->p, col, R->grp_ev.a[R->grp_evoff.a[g] + i], &v);
       if (rc) return rc;
-      if (v.t == T_F64) sum += v.u.d; else isum += (v.t == T_I32 ? v.u.i : v.u.l);
+      if (v.t == T_F64) jsum_add(&js, v.u.d); else isum += (v.t == T_I32 ? v.u.i : v.u.l);
       cnt++;
     }
   /* drop the temporary traversal + groups */
@@ -883,7 +901,7 @@ static int seq_avg(EC* c, int col, Val* out) {
   R->grp_ev.n = ge > gb ? R->grp_evoff.a[gb] : R->grp_ev.n;
   R->grp_name.n = gb; R->grp_cnt.n = gb; R->grp_evoff.n = gb;
   out->t = T_F64;
-  out->u.d = cnt ? (R->p->coltype[col] == T_F64 ? sum : (double)isum) / (double)cnt : 0.0;
+  out->u.d = cnt ? (R->p->coltype[col] == T_F64 ? jsum_final(&js) : (double)isum) / (double)cnt : 0.0;
   return ORC_OK;
 }
 
@@ -901,6 +919,7 @@ static int seq_agg(EC* c, int kind, int col, int stage, uint8_t t, Val* out) {
   int64_t gb, ge;
   materialise(R, eb, ee, &gb, &ge);
   int64_t n = 0; uint64_t isum = 0; Val acc = {0}; int64_t first = -1, last = -1;
+  JSum js = {0, 0, 0};
   const uint8_t ctype = R->p->coltype[col];
   for (int64_t g = gb; g < ge && !rc; g++) {
     if (stage != -1 && R->grp_name.a[g] != stage) continue;
@@ -911,7 +930,8 @@ static int seq_agg(EC* c, int kind, int col, int stage, uint8_t t, Val* out) {
       Val v;
       rc = read_col(R->b, R->p, col, ev, &v);
       if (rc) break;
-      if (kind == SEQ_SUM) isum += (uint64_t)(v.t == T_I32 ? (int64_t)v.u.i : v.u.l);
+      if (kind == SEQ_SUM && v.t == T_F64) jsum_add(&js, v.u.d);
+      else if (kind == SEQ_SUM) isum += (uint64_t)(v.t == T_I32 ? (int64_t)v.u.i : v.u.l);
       else if (kind == SEQ_MIN || kind == SEQ_MAX) {
         if (n == 0) acc = v;
         else if (ctype == T_F64) {
@@ -938,6 +958,7 @@ static int seq_agg(EC* c, int kind, int col, int stage, uint8_t t, Val* out) {
     return err_at(R, ORC_E_NPE, "Sequence.getByName: no such stage in the partial sequence");
   out->t = t;
   if (kind == SEQ_COUNT) out->u.l = n;
+  else if (kind == SEQ_SUM && t == T_F64) out->u.d = jsum_final(&js);
   else if (kind == SEQ_SUM) out->u.l = (int64_t)isum;
   else if (kind == SEQ_MIN || kind == SEQ_MAX) *out = acc;
   else return read_col(R->b, R->p, col, kind == SEQ_FIRST ? first : last, out);

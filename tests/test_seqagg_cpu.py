@@ -68,10 +68,49 @@ def test_missing_stage_is_a_null_pointer():
 def test_dsl_rules():
     with pytest.raises(ValueError):
         SequenceAgg.first()                          # first/last read one stage's TreeSet
+
+
+def java8_double_sum(vals):
+    """DoubleStream.sum of Java 8 (Collectors.sumWithCompensation + computeFinalSum: the Kahan sum
+    finished as sum + compensation, the simple sum if that is NaN and the simple sum infinite),
+    restated from the JDK 8 sources' algorithm for the hand-pinned expectations below."""
+    s = c = simple = 0.0
+    for d in vals:
+        tmp = d - c
+        velvel = s + tmp
+        c = (velvel - s) - tmp
+        s = velvel
+        simple += d
+    t = s + c
+    return simple if (t != t and abs(simple) == float("inf")) else t
+
+
+def test_double_sum_is_compensated():
+    """SequenceAgg.sum over a double column is DoubleStream.sum: compensated.  1e16 + 1.0 + 1.0 in
+    Sequence order (a, then b's TreeSet) is 1e16 naively but 1e16 + 2 compensated, so c's predicate
+    sum > 1e16 holds.  Parity unpinned by the reference itself (no JVM here): the expectation follows
+    JDK 8's summation algorithm (java8_double_sum)."""
+    assert java8_double_sum([1e16, 1.0, 1.0]) == 1e16 + 2 and (1e16 + 1.0) + 1.0 == 1e16
     sch = Schema([("px", "f64")])
-    p = QueryBuilder().select("a").where(Event.field("px") > SequenceAgg.sum("px")).build()
-    with pytest.raises(TypeError):
-        p.to_ir(sch)                                 # DoubleStream.sum is compensated: not lowered
+    px = Event.field("px")
+    p = (QueryBuilder().select("a").where(px >= 1e15).then()
+         .select("b").oneOrMore().where((px > 0.0) & (px < 10.0)).then()
+         .select("c").where((px < 0.0) & (SequenceAgg.sum("px") > 1e16)).build())
+    op = O.OraclePattern(p.to_ir(sch))
+    vals = np.array([1e16, 1.0, 1.0, -1.0, 1e16, 1.0, -1.0], np.float64)   # second run: 1e16 + 1 -> 1e16
+    r = O.OracleRun(op, O.MODE_PROCESSOR)
+    r.process(O.BatchArrays(np.zeros(len(vals), np.int32), [vals], [3]))
+    got = [m.record for m in r.matches(with_groups=False)]
+    assert got == [3]
+    # the average over a double column is DoubleStream.average: the same compensated sum / count.
+    # run 1: (1e16 + 2) / 3 * 3 > 1e16 (naively 1e16 / 3 * 3 == 1e16, no match); run 2: 1e16 / 2 * 3
+    assert java8_double_sum([1e16, 1.0, 1.0]) / 3 * 3.0 > 1e16 and (1e16 + 1.0 + 1.0) / 3 * 3.0 == 1e16
+    q = (QueryBuilder().select("a").where(px >= 1e15).then()
+         .select("b").oneOrMore().where((px > 0.0) & (px < 10.0)).then()
+         .select("c").where((px < 0.0) & (SequenceAgg.avg("px") * 3.0 > 1e16)).build())
+    r = O.OracleRun(O.OraclePattern(q.to_ir(sch)), O.MODE_PROCESSOR)
+    r.process(O.BatchArrays(np.zeros(len(vals), np.int32), [vals], [3]))
+    assert [m.record for m in r.matches(with_groups=False)] == [3, 6]
 
 
 def test_native_compile_routes_to_general_path():

@@ -93,3 +93,29 @@ def test_missing_stage_raises_npe_at_the_same_record():
     key, val = rand_stream(3, 40, 10, 3)
     want, got, oerr, gerr = run_both(p.to_ir(PL.I32), O.MODE_PROCESSOR, key, [val], [1])
     assert oerr is not None and oerr[0] == 4 and gerr == oerr and got == want
+
+
+@pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
+@pytest.mark.parametrize("interpret", [False, True], ids=["jit", "interp"])
+def test_double_sum_and_average_compensated(interpret, lane_nfa):
+    """SequenceAgg.sum / avg over a double column are DoubleStream.sum / average: Java 8's compensated
+    sum, over the partial sequence in Sequence order (stages in build(true) order, each stage's
+    TreeSet ascending).  Magnitudes mixed so that the compensation and the order change results;
+    the device must agree with the oracle on every match (tests/test_seqagg_cpu.py pins the
+    algorithm by hand)."""
+    from kcep import Schema
+    sch = Schema([("px", "f64")])
+    px = Event.field("px")
+    p = (QueryBuilder().select("a").where(px > 1e12).then()
+         .select("b", Selected.withSkipTilNextMatch()).oneOrMore().where((px > 0.0) & (px < 1e3)).then()
+         .select("c", Selected.withSkipTilNextMatch())
+         .where((px < 0.0) & ((SequenceAgg.sum("px") * 7.0 > SequenceAgg.avg("px") * 7.0 * SequenceAgg.count())
+                              | (SequenceAgg.sum("px", stage="b") > 1.5))).build())
+    rng = np.random.default_rng(11)
+    key, _ = rand_stream(21, 120, 12, 4)
+    kind = rng.integers(0, 3, len(key))
+    val = np.where(kind == 0, rng.choice([1e16, 3e15, 7.1e12], len(key)),
+                   np.where(kind == 1, rng.choice([1.0, 0.5, 0.1, 3.3], len(key)), -1.0)).astype(np.float64)
+    want, got, oerr, gerr = run_both(p.to_ir(sch), O.MODE_PROCESSOR, key, [val], [3], interpret=interpret,
+                                     lane_nfa=lane_nfa)
+    assert oerr is None and gerr is None and got == want and len(want) > 0
