@@ -272,7 +272,7 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int64_t ntiles = stencil_tiles(b->n);
   StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic, SP.chain,
                   s->slots.as<int32_t>(), tc, tc + ntiles + 1, s->counter.as<int64_t>(), s->out.as<int32_t>(),
-                  s->out_cap, s->total.as<int64_t>(), StencilCarry{}};
+                  s->out_cap, s->total.as<int64_t>(), StencilCarry{}, !getenv_flag("KCEP_STENCIL_KEYED")};
   if (s->carry) {                                // the keys' halos: read the previous, write the next
     HIPCHECK(hipMemsetAsync(s->hflags.p, 0, 8, st));
     const char* dbg = getenv("KCEP_CARRY_DBG");   // A/B probes of the carry kernel's parts (tools/carry_probe.py)

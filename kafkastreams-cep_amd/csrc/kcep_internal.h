@@ -170,6 +170,7 @@ struct StencilLaunch {
   int64_t out_cap;                // matches
   int64_t* total;                 // device: number of matches
   StencilCarry carry;             // halo != nullptr: carry session
+  int plain;                      // plain stencil (no carry, no chain, k <= 7): the keyless kernel (KCEP_STENCIL_KEYED=1: off)
 };
 
 // compile.cpp

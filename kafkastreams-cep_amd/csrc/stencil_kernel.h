@@ -748,9 +748,201 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 }
 
 
+// ---- the plain stencil (no carry, no optional stage, K <= 7): no keys in LDS ----
+// A match needs the K-1 records before record j to have j's key, i.e. the chain of "same key as the
+// record before" bits over j-K+2..j.  So the LDS image of a tile holds ONE byte per record: the
+// stage bits (bits 0..K-1) with the same-key bit in bit 7, computed by the loading thread (the key
+// of the record before its first one comes from the lane below by a shuffle).  Only records at a
+// multiple of 256 in the tile have their predecessor in another wave: their bit is resolved by the
+// reader from two 17-entry LDS key tables.  The window test is bit-parallel over the thread's 24
+// window records (8 of history + its 16): hit(p) = AND_s B_s(p-K+1+s) AND_d same(p-d), d < K-1.
+// Against the keyed kernel: 4 B instead of 5 B of LDS traffic per record written and 3 instead of
+// 9 LDS reads per window, ~12 KB of LDS per workgroup instead of 25 KB, no 24-key register window.
+// load_chunk for a tile that lies wholly inside the batch (uniform branch): uniform tile base
+// pointers and 32-bit lane offsets, so every load is one saddr + voffset instruction
+template <class VT, bool TOPIC>
+__device__ __forceinline__ void load_tile(Chunk<VT, TOPIC>& c, const int32_t* __restrict__ key,
+                                          const VT* __restrict__ val, const int32_t* __restrict__ topic,
+                                          int64_t base, int64_t n, int tid) {
+  if (base + ST_TILE > n) {
+    load_chunk<VT, TOPIC>(c, key, val, topic, base, n, tid);
+    return;
+  }
+  const int32_t* kb = key + base;
+  const VT* vb = val + base;
+  const int32_t* tb = TOPIC ? topic + base : nullptr;
+#pragma unroll
+  for (int q = 0; q < ST_EPT / 4; q++) {
+    const uint32_t o = uint32_t(q * (ST_THREADS * 4) + tid * 4);
+    c.k[q] = ld_nt4(kb + o);
+    if constexpr (sizeof(VT) == 4) {
+      c.v[q].a = ld_nt4(vb + o);
+    } else {
+      c.v[q].a = ld_nt2(vb + o);
+      c.v[q].b = ld_nt2(vb + o + 2);
+    }
+    if constexpr (TOPIC) c.t[q] = ld_nt4(tb + o);
+  }
+}
+
+#ifndef ST_PLAIN_EARLY
+#define ST_PLAIN_EARLY 1                          // next tile's loads issued before the image barrier (A/B knob)
+#endif
+#ifndef ST_PLAIN_WAVES
+#define ST_PLAIN_WAVES 6                          // waves per SIMD the register budget is cut for (A/B knob)
+#endif
+template <int K, class VT, bool TOPIC, int SUB>
+__global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kernel(
+    const int32_t* __restrict__ key, const VT* __restrict__ val, const int32_t* __restrict__ topic, int64_t n,
+    const StencilProgram* __restrict__ P, int32_t* __restrict__ out, int64_t* __restrict__ tile_count,
+    int64_t ntiles) {
+  static_assert(K >= 1 && K <= 7, "bit 7 of a record's byte is its same-key bit");
+  __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];   // record r at r + 16
+  __shared__ int32_t s_lastk[2][17];   // [tile & 1][m]: key of tile record 256m - 1 (m >= 1); [0][0]: before tile 0
+  __shared__ int32_t s_firstk[16];     // key of tile record 256m
+  __shared__ uint16_t s_match[ST_TILE];
+  __shared__ int32_t s_wsum[2][ST_THREADS / 64];
+  __shared__ uint8_t s_tab[64];
+  __shared__ uint8_t s_lut[256];
+  __shared__ uint8_t s_nan[4];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  if (tid < 64) s_tab[tid] = P->table[tid];
+  s_lut[tid] = P->lut[tid];                       // (ST_THREADS == 256 entries)
+  if (tid < 4) s_nan[tid] = P->nan_mask[tid];
+  const int64_t tile0 = int64_t(blockIdx.x) * SUB;
+  const int ntl = int(ntiles - tile0 < SUB ? ntiles - tile0 : SUB);
+
+  Chunk<VT, TOPIC> cur;
+  load_tile<VT, TOPIC>(cur, key, val, topic, tile0 * ST_TILE, n, tid);
+  // the first tile's halo (its K-1 records before; later tiles take the previous tile's LDS bytes)
+  const bool halo_lane = tid >= 16 - (K - 1) && tid < 16;
+  const int64_t hg = tile0 * ST_TILE - 16 + tid;
+  int32_t h_key = INT32_MIN, h_prev = INT32_MIN, h_top = 0;
+  VT h_val{};
+  if (halo_lane && hg >= 0) {
+    h_key = key[hg];
+    h_val = val[hg];
+    if constexpr (TOPIC) h_top = topic[hg];
+    if (hg > 0) h_prev = key[hg - 1];
+  }
+  int32_t before0 = INT32_MIN;                    // key of the record before the workgroup's first tile
+  if (tid == 0 && tile0 > 0) before0 = key[tile0 * ST_TILE - 1];
+  __syncthreads();                                // the tables
+  uint32_t h_mask = 0;
+  if (halo_lane && hg >= 0)
+    h_mask = mask_of<VT, TOPIC>(P, s_tab, s_nan, h_val, h_top) | (uint32_t(hg > 0 && h_prev == h_key) << 7);
+
+  // per tile: count, then its matches compacted in LDS and written as one run into the super-tile's
+  // slot right away (the next tile's loads are in flight meanwhile)
+  int32_t* slot = out + tile0 * int64_t(ST_TILE) * K;
+  int64_t sum = 0;
+  for (int j = 0; j < ntl; j++) {                 // uniform
+    const int64_t base = (tile0 + j) * ST_TILE;
+    uint32_t packed[4];
+    masks_of_chunk<VT, TOPIC>(cur, P, s_tab, s_nan, packed, s_lut);
+#pragma unroll
+    for (int q = 0; q < ST_EPT / 4; q++) {
+      const int local = q * (ST_THREADS * 4) + tid * 4;
+      const v4i k = cur.k[q];
+      // the record before this lane's first: lane - 1's last (DPP wave_shr:1; lane 0: resolved by readers)
+      const int32_t kp = __builtin_amdgcn_update_dpp(INT32_MIN, k[3], 0x138, 0xF, 0xF, false);
+      const uint32_t same = uint32_t(lane > 0 && kp == k[0]) | (uint32_t(k[1] == k[0]) << 8) |
+                            (uint32_t(k[2] == k[1]) << 16) | (uint32_t(k[3] == k[2]) << 24);
+      uint32_t w = packed[q] | (same << 7);
+      const int64_t left = n - (base + local);    // records >= n match nothing
+      if (left < 4) w &= left <= 0 ? 0u : (0xFFFFFFFFu >> (8 * (4 - left)));
+      *reinterpret_cast<uint32_t*>(&s_mask[16 + local]) = w;
+      if (lane == 0) s_firstk[4 * q + wid] = k[0];
+      if (lane == 63) s_lastk[j & 1][4 * q + wid + 1] = k[3];
+    }
+    if (tid < 16) s_mask[tid] = halo_lane ? uint8_t(h_mask) : 0;
+    if (j == 0 && tid == 0) s_lastk[0][0] = before0;
+    // the chunk is consumed: the next tile's loads go out before the barrier, so a wave whose data
+    // came early does not hold its refill back until the slowest wave's has arrived
+#if ST_PLAIN_EARLY
+    if (j + 1 < ntl) load_tile<VT, TOPIC>(cur, key, val, topic, base + ST_TILE, n, tid);
+#endif
+    __syncthreads();                              // (A) the tile's image
+#if !ST_PLAIN_EARLY
+    if (j + 1 < ntl) load_tile<VT, TOPIC>(cur, key, val, topic, base + ST_TILE, n, tid);   // prefetch
+#endif
+
+    const int lb = ST_EPT * tid + 8;              // LDS byte of window record 0 (tile record 16 tid - 8)
+    uint64_t m8[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) m8[q] = *reinterpret_cast<const uint64_t*>(&s_mask[lb + 8 * q]);
+    uint32_t S = 0;
+#pragma unroll
+    for (int q = 0; q < 3; q++) S |= byte_bits(m8[q], 7) << (8 * q);
+    // the window's record at a multiple of 256 (if any): its same-key bit from the key tables
+    const int rb = ((ST_EPT * tid + 15) >> 8) << 8;
+    const int pb = rb - (ST_EPT * tid - 8);
+    if (pb >= 0 && pb < 24) {
+      const int m = rb >> 8;
+      const int32_t kb = m == 0 ? (j == 0 ? s_lastk[0][0] : s_lastk[(j - 1) & 1][16]) : s_lastk[j & 1][m];
+      S = (S & ~(1u << pb)) | (uint32_t(kb == s_firstk[m]) << pb);
+    }
+    uint32_t h = 0xFFFFFFFFu;
+#pragma unroll
+    for (int s = 0; s < K; s++) {
+      uint32_t B = 0;
+#pragma unroll
+      for (int q = 0; q < 3; q++) B |= byte_bits(m8[q], s) << (8 * q);
+      h &= B << (K - 1 - s);
+    }
+#pragma unroll
+    for (int d = 0; d < K - 1; d++) h &= S << d;
+    uint32_t hit = (h >> 8) & 0xFFFFu;
+    const int cnt = __popc(hit);
+    // the wave's exclusive prefix of the counts (<= 16: five bits) by ballots, no shuffle table
+    int before = 0, wtot = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+      const uint64_t m = __ballot((cnt >> b) & 1);
+      before += int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) << b;
+      wtot += __popcll(m) << b;
+    }
+    if (lane == 0) s_wsum[j & 1][wid] = wtot;
+    if (halo_lane) h_mask = s_mask[ST_TILE + tid];   // the next tile's halo: this tile's last records
+    __syncthreads();                              // (B) wave sums
+    int o = before, tot = 0;
+#pragma unroll
+    for (int w = 0; w < ST_THREADS / 64; w++) {
+      const int x = s_wsum[j & 1][w];
+      o += w < wid ? x : 0;
+      tot += x;
+    }
+    tot = __builtin_amdgcn_readfirstlane(tot);
+    while (hit) {
+      const int i = __ffs(hit) - 1;
+      hit &= hit - 1;
+      s_match[o++] = uint16_t(tid * ST_EPT + i);
+    }
+    __syncthreads();                              // (C) the tile's match list
+    const int words = tot * K;
+    const int32_t b32 = int32_t(base) - (K - 1);  // record index < 2^31 (checked by the launcher)
+    for (int w = tid; w < words; w += ST_THREADS) {
+      const int m = w / K, s = w - m * K;
+      slot[w] = b32 + int32_t(s_match[m]) + s;
+    }
+    slot += words;
+    sum += tot;
+  }
+  if (tid == 0) tile_count[blockIdx.x] = sum;
+}
+
 template <int K, class VT, bool TP, bool CH, int SUB>
 inline void launch_kts(const StencilLaunch& L, int64_t ntiles, hipStream_t st) {
   const int64_t nsuper = (ntiles + SUB - 1) / SUB;
+  if constexpr (!CH && K <= 7) {
+    if (!L.carry.hdr && L.plain) {
+      hipLaunchKernelGGL((stencil_plain_kernel<K, VT, TP, SUB>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
+                         static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles);
+      return;
+    }
+  }
   if (L.carry.hdr)
     hipLaunchKernelGGL((stencil_kernel<K, VT, TP, CH, true, SUB>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
                        L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles,
