@@ -34,7 +34,7 @@ hipError_t stencil_resolve_launch(const int32_t* key, const int32_t* out, int k,
                                   int64_t* pos, const StencilProgram* P, unsigned long long* sum, hipStream_t st);
 
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf);
-hipError_t nfa_wave_launch(const NfaArgs& A, int64_t nwg, hipStream_t st, hipFunction_t jf);
+hipError_t nfa_wave_launch(const NfaArgs& A, bool grouped, hipStream_t st, const JitModule* j);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
 hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
@@ -181,6 +181,8 @@ struct cep_session {
   bool jitg_tried = false;
   int64_t live_hwm = 0;                    // general path: most live runs any key held in the last batch
   bool wave = false;                       // general path: one key per wave (nfa_wave.h) for this pattern
+  bool grouped = false;                    // ... or four light keys per wave, outgrown keys on whole waves
+  DBuf heavy;                              // the grouped launch's outgrown segments
   bool g_any_err = false;                  // general path: some key of the last batch raised
   DBuf r_prof;                             // CEP_SESSION_PROFILE: per key segment {live max, evaluations, cycles}
   std::string jit_why;
@@ -238,7 +240,7 @@ bool getenv_flag(const char* name) {
 StencilCarry carry_args(const cep_session* s) {
   return StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), s->pat->prog.stencil.k - 1, s->halo_stamp,
                       int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->halo_base,
-                      s->hflags.as<unsigned long long>(), 0};
+                      s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), 0};
 }
 
 int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
@@ -272,13 +274,15 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int64_t ntiles = stencil_tiles(b->n);
   StencilLaunch L{key, col, topic, b->n, s->prog.as<StencilProgram>(), SP.k, SP.coltype, SP.use_topic, SP.chain,
                   s->slots.as<int32_t>(), tc, tc + ntiles + 1, s->counter.as<int64_t>(), s->out.as<int32_t>(),
-                  s->out_cap, s->total.as<int64_t>(), StencilCarry{}, !getenv_flag("KCEP_STENCIL_KEYED")};
+                  s->out_cap, s->total.as<int64_t>(), StencilCarry{}, !getenv_flag("KCEP_STENCIL_KEYED"), nullptr};
   if (s->carry) {                                // the keys' halos: read the previous, write the next
-    HIPCHECK(hipMemsetAsync(s->hflags.p, 0, 8, st));
+    // the batch's error flags: one of two words by the stamp's parity; the other one, cleared by this
+    // batch's scan kernel, serves the next batch (no memset launch per batch)
+    L.clear_flag = s->hflags.as<unsigned long long>() + (s->halo_stamp & 1);
     const char* dbg = getenv("KCEP_CARRY_DBG");   // A/B probes of the carry kernel's parts (tools/carry_probe.py)
     L.carry = StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), SP.k - 1, ++s->halo_stamp,
                            int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->base,
-                           s->hflags.as<unsigned long long>(), dbg ? atoi(dbg) : 0};
+                           s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), dbg ? atoi(dbg) : 0};
     s->halo_base = s->base;
     s->base += b->n;
   }
@@ -474,6 +478,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.base = 0;
   A.pos = rcarry ? X.pos : nullptr;               // carry: stream positions; runs ending in a tail are old
   A.emit_from = s->base;
+  A.chunk = runs_chunk(n);
   unsigned long long* ctl = s->ctl.as<unsigned long long>();
   A.nmatch = ctl;
   A.err_min = ctl + 1;
@@ -622,6 +627,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   cap.out_mult = std::max<int32_t>(1, int32_t(cap.out_mult * scale));
   const size_t sb = size_t(nseg) * 8;
   if (s->r_matches.ensure(sb) || s->r_words.ensure(sb) || s->r_out.ensure(sb) || s->r_err.ensure(sb) ||
+      s->heavy.ensure(size_t(nseg) * 4 + 4) ||
       s->r_errrec.ensure(sb) || s->r_carry.ensure(sb) || s->ents.ensure(sb) || s->moff.ensure(sb) || s->eoff.ensure(sb))
     return fail(CEP_E_HIP, "allocation failed");
   // first-allocation words of every key (NfaCaps) plus the events carried into the batch
@@ -666,11 +672,12 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.cpool_cap = s->carry ? s->cpool_words : 0;
     A.last_attempt = attempt >= kMaxRetry ? 1 : 0;     // then an overflowing key is handed back per key
     A.max_key_words = s->opts.max_key_words;
-    unsigned long long init[5] = {0, (unsigned long long)s->cpool_used, 0, 0, 0};
+    unsigned long long init[6] = {0, (unsigned long long)s->cpool_used, 0, 0, 0, 0};   // [5]: heavy count
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
-    A.wave_seg = nullptr;
-    if (s->wave) HIPCHECK(nfa_wave_launch(A, nseg, st, s->jitg ? s->jitg->nfa_wave : nullptr));
+    A.heavy = s->heavy.as<int32_t>();
+    A.heavy_n = reinterpret_cast<int32_t*>(ctl + 5);
+    if (s->wave) HIPCHECK(nfa_wave_launch(A, s->grouped, st, s->jitg.get()));
     else HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
     if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
     timed = true;
@@ -860,9 +867,9 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   }
   if (carry && (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN)) {   // per key two halo slots, none written yet
     s->carry = true;
-    if (s->halo.ensure(size_t(opts->max_keys) * sizeof(HaloHdr)) || s->hflags.ensure(8) ||
+    if (s->halo.ensure(size_t(opts->max_keys) * sizeof(HaloHdr)) || s->hflags.ensure(16) ||
         s->hpos.ensure(size_t(opts->max_keys) * 2 * size_t(std::max(1, P.stencil.k - 1)) * 8) ||
-        hipMemset(s->halo.p, 0, size_t(opts->max_keys) * sizeof(HaloHdr)) || hipMemset(s->hflags.p, 0, 8))
+        hipMemset(s->halo.p, 0, size_t(opts->max_keys) * sizeof(HaloHdr)) || hipMemset(s->hflags.p, 0, 16))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
   } else if (carry && path == CEP_PATH_RUNS) {    // per key a carried tail, none yet (runs.hip)
     s->carry = true;
@@ -895,6 +902,11 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   else if (opts->flags & CEP_SESSION_WAVE_NFA) wave = true;
   else if (env_wave) wave = env_wave[0] == '1';
   s->wave = P.general_ok && wave && wave_ok(P.dev);
+  // KCEP_NFA_GROUPED=1: four keys per wave, keys past GROUP_RUNS live runs re-run on whole waves
+  // (C4: 8.8 vs 8.5-8.9 ms -- the grouped kernel takes the light keys in 5.5 ms, the outgrown keys
+  // then need 2.7 ms more on whole waves, profiles/r03_ab_c4_grouped.jsonl); default: one key per wave
+  const char* env_grp = getenv("KCEP_NFA_GROUPED");
+  s->grouped = env_grp && env_grp[0] == '1';
   const char* env_jit = getenv("KCEP_JIT");
   s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
   if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels
@@ -908,7 +920,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 
 void cep_session_close(cep_session* s) {
   if (!s) return;
-  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->h_key, &s->h_valid,
+  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->heavy, &s->h_key, &s->h_valid,
                   &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
@@ -1132,7 +1144,7 @@ int cep_collect(cep_session* s, cep_matches* o) {
     std::vector<int64_t> pos_host;
     if (s->carry) {
       unsigned long long hf = 0;
-      HIPCHECK(hipMemcpy(&hf, s->hflags.p, 8, hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(&hf, s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), 8, hipMemcpyDeviceToHost));
       if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
       if (hf & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
       if (hf & 4) return fail(CEP_E_RUN_CAPACITY, "chain carry batch: more runs completing in one tile than its match space");
@@ -1496,6 +1508,7 @@ int cep_state_clear(cep_session* s) {
   s->base = 0;
   if (halo_session(s)) {
     HIPCHECK(hipMemset(s->halo.p, 0, size_t(s->opts.max_keys) * sizeof(HaloHdr)));
+    HIPCHECK(hipMemset(s->hflags.p, 0, 16));       // both error-flag words (by stamp parity)
     s->halo_stamp = 0;
     return CEP_OK;
   }

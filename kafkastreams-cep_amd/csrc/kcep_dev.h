@@ -152,7 +152,8 @@ struct NfaArgs {
   int32_t wave_agg;               // wave kernel: bit 0 the pattern folds / reads / copies aggregates (rounds
                                   // check for runs sharing a sequence), bit 1 it has SequenceMatchers
   int32_t last_attempt;           // 1: no pool regrowth follows -- an overflowing key reports CEP_E_RUN_CAPACITY
-  const int32_t* wave_seg;        // wave kernel: the segment of each workgroup (nullptr: workgroup = segment)
+  int32_t* heavy;                 // grouped wave kernel: segments that outgrew their group (nfa_wave.h) ...
+  int32_t* heavy_n;               // ... and their count (zeroed before the launch)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY
   unsigned long long* err_any;    // set when any key reports an exception (the host reads res_err only then)
 };
@@ -182,7 +183,15 @@ struct RunsArgs {
   // runs ending or failing at a position < emit_from were handled by an earlier batch (not emitted)
   const int64_t* pos;
   int64_t emit_from;
+  int32_t chunk;                  // items per wave (a power of two <= RUNS_CHUNK; runs_chunk)
 };
 constexpr int RUNS_MAX_SEGS = 8;
+constexpr int RUNS_CHUNK = 1024;
+KCEP_HD inline int32_t runs_chunk(int64_t items) {
+  int32_t c = RUNS_CHUNK;
+  while (c > 128 && items < int64_t(c) * 3072) c >>= 1;          // 3 waves on each of 1024 SIMDs
+  return c;
+}
+
 
 }  // namespace kcep

@@ -171,6 +171,7 @@ struct StencilLaunch {
   int64_t* total;                 // device: number of matches
   StencilCarry carry;             // halo != nullptr: carry session
   int plain;                      // plain stencil (no carry, no chain, k <= 7): the keyless kernel (KCEP_STENCIL_KEYED=1: off)
+  unsigned long long* clear_flag; // carry: the next batch's error-flag word, zeroed by the scan kernel (or null)
 };
 
 // compile.cpp

@@ -44,6 +44,7 @@
 #include "interp.h"
 #include "nfa_dev.h"
 #include "nfa_wave.h"
+#include "jit.h"
 
 namespace kcep {
 
@@ -51,13 +52,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nf
   nfa_kernel_body(A);
 }
 
-// one key per wave, one queued run per lane (nfa_wave.h); patterns without aggregates
+// one key per wave, one queued run per lane (nfa_wave.h); AGG: patterns with aggregates or
+// SequenceMatchers.  GL = 64: every key on a whole wave; GL = GROUP_LANES: four keys per wave, the
+// keys that outgrow their group re-run on a whole wave by nfa_wave_heavy_kernel
+template <bool AGG, int GL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_kernel(NfaArgs A) {
-  nfa_wave_body<false>(A);
+  nfa_wave_body<AGG, GL>(A);
 }
-// ... and patterns with aggregates or SequenceMatchers
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_agg_kernel(NfaArgs A) {
-  nfa_wave_body<true>(A);
+template <bool AGG>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_heavy_kernel(NfaArgs A) {
+  nfa_wave_heavy<AGG>(A);
 }
 
 // ---- segments, scans, output compaction, carry commit ----
@@ -150,16 +154,33 @@ hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf) {
   return hipGetLastError();
 }
 
-// jf: the pattern's compiled wave kernel, nullptr for the built-in one.  nwg workgroups of one wave.
-hipError_t nfa_wave_launch(const NfaArgs& A, int64_t nwg, hipStream_t st, hipFunction_t jf) {
-  if (nwg <= 0) return hipSuccess;
-  if (jf) {
-    NfaArgs a = A;
-    void* args[] = {&a};
-    return hipModuleLaunchKernel(jf, unsigned(nwg), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+// The wave kernels over A.nseg key segments: grouped (four keys per wave, then the outgrown keys on
+// whole waves; A.heavy_n zeroed by the caller) or one key per wave.  j: the pattern's compiled
+// kernels (null: the built-in interpreting ones).
+hipError_t nfa_wave_launch(const NfaArgs& A, bool grouped, hipStream_t st, const JitModule* j) {
+  if (A.nseg <= 0) return hipSuccess;
+  NfaArgs a = A;
+  void* args[] = {&a};
+  constexpr int NG = 64 / GROUP_LANES;
+  if (!grouped) {
+    if (j) return hipModuleLaunchKernel(j->nfa_wave, unsigned(A.nseg), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+    if (A.wave_agg) hipLaunchKernelGGL((nfa_wave_kernel<true, 64>), dim3(unsigned(A.nseg)), dim3(64), 0, st, A);
+    else hipLaunchKernelGGL((nfa_wave_kernel<false, 64>), dim3(unsigned(A.nseg)), dim3(64), 0, st, A);
+    return hipGetLastError();
   }
-  if (A.wave_agg) hipLaunchKernelGGL(nfa_wave_agg_kernel, dim3(unsigned(nwg)), dim3(64), 0, st, A);
-  else hipLaunchKernelGGL(nfa_wave_kernel, dim3(unsigned(nwg)), dim3(64), 0, st, A);
+  const unsigned grid = unsigned((A.nseg + NG - 1) / NG);
+  const unsigned hgrid = unsigned(A.nseg < 4096 ? A.nseg : 4096);   // persistent over the heavy list
+  if (j) {
+    hipError_t e = hipModuleLaunchKernel(j->nfa_wave16, grid, 1, 1, 64, 1, 1, 0, st, args, nullptr);
+    return e != hipSuccess ? e : hipModuleLaunchKernel(j->nfa_heavy, hgrid, 1, 1, 64, 1, 1, 0, st, args, nullptr);
+  }
+  if (A.wave_agg) {
+    hipLaunchKernelGGL((nfa_wave_kernel<true, GROUP_LANES>), dim3(grid), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(nfa_wave_heavy_kernel<true>, dim3(hgrid), dim3(64), 0, st, A);
+  } else {
+    hipLaunchKernelGGL((nfa_wave_kernel<false, GROUP_LANES>), dim3(grid), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(nfa_wave_heavy_kernel<false>, dim3(hgrid), dim3(64), 0, st, A);
+  }
   return hipGetLastError();
 }
 

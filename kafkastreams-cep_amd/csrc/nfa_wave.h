@@ -35,33 +35,86 @@ constexpr int WAVE = 64;
 #define WAVE_ARENA 2048                    // LDS words per key workspace (KCEP_WAVE_ARENA A/B: 0 = pool only)
 #endif
 #ifndef WAVE_PRIV
-#define WAVE_PRIV 16                       // LDS words per lane for its private run list + operation log
+#define WAVE_PRIV 0                        // LDS words per lane for its private run list + operation log
 #endif                                     // (KCEP_WAVE_PRIV A/B; 0 = in the pool)
+#ifndef GROUP_LANES
+#define GROUP_LANES 16                     // lanes per key of the grouped kernel (4 keys per wave)
+#endif
+#ifndef GROUP_ARENA
+#define GROUP_ARENA 1024                   // LDS words per key workspace of the grouped kernel (KCEP_GROUP_ARENA A/B)
+#endif
+#ifndef GROUP_RUNS
+#define GROUP_RUNS 32                      // a key of the grouped kernel with more live runs moves to a whole wave
+#endif
+
+// The lanes of one key: GL consecutive lanes of the wave (GL = 64: the whole wave, one key per
+// workgroup; GL = 16: four keys per wave).  Ballots, broadcasts and scans stay inside the group, so
+// the keys of one wave never exchange anything; their lanes merely share the instruction stream,
+// which is what a latency-bound key leaves idle.
+template <int GL>
+struct Grp {
+  int gl;                                  // lane within the group
+  int base;                                // the group's first lane in the wave
+  __device__ __forceinline__ uint64_t ballot(bool x) const {
+    const uint64_t b = __ballot(x);
+    if constexpr (GL == 64) return b;
+    else return (b >> base) & ((1ull << GL) - 1);
+  }
+  template <class T>
+  __device__ __forceinline__ T bcast(T v, int src = 0) const { return __shfl(v, src, GL); }
+  // exclusive prefix of v over the group's lanes, and the group total
+  __device__ __forceinline__ int excl_scan(int v, int& total) const {
+    int x = v;
+    for (int d = 1; d < GL; d <<= 1) {
+      const int y = __shfl_up(x, d, GL);
+      if (gl >= d) x += y;
+    }
+    total = __shfl(x, GL - 1, GL);
+    return x - v;
+  }
+  __device__ __forceinline__ int max_all(int v) const {
+    for (int d = GL / 2; d > 0; d >>= 1) { const int o = __shfl_xor(v, d, GL); v = o > v ? o : v; }
+    return v;
+  }
+};
+
+// A hand-off between lanes of the wave (the workgroup is one wave): a wavefront performs its
+// memory operations in program order, so only the compiler must not move them across it.  No
+// s_barrier, which the grouped kernel could not take anyway: its keys leave loops at different
+// times.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // the key's shared workspace descriptor (LDS); lanes keep register copies in their Lane
+template <int GL>
 struct WaveShared {
   int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm, *aggs;
   int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs, seqcap;
   int64_t nmatch;
   unsigned long long pool_words;   // the key's pool words (every lane allocates for the key)
   int32_t err, overflow, cap_hit;
-  int32_t* logp[WAVE];
-  int32_t logn[WAVE], errc[WAVE];
+  int32_t* logp[GL];
+  int32_t logn[GL], errc[GL];
   int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
   int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
-  int32_t *arena, arena_used;      // the key's LDS arena and its bump pointer (re-allocations go there first)
+  int32_t *arena, arena_used, arena_cap;   // the key's LDS arena, its bump pointer (re-allocations go there first), size
   // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
-  int32_t ms_slot[WAVE], ms_e[WAVE], ms_pv[WAVE], ms_cnt[WAVE], ms_done[WAVE], ms_err[WAVE];
+  int32_t ms_slot[GL], ms_e[GL], ms_pv[GL], ms_cnt[GL], ms_done[GL], ms_err[GL];
+  int32_t conf[2 * GL];            // stateful rounds: each lane's run sequence, whether it wrote it
 };
 
-__device__ __forceinline__ void ws_to_lane(Lane& l, const WaveShared& w) {
+template <class W>
+__device__ __forceinline__ void ws_to_lane(Lane& l, const W& w) {
   l.nodes = w.nodes; l.heap = w.heap; l.qa = w.qa; l.qb = w.qb; l.fq = w.fq; l.out = w.out; l.hwm = w.hwm;
   l.aggs = w.aggs; l.seqcap = w.seqcap;
   l.heapcap = w.heapcap; l.heap_top = w.heap_top; l.qa_cap = w.qa_cap; l.qb_cap = w.qb_cap; l.fq_cap = w.fq_cap;
   l.qlen = w.qlen; l.outcap = w.outcap; l.out_top = w.out_top; l.nhwm = w.nhwm; l.runs = w.runs;
   l.nmatch = w.nmatch; l.err = w.err; l.overflow = w.overflow; l.cap_hit = w.cap_hit;
 }
-__device__ __forceinline__ void lane_to_ws(WaveShared& w, const Lane& l) {
+template <class W>
+__device__ __forceinline__ void lane_to_ws(W& w, const Lane& l) {
   w.nodes = l.nodes; w.heap = l.heap; w.qa = l.qa; w.qb = l.qb; w.fq = l.fq; w.out = l.out; w.hwm = l.hwm;
   w.aggs = l.aggs; w.seqcap = l.seqcap;
   w.heapcap = l.heapcap; w.heap_top = l.heap_top; w.qa_cap = l.qa_cap; w.qb_cap = l.qb_cap; w.fq_cap = l.fq_cap;
@@ -69,26 +122,17 @@ __device__ __forceinline__ void lane_to_ws(WaveShared& w, const Lane& l) {
   w.nmatch = l.nmatch; w.err = l.err; w.overflow = l.overflow; w.cap_hit = l.cap_hit;
 }
 
-__device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
-  int x = v;
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const int y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
-  total = __shfl(x, WAVE - 1);
-  return x - v;
-}
-
 // A shared array of `cap` words (used up to `used`) re-allocated at >= need words: lane 0 draws it
-// from the pool, the wave copies.  Returns the new array (nullptr: pool exhausted -> w.overflow).
+// from the pool, the group copies.  Returns the new array (nullptr: pool exhausted -> w.overflow).
 // lds_ok: the array may move into the key's LDS arena (not the match output, read after the kernel)
-__device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared& w, int32_t* a, int32_t& cap, int64_t used,
-                                                int64_t need, int lane, bool lds_ok = true) {
+template <int GL>
+__device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int32_t* a, int32_t& cap, int64_t used,
+                                                int64_t need, const Grp<GL>& g, bool lds_ok = true) {
   int64_t nc = int64_t(cap) * 2;
   if (nc < need) nc = need;
-  __syncthreads();
-  if (lane == 0) {
-    if (lds_ok && w.arena_used + nc <= WAVE_ARENA) {   // room left in the LDS arena
+  wave_sync();
+  if (g.gl == 0) {
+    if (lds_ok && w.arena_used + nc <= w.arena_cap) {   // room left in the LDS arena
       w.grown = w.arena + w.arena_used;
       w.arena_used += int32_t((nc + 3) & ~int64_t(3));
     } else {
@@ -96,29 +140,31 @@ __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared& w, int32_t*
     }
     if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
   }
-  __syncthreads();
+  wave_sync();
   int32_t* na = w.grown;
   if (!na) return nullptr;
-  for (int64_t i = lane; i < used; i += WAVE) na[i] = a[i];
+  for (int64_t i = g.gl; i < used; i += GL) na[i] = a[i];
   cap = int32_t(nc);
-  __syncthreads();
+  wave_sync();
   return na;
 }
 
-__device__ __forceinline__ bool wave_heap_reserve(Lane& l, WaveShared& w, int64_t need_top, int lane) {
+template <int GL>
+__device__ __forceinline__ bool wave_heap_reserve(Lane& l, WaveShared<GL>& w, int64_t need_top, const Grp<GL>& g) {
   if (need_top <= w.heapcap) return true;
   int32_t cap = w.heapcap;
-  int32_t* na = wave_regrow(l, w, w.heap, cap, w.heap_top, need_top, lane);
+  int32_t* na = wave_regrow(l, w, w.heap, cap, w.heap_top, need_top, g);
   if (!na) return false;
-  if (lane == 0) { w.heap = na; w.heapcap = cap; }
-  __syncthreads();
+  if (g.gl == 0) { w.heap = na; w.heapcap = cap; }
+  wave_sync();
   return true;
 }
 
 // the round's buffer operations, none of which can see another's effect (see the header): branch
 // walks with atomic refcounts and the existence checks, then the current record's nodes.  Returns
 // the reference exception of the first failing operation in queue order (CEP_OK if none).
-__device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int lane, int r, int nact) {
+template <int GL>
+__device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int r) {
   const auto& P = KCEP_PROG(l);
   const int ns = P.nslots;
   // (1) existence of every 5-arg put's predecessor node; branch walks (refs++)
@@ -141,18 +187,18 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
       }
     }
   }
-  const uint64_t em = __ballot(my_err != 0);
-  if (em) return __shfl(my_err, __builtin_ctzll(em));
+  const uint64_t em = g.ballot(my_err != 0);
+  if (em) return g.bcast(my_err, __builtin_ctzll(em));
   // (2) the current record's nodes: the last 3-arg put of a node overwrites, later 5-arg puts append
   int before = 0, total = 0;
-  before = wave_excl_scan(l.log_n, lane, total);
-  for (int s = lane; s < ns; s += WAVE) { w.lastp3[s] = -1; w.scnt[s] = 0; }
-  __syncthreads();
+  before = g.excl_scan(l.log_n, total);
+  for (int s = g.gl; s < ns; s += GL) { w.lastp3[s] = -1; w.scnt[s] = 0; }
+  wave_sync();
   for (int k = 0; k < l.log_n; k++) {
     const int32_t* o = l.log + k * WL;
     if ((o[0] & 0xFF) == WOP_PUT3) atomicMax(&w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)], before + k);
   }
-  __syncthreads();
+  wave_sync();
   auto survives = [&](const int32_t* o, int gi) {
     const int kind = o[0] & 0xFF;
     if (kind == WOP_BRANCH || kind == WOP_AGG) return false;
@@ -165,16 +211,16 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
     if (survives(o, before + k)) { atomicAdd(&w.scnt[slot_of(l, (o[0] >> 8) & 0xFF)], 1); npred++; }
   }
   int all = 0;
-  wave_excl_scan(npred, lane, all);
-  __syncthreads();
-  if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(PW) * all, lane)) return CEP_OK;   // w.overflow
-  if (lane == 0) {
+  g.excl_scan(npred, all);
+  wave_sync();
+  if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(PW) * all, g)) return CEP_OK;   // w.overflow
+  if (g.gl == 0) {
     int top = w.heap_top;
     for (int s = 0; s < ns; s++)
       if (w.scnt[s]) { w.sblk[s] = top; top += PW * w.scnt[s]; }
     w.heap_top = top;
   }
-  __syncthreads();
+  wave_sync();
   l.heap = w.heap;
   l.heapcap = w.heapcap;
   for (int s = 0; s < ns; s++) {                             // uniform loop over the record's slots
@@ -186,7 +232,7 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
       if (survives(o, before + k) && slot_of(l, (o[0] >> 8) & 0xFF) == s) mine++;
     }
     int tot = 0;
-    const int ex = wave_excl_scan(mine, lane, tot);
+    const int ex = g.excl_scan(mine, tot);
     int j = 0;
     for (int k = 0; k < l.log_n; k++) {
       const int32_t* o = l.log + k * WL;
@@ -202,7 +248,7 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
       l.heap[p + 4] = l.heap[ver];
       l.heap[p + 5] = l.heap[ver + 1];
     }
-    if (lane == 0) {
+    if (g.gl == 0) {
       int32_t* nd = node(l, s, r);
       const int last = w.sblk[s] + PW * (cnt - 1);
       if (w.lastp3[s] >= 0 || !exists(nd)) {                 // overwritten by a 3-arg put, or created: refs 1
@@ -214,7 +260,6 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
       }
     }
   }
-  (void)nact;
   return CEP_OK;
 }
 
@@ -226,14 +271,16 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared& w, int 
 // read-only node each lane picks its predecessor in parallel; the walks standing at a changing node
 // are stepped by lane 0 in final-run order -- every walk that will ever reach that node is there,
 // since none is left above the frontier.  The result is the sequential construction's.
-__device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int lane, int flen) {
+template <int GL>
+__device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int flen) {
   const auto& P = KCEP_PROG(l);
+  const int lane = g.gl;
   const int64_t pos = l.A->base + l.g;
   const int maxp = l.nev + 1;                                  // one node per event at most
-  for (int base = 0; base < flen; base += WAVE) {
-    const int nact = flen - base < WAVE ? flen - base : WAVE;
+  for (int base = 0; base < flen; base += GL) {
+    const int nact = flen - base < GL ? flen - base : GL;
     const bool act = lane < nact;
-    if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(WAVE) * 2 * maxp, lane)) return false;
+    if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(GL) * 2 * maxp, g)) return false;
     l.heap = w.heap;
     l.heapcap = w.heapcap;
     int32_t* paths = w.heap + w.heap_top;                      // scratch above the heap top
@@ -247,8 +294,7 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
     }
     for (;;) {
       const bool live = !done && !my_err;
-      int fr = live ? e : -1;
-      for (int d = 32; d > 0; d >>= 1) { const int o = __shfl_xor(fr, d); fr = o > fr ? o : fr; }
+      const int fr = g.max_all(live ? e : -1);
       if (fr < 0) break;
       const bool at = live && e == fr;
       bool mut = false;
@@ -263,11 +309,11 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
           else { pv = l.heap[p]; slot = l.heap[p + 1]; e = l.heap[p + 2]; }
         }
       }
-      const uint64_t mm = __ballot(at && !my_err && mut);
+      const uint64_t mm = g.ballot(at && !my_err && mut);
       if (mm) {                                                // changing nodes: lane 0, in walk order
         w.ms_slot[lane] = slot; w.ms_e[lane] = e; w.ms_pv[lane] = pv; w.ms_cnt[lane] = cnt; w.ms_done[lane] = done;
         w.ms_err[lane] = my_err;
-        __syncthreads();
+        wave_sync();
         if (lane == 0) {
           for (uint64_t m = mm; m; m &= m - 1) {
             const int j = __builtin_ctzll(m);
@@ -293,30 +339,30 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
             else { w.ms_pv[j] = l.heap[p]; w.ms_slot[j] = l.heap[p + 1]; w.ms_e[j] = l.heap[p + 2]; }
           }
         }
-        __syncthreads();
+        wave_sync();
         if ((mm >> lane) & 1) {
           slot = w.ms_slot[lane]; e = w.ms_e[lane]; pv = w.ms_pv[lane]; cnt = w.ms_cnt[lane];
           done = w.ms_done[lane]; my_err = w.ms_err[lane];
         }
       }
     }
-    const uint64_t em = __ballot(my_err != 0);
+    const uint64_t em = g.ballot(my_err != 0);
     if (em) {                                                  // the reference throws at the first failing walk
-      const int code = __shfl(my_err, __builtin_ctzll(em));
+      const int code = g.bcast(my_err, __builtin_ctzll(em));
       if (lane == 0) w.err = code;
-      __syncthreads();
+      wave_sync();
       return true;
     }
     // the matches, in final-run order: [pos lo, pos hi, cnt, (name, pos lo, pos hi) x cnt]
     int total = 0;
     const int words = act ? 3 + 3 * cnt : 0;
-    const int off = wave_excl_scan(words, lane, total);
+    const int off = g.excl_scan(words, total);
     if (w.out_top + total > w.outcap) {
       int32_t cap = w.outcap;
-      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, lane, false);
+      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, g, false);
       if (!na) return false;
       if (lane == 0) { w.out = na; w.outcap = cap; }
-      __syncthreads();
+      wave_sync();
     }
     if (act) {
       int32_t* o = w.out + w.out_top + off;
@@ -330,9 +376,9 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
         o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
       }
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0) { w.out_top += total; w.nmatch += nact; }
-    __syncthreads();
+    wave_sync();
   }
   return true;
 }
@@ -341,7 +387,8 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared& w, int la
 // order.  Without a conflict (wave_round_conflict) no two lanes write one (sequence, state) -- a lane
 // writes its own run's sequence and sequences it created -- so every lane applies its own entries,
 // placeholders numbered as the run words are (rb).  The table first grows to the largest sequence.
-__device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared& w, int lane, int rb) {
+template <int GL>
+__device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int rb) {
   const int ns = KCEP_PROG(l).nstates;
   auto real = [&](int sq) { return sq < -1 ? rb + (-sq - 2) + 1 : sq; };
   int need = -1;
@@ -349,17 +396,17 @@ __device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared& w, int lane
     const int32_t* o = l.log + k * WL;
     if ((o[0] & 0xFF) == WOP_AGG) { const int sq = real(o[1]); need = sq > need ? sq : need; }
   }
-  for (int d = 32; d > 0; d >>= 1) { const int x = __shfl_xor(need, d); need = x > need ? x : need; }
+  need = g.max_all(need);
   if (need < 0) return true;
   if (need >= w.seqcap) {
     int32_t capw = w.seqcap * ns * 3;
     const int64_t used = int64_t(capw);
-    int32_t* na = wave_regrow(l, w, w.aggs, capw, used, (int64_t(need) + 1) * ns * 3, lane);
+    int32_t* na = wave_regrow(l, w, w.aggs, capw, used, (int64_t(need) + 1) * ns * 3, g);
     if (!na) return false;
-    for (int64_t i = used + lane; i < capw; i += WAVE) na[i] = 0;       // the new rows: every state null
-    __syncthreads();
-    if (lane == 0) { w.aggs = na; w.seqcap = capw / (ns * 3); }
-    __syncthreads();
+    for (int64_t i = used + g.gl; i < capw; i += GL) na[i] = 0;       // the new rows: every state null
+    wave_sync();
+    if (g.gl == 0) { w.aggs = na; w.seqcap = capw / (ns * 3); }
+    wave_sync();
   }
   l.aggs = w.aggs;
   l.seqcap = w.seqcap;
@@ -369,7 +416,7 @@ __device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared& w, int lane
     int32_t* e = l.aggs + (int64_t(real(o[1])) * ns + ((o[0] >> 8) & 0xFF)) * 3;
     e[0] = (o[0] >> 16) & 0xFF; e[1] = o[2]; e[2] = o[3];
   }
-  __syncthreads();
+  wave_sync();
   return true;
 }
 
@@ -378,18 +425,20 @@ __device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared& w, int lane
 // and one of them wrote it -- the later run would have read the earlier one's fold (NFA.java:319-321,
 // 362-369) -- or, with SequenceMatchers, a run died before others read partial sequences (its
 // removePattern, NFA.java:142-143, changes the buffer they walk).
-// conf: 2 x WAVE words of LDS (each lane's run sequence, whether it wrote it)
-__device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf, int lane, bool act, int seq,
+// conf: 2 x GL words of LDS (each lane's run sequence, whether it wrote it)
+template <int GL>
+__device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf, const Grp<GL>& g, bool act, int seq,
                                                     uint64_t dmask) {
   if ((l.A->wave_agg & 2) && dmask) return true;
   if (!(l.A->wave_agg & 1)) return false;
+  const int lane = g.gl;
   conf[lane] = act ? seq : INT32_MIN;
-  conf[WAVE + lane] = act && l.ov_own;
-  __syncthreads();
+  conf[GL + lane] = act && l.ov_own;
+  wave_sync();
   bool c = false;
-  for (int j = 0; j < lane && act; j++) c = c || (conf[j] == seq && (conf[WAVE + j] || l.ov_own));
-  __syncthreads();
-  return __ballot(c) != 0;
+  for (int j = 0; j < lane && act; j++) c = c || (conf[j] == seq && (conf[GL + j] || l.ov_own));
+  wave_sync();
+  return g.ballot(c) != 0;
 }
 
 // profiling kernels (KCEP_PHASES): lane 0's clocks per phase of the record loop -- record setup,
@@ -405,28 +454,28 @@ __device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf
 // AGG: the pattern reads or writes aggregates / reads partial sequences (DevProgram, abi.cpp
 // wave_stateful): the round machinery for them (conflict checks, the sequential re-evaluation,
 // applying the logged aggregate writes) is compiled in only then.
-template <bool AGG>
-__device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
-  __shared__ WaveShared w;
-  __shared__ int32_t s_conf[AGG ? 2 * WAVE : 1];
-  const int lane = threadIdx.x;
-  const int seg = A.wave_seg ? A.wave_seg[blockIdx.x] : int(blockIdx.x);
-  if (seg >= A.nseg) return;
+// One key (segment `seg`) on the GL lanes of group gp (w, s_arena, s_priv: the group's LDS).
+// Returns false when a grouped key (GL < 64) outgrew its group (more than GROUP_RUNS live runs):
+// nothing of it was committed and it is re-run on a whole wave (nfa_wave_heavy).
+template <bool AGG, int GL>
+__device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL>& gp, WaveShared<GL>& w,
+                                         int32_t* s_arena, int arena_words, int32_t*& s_priv) {
+  const int lane = gp.gl;
   Lane l;
   int ok = 1;
-  __shared__ __attribute__((aligned(16))) int32_t s_arena[WAVE_ARENA];   // the key's hot workspace, if it fits
   if (lane == 0) {
-    ok = key_begin(l, A, seg, s_arena, WAVE_ARENA) ? 1 : 0;
+    ok = key_begin(l, A, seg, s_arena, arena_words) ? 1 : 0;
     if (ok) {
       lane_to_ws(w, l);
       w.pool_words = l.pool_words;
       w.arena = s_arena;
-      w.arena_used = l.arena_used >= 0 ? (l.arena_used + 3) & ~3 : WAVE_ARENA;
+      w.arena_cap = arena_words;
+      w.arena_used = l.arena_used >= 0 ? (l.arena_used + 3) & ~3 : arena_words;
     }
   }
-  ok = __shfl(ok, 0);
-  if (!ok) return;
-  __syncthreads();
+  ok = gp.bcast(ok);
+  if (!ok) return true;
+  wave_sync();
   if (lane != 0) {
     l.A = &A; l.P = A.P;
     l.seg0 = A.seg_start[seg];
@@ -435,35 +484,33 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   }
   l.wpool = &w.pool_words;
   // every lane: the key's fixed shape (lane 0's key_begin set it)
-  l.C = __shfl(l.C, 0);
-  l.nev = __shfl(l.nev, 0);
-  l.evw = __shfl(l.evw, 0);
-  l.cev = reinterpret_cast<const int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.cev), 0));
-  l.tq = reinterpret_cast<int32_t*>(__shfl(reinterpret_cast<uintptr_t>(l.tq), 0));
-  l.tq_cap = __shfl(l.tq_cap, 0);
-  l.runs_delta = __shfl(l.runs_delta, 0);
+  l.C = gp.bcast(l.C);
+  l.nev = gp.bcast(l.nev);
+  l.evw = gp.bcast(l.evw);
+  l.cev = reinterpret_cast<const int32_t*>(gp.bcast(reinterpret_cast<uintptr_t>(l.cev)));
+  l.tq = reinterpret_cast<int32_t*>(gp.bcast(reinterpret_cast<uintptr_t>(l.tq)));
+  l.tq_cap = gp.bcast(l.tq_cap);
+  l.runs_delta = gp.bcast(l.runs_delta);
   l.pool_words = 0;
   l.rec_out_top = 0; l.rec_nmatch = 0;
   l.slm = 0; l.sle = 0; l.flen = 0; l.tlen = 0;
   ws_to_lane(l, w);
   // private run lists and operation logs: written by every evaluation and read back by the commit
-  // and the queue placement, so they start in LDS (a lane's list that outgrows its slice moves to the
-  // pool like any other array)
-  __shared__ int32_t* s_priv;
+  // and the queue placement.  In the pool by default (2 runs per lane, growing on demand): a slice of
+  // LDS per lane (WAVE_PRIV words) cut the kernel's HBM writes but cost occupancy, C4 9.39 vs 8.34 ms
+  // (profiles/r03_ab_s5.jsonl)
   const int q0 = 2;
 #if WAVE_PRIV > 0
-  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
   constexpr int priv_stride = WAVE_PRIV, log0 = (WAVE_PRIV - 4 * q0) / WL;
   static_assert(WAVE_PRIV % 4 == 0 && log0 >= 1, "WAVE_PRIV: room for the run list and one log entry");
-  if (lane == 0) s_priv = s_priv_lds;
 #else
   constexpr int priv_stride = 4 * (q0 + q0 * WL / 4 + 4), log0 = q0;
   if (lane == 0) {
-    s_priv = pool_alloc(l, int64_t(WAVE) * priv_stride);
+    s_priv = pool_alloc(l, int64_t(GL) * priv_stride);
     if (!s_priv) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
   }
 #endif
-  __syncthreads();
+  wave_sync();
   const auto& P = KCEP_PROG(l);
   const int ns = P.nslots;
   Frame fr[MAXD];
@@ -484,28 +531,29 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   }
   l.wtop = &w.heap_top;
   for (int i = 0; i < l.L && !w.err && !w.overflow; i++) {
+    if (GL < WAVE && w.qlen > GROUP_RUNS) return false;          // too many runs for the group: a whole wave
     const int r = l.C + i;
     const int64_t g = l.seg0 + i;
     l.r = r;
     l.g = g;
     KWP_MARK(t_rec);
     ws_to_lane(l, w);
-    for (int x = lane; x < ns * NW; x += WAVE) {                 // the record's buffer nodes: none yet
+    for (int x = lane; x < ns * NW; x += GL) {                   // the record's buffer nodes: none yet
       const int k = x & (NW - 1);
       l.nodes[(int64_t(r) * ns) * NW + x] = (k == 1 || k == 2) ? -1 : 0;
     }
     if (proc) {
-      if (!record_admitted(l, g)) { __syncthreads(); continue; }
-      for (int k = lane; k < w.qlen; k += WAVE) l.qa[4 * k] &= ~(1 << 17);   // isIgnored not serialised (Q3)
+      if (!record_admitted(l, g)) { wave_sync(); continue; }
+      for (int k = lane; k < w.qlen; k += GL) l.qa[4 * k] &= ~(1 << 17);   // isIgnored not serialised (Q3)
     }
-    __syncthreads();
+    wave_sync();
     eval_event_only(l);
     const int n = w.qlen;
     evals += n;
     if (lane == 0) { l.rec_out_top = w.out_top; l.rec_nmatch = w.nmatch; }
     int qn = 0, flen = 0;
     KWP_ADD(0, t_rec);
-    for (int base = 0; base < n && !w.err && !w.overflow; base += WAVE) {
+    for (int base = 0; base < n && !w.err && !w.overflow; base += GL) {
       const int my = base + lane;
       const bool act = my < n;
       Run run{0, 0, 0, 0};
@@ -514,7 +562,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         run = Run{x.x, x.y, x.z, x.w};
       }
       const int top0 = w.heap_top;
-      const int nact = n - base < WAVE ? n - base : WAVE;
+      const int nact = n - base < GL ? n - base : GL;
       bool good = true, seqd = false;
       int jj = 0;                                              // sequential mode: the lane evaluating
       uint64_t emask = 0, dmask = 0;
@@ -526,7 +574,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         // immediate ones, on the key's shared state, lanes in queue order (one call site of evaluate)
         const bool me = seqd ? lane == jj : act;
         if (seqd) {
-          __syncthreads();
+          wave_sync();
           if (me) ws_to_lane(l, w);
         } else {
           l.heap = w.heap; l.heapcap = w.heapcap;
@@ -544,39 +592,39 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
             if (e) w.err = e;
             if (o) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
           }
-          __syncthreads();
+          wave_sync();
           if (w.err || w.overflow || ++jj >= nact) break;
           continue;
         }
-        const bool grow = __ballot(l.wgrow) != 0;
-        const bool pool_out = __ballot(l.overflow && !l.wgrow) != 0;
+        const bool grow = gp.ballot(l.wgrow) != 0;
+        const bool pool_out = gp.ballot(l.overflow && !l.wgrow) != 0;
         if (pool_out) {                                        // a private list could not grow
           if (lane == 0) w.overflow = 1;
-          const uint64_t ch = __ballot(l.cap_hit);
+          const uint64_t ch = gp.ballot(l.cap_hit);
           if (lane == 0 && ch) w.cap_hit = 1;
           break;
         }
         if (grow) {
-          __syncthreads();
+          wave_sync();
           if (lane == 0) w.heap_top = top0;
-          __syncthreads();
-          if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, lane)) break;
+          wave_sync();
+          if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, gp)) break;
           continue;
         }
         err_lane = act && !good && l.err;
         const bool dead = act && good && l.tlen == 0;
-        emask = __ballot(err_lane);
-        dmask = __ballot(dead);
+        emask = gp.ballot(err_lane);
+        dmask = gp.ballot(dead);
         // a conflict is checked before the errors: a run may throw on a state an earlier run of the
         // round would have folded first
-        if (AGG && A.wave_agg && wave_round_conflict(l, s_conf, lane, act, run.seq, dmask)) {
+        if (AGG && A.wave_agg && wave_round_conflict(l, w.conf, gp, act, run.seq, dmask)) {
           seqd = true;
           l.tlen = 0; l.log_n = 0; l.nph = 0;                  // the parallel pass is discarded
           continue;
         }
         break;
       }
-      __syncthreads();
+      wave_sync();
       KWP_ADD(1, t_ev);
       if (w.overflow) break;
       // commit in queue order
@@ -585,14 +633,14 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         ws_to_lane(l, w);
         if (w.err) { KWP_ADD(2, t_cm); break; }
       } else if (!emask && !dmask) {
-        const int e = wave_commit_parallel(l, w, lane, r, nact);
+        const int e = wave_commit_parallel(l, w, gp, r);
         if (lane == 0 && e) w.err = e;
-        __syncthreads();
+        wave_sync();
       } else {
         w.logp[lane] = l.log;
         w.logn[lane] = l.log_n;
         w.errc[lane] = err_lane ? l.err : 0;
-        __syncthreads();
+        wave_sync();
         if (lane == 0) {                                       // the reference's order, sequentially
           ws_to_lane(l, w);
           l.err = 0; l.overflow = 0;
@@ -614,7 +662,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
           }
           lane_to_ws(w, l);
         }
-        __syncthreads();
+        wave_sync();
         ws_to_lane(l, w);
       }
       KWP_ADD(2, t_cm);
@@ -622,8 +670,8 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       // NFA.runs: the round's placeholders in queue order
       KWP_MARK(t_pl);
       int nrun = 0;
-      const int rb = w.runs + wave_excl_scan(l.nph, lane, nrun);
-      if (AGG && (A.wave_agg & 1) && !seqd && !wave_apply_aggs(l, w, lane, rb)) {   // the round's folds and copies
+      const int rb = w.runs + gp.excl_scan(l.nph, nrun);
+      if (AGG && (A.wave_agg & 1) && !seqd && !wave_apply_aggs(l, w, gp, rb)) {   // the round's folds and copies
         if (lane == 0) w.overflow = 1;
         break;
       }
@@ -634,23 +682,23 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
         if (is_fwd_final(l, y->x & 0xFF, (y->x >> 8) & 0xFF)) nf++; else nq++;
       }
       int tf = 0, tq = 0;
-      const int ef = wave_excl_scan(nf, lane, tf), eq = wave_excl_scan(nq, lane, tq);
-      __syncthreads();
+      const int ef = gp.excl_scan(nf, tf), eq = gp.excl_scan(nq, tq);
+      wave_sync();
       if (lane == 0) w.runs += nrun;
       // room in the next queue and the final list
       if (qn + tq > w.qb_cap) {
         int32_t capw = w.qb_cap * 4;
-        int32_t* na = wave_regrow(l, w, w.qb, capw, int64_t(qn) * 4, int64_t(qn + tq) * 4, lane);
+        int32_t* na = wave_regrow(l, w, w.qb, capw, int64_t(qn) * 4, int64_t(qn + tq) * 4, gp);
         if (!na) break;
         if (lane == 0) { w.qb = na; w.qb_cap = capw / 4; }
       }
       if (flen + tf > w.fq_cap) {
         int32_t capw = w.fq_cap * 4;
-        int32_t* na = wave_regrow(l, w, w.fq, capw, int64_t(flen) * 4, int64_t(flen + tf) * 4, lane);
+        int32_t* na = wave_regrow(l, w, w.fq, capw, int64_t(flen) * 4, int64_t(flen + tf) * 4, gp);
         if (!na) break;
         if (lane == 0) { w.fq = na; w.fq_cap = capw / 4; }
       }
-      __syncthreads();
+      wave_sync();
       int a = qn + eq, b = flen + ef;
       for (int t = 0; t < l.tlen; t++) {
         const int4 y = reinterpret_cast<const int4*>(l.tq)[t];
@@ -659,7 +707,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       }
       qn += tq;
       flen += tf;
-      __syncthreads();
+      wave_sync();
       KWP_ADD(3, t_pl);
     }
     if (w.err) { err_rec = A.base + g; break; }
@@ -670,29 +718,70 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
       const int32_t c = w.qa_cap; w.qa_cap = w.qb_cap; w.qb_cap = c;
       w.qlen = qn;
     }
-    __syncthreads();
+    wave_sync();
     KWP_MARK(t_mc);
-    if (flen && !wave_emit_matches(l, w, lane, flen)) {
+    if (flen && !wave_emit_matches(l, w, gp, flen)) {
       if (lane == 0) w.overflow = 1;
     }
-    __syncthreads();
+    wave_sync();
     KWP_ADD(4, t_mc);
     if (lane == 0 && !w.err && !w.overflow) {
       ws_to_lane(l, w);
       if (proc && !record_hwm(l, g)) l.overflow = 1;
       lane_to_ws(w, l);
     }
-    __syncthreads();
+    wave_sync();
     if (w.err) { err_rec = A.base + g; break; }
     live_max = w.qlen > live_max ? w.qlen : live_max;
   }
-  __syncthreads();
+  wave_sync();
   if (lane == 0) {
     ws_to_lane(l, w);
     l.pool_words = int64_t(w.pool_words);
     l.wpool = nullptr;
     l.wave = 0;
     key_end(l, A, seg, err_rec, live_max, evals, t0);
+  }
+  return true;
+}
+
+// The key segments of a batch, GL lanes per key: workgroup b takes segments b * (64 / GL) ... (one
+// per group).  GL < 64 (light keys): a key whose live runs outgrow its group is appended to the
+// heavy list (A.heavy / A.heavy_n) for nfa_wave_heavy.
+template <bool AGG, int GL>
+__device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
+  constexpr int NG = WAVE / GL;
+  constexpr int ARENA = (GL == WAVE ? WAVE_ARENA : GROUP_ARENA) & ~3;   // LDS words of each key's hot workspace
+  __shared__ WaveShared<GL> ws[NG];
+  __shared__ __attribute__((aligned(16))) int32_t s_arena[NG * ARENA + 4];
+  __shared__ int32_t* s_priv[NG];
+  const Grp<GL> gp{int(threadIdx.x) & (GL - 1), int(threadIdx.x) & ~(GL - 1)};
+  const int grp = int(threadIdx.x) / GL;
+  const int seg = int(blockIdx.x) * NG + grp;
+  if (seg >= A.nseg) return;
+#if WAVE_PRIV > 0
+  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
+  if (gp.gl == 0) s_priv[grp] = s_priv_lds + gp.base * WAVE_PRIV;
+#endif
+  if (!wave_key<AGG, GL>(A, seg, gp, ws[grp], s_arena + grp * ARENA, ARENA, s_priv[grp]) && gp.gl == 0)
+    A.heavy[atomicAdd(A.heavy_n, 1)] = seg;
+}
+
+// The heavy list of a grouped launch, one key per workgroup-wave (persistent over the list).
+template <bool AGG>
+__device__ __forceinline__ void nfa_wave_heavy(const NfaArgs& A) {
+  __shared__ WaveShared<WAVE> w;
+  __shared__ __attribute__((aligned(16))) int32_t s_arena[WAVE_ARENA];
+  __shared__ int32_t* s_priv;
+#if WAVE_PRIV > 0
+  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
+  s_priv = s_priv_lds;
+#endif
+  const Grp<WAVE> gp{int(threadIdx.x), 0};
+  const int nh = *A.heavy_n;
+  for (int i = blockIdx.x; i < nh; i += gridDim.x) {
+    wave_key<AGG, WAVE>(A, A.heavy[i], gp, w, s_arena, WAVE_ARENA, s_priv);
+    wave_sync();
   }
 }
 

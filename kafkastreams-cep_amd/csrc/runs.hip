@@ -258,8 +258,8 @@ __global__ void rc_gc_copy(int64_t* __restrict__ rtab, int64_t nkeys, const int6
 
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
 
-static unsigned runs_blocks(int64_t items) {
-  const int64_t waves = (items + RUNS_CHUNK - 1) / RUNS_CHUNK;
+static unsigned runs_blocks(int64_t items, int32_t chunk) {
+  const int64_t waves = (items + chunk - 1) / chunk;
   return unsigned((waves * 64 + RT - 1) / RT);
 }
 
@@ -269,9 +269,9 @@ hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hi
   if (jf) {
     RunsArgs a = A;
     void* args[] = {&a, &flag, &end_of};
-    return hipModuleLaunchKernel(jf, runs_blocks(A.n), 1, 1, RT, 1, 1, 0, st, args, nullptr);
+    return hipModuleLaunchKernel(jf, runs_blocks(A.n, A.chunk), 1, 1, RT, 1, 1, 0, st, args, nullptr);
   }
-  hipLaunchKernelGGL(runs_sim, dim3(runs_blocks(A.n)), dim3(RT), 0, st, A, flag, end_of);
+  hipLaunchKernelGGL(runs_sim, dim3(runs_blocks(A.n, A.chunk)), dim3(RT), 0, st, A, flag, end_of);
   return hipGetLastError();
 }
 
@@ -358,11 +358,12 @@ hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted
     return exclusive_scan(len, nm, ent_off, total, scan_tmp, st);
   }
   WriteArgs W{R, sorted, nm, ent_off, match_record, match_key, ent_off_out, ent_name, ent_record};
+  W.R.chunk = runs_chunk(nm);
   if (jf) {
     void* args[] = {&W};
-    return hipModuleLaunchKernel(jf, runs_blocks(nm), 1, 1, RT, 1, 1, 0, st, args, nullptr);
+    return hipModuleLaunchKernel(jf, runs_blocks(nm, W.R.chunk), 1, 1, RT, 1, 1, 0, st, args, nullptr);
   }
-  hipLaunchKernelGGL(runs_write, dim3(runs_blocks(nm)), dim3(RT), 0, st, W);
+  hipLaunchKernelGGL(runs_write, dim3(runs_blocks(nm, W.R.chunk)), dim3(RT), 0, st, W);
   return hipGetLastError();
 }
 

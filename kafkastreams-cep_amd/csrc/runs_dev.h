@@ -83,10 +83,12 @@ __device__ __forceinline__ bool wave_any(bool x) { return __builtin_amdgcn_ballo
 // then the one consuming edge (BEGIN / TAKE, with the stage's folds,
 // :319-321) or the one recursion edge applies.
 //
-// A wave owns a chunk of RUNS_CHUNK items (start records, or completed runs to
+// A wave owns a chunk of A.chunk items (start records, or completed runs to
 // write); a lane whose run ends takes the next item of the chunk at the next
-// step, so the wave does not idle behind its longest run.
-constexpr int RUNS_CHUNK = 1024;
+// step, so the wave does not idle behind its longest run.  Large batches take
+// RUNS_CHUNK items per wave (fewer, longer-lived waves: r02 sweep 1.86 ms at
+// 1024 vs 2.59 at 128 on C3); a batch too small to give every SIMD three waves
+// that way takes smaller chunks (runs_chunk).
 
 struct RunResult {
   int64_t end;        // record where the run consumed its last stage, -1 none
@@ -244,7 +246,7 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
   __shared__ int32_t s_end[RT / 64][RUNS_CHUNK];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
-  const int64_t i0 = wave * RUNS_CHUNK, i1 = i0 + RUNS_CHUNK < A.n ? i0 + RUNS_CHUNK : A.n;
+  const int64_t i0 = wave * A.chunk, i1 = i0 + A.chunk < A.n ? i0 + A.chunk : A.n;
   uint32_t* const myseg = s_seg[threadIdx.x];
   if (i0 < A.n) {
     int64_t seg_item = -1;                                      // the lane's current start record
@@ -309,7 +311,7 @@ __device__ __forceinline__ void put_entry(const Tab& T, const WriteArgs& W, int6
 template <class Tab>
 __device__ __forceinline__ void runs_write_body(const Tab& T, const WriteArgs& W) {
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
-  const int64_t i0 = wave * RUNS_CHUNK, i1 = i0 + RUNS_CHUNK < W.nm ? i0 + RUNS_CHUNK : W.nm;
+  const int64_t i0 = wave * W.R.chunk, i1 = i0 + W.R.chunk < W.nm ? i0 + W.R.chunk : W.nm;
   if (i0 >= W.nm) return;
   run_engine(
       T, W.R, i0, i1,

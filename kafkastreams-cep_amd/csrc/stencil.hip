@@ -34,7 +34,7 @@ int64_t stencil_tiles(int64_t n) { return (n + ST_TILE - 1) / ST_TILE; }
 // the total (a batch has at most 2^31 / 16384 super-tiles: <= 128 per thread;
 // the loads go out 8 at a time)
 __global__ __launch_bounds__(1024) void tile_scan(const int64_t* __restrict__ cnt, int64_t nt, int64_t* __restrict__ pre,
-                                                  int64_t* __restrict__ total) {
+                                                  int64_t* __restrict__ total, unsigned long long* __restrict__ clear_flag) {
   __shared__ int64_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t per = (nt + 1023) / 1024, a = tid * per, b = a + per < nt ? a + per : nt;
@@ -80,6 +80,7 @@ __global__ __launch_bounds__(1024) void tile_scan(const int64_t* __restrict__ cn
     }
   }
   if (tid == 1023) *total = run;
+  if (tid == 0 && clear_flag) *clear_flag = 0;    // carry: the next batch's error-flag word (the kernel is done)
 }
 
 // small batches (processor flushes): the scan and the gather in one workgroup, one launch instead of
@@ -88,7 +89,8 @@ constexpr int SMALL_FINISH = 1024;
 __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __restrict__ slots,
                                                              const int64_t* __restrict__ cnt, int64_t nt, int k,
                                                              int32_t* __restrict__ out, int64_t out_cap, int sub,
-                                                             int64_t* __restrict__ total) {
+                                                             int64_t* __restrict__ total,
+                                                             unsigned long long* __restrict__ clear_flag) {
   __shared__ int64_t s_pre[SMALL_FINISH + 1];
   __shared__ int64_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -105,6 +107,7 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
   for (int w = 0; w < wid; w++) run += s_w[w];
   s_pre[tid] = run;
   if (tid == 1023) { s_pre[SMALL_FINISH] = run + c; *total = run + c; }
+  if (tid == 0 && clear_flag) *clear_flag = 0;    // carry: the next batch's error-flag word (the kernel is done)
   __syncthreads();
   for (int64_t t = wid; t < nt; t += 16) {                 // one wave per super-tile
     const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
@@ -136,6 +139,7 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   // null events: timing off (cep_session_set_timing), no event packets in the stream
   if (L.n <= 0) {
     hipError_t e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
+    if (e == hipSuccess && L.clear_flag) e = hipMemsetAsync(L.clear_flag, 0, 8, st);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
     return e == hipSuccess ? hipMemsetAsync(L.total, 0, sizeof(int64_t), st) : e;
   }
@@ -148,10 +152,10 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e != hipSuccess) return e;
   if (nsuper <= SMALL_FINISH) {
     hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
-                       L.out_cap, sub, L.total);
+                       L.out_cap, sub, L.total, L.clear_flag);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total);
+  hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
   hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre, L.k,
                      L.out, L.out_cap, sub);
   return hipGetLastError();

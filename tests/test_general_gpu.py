@@ -260,3 +260,24 @@ def test_c4_heavy_keys(lane_nfa):
     got = product_matches(s, s.collect())
     assert got == want and len(want) > 0
     assert s.live_run_hwm() > 128
+
+
+@pytest.mark.parametrize("grouped", ["0", "1"], ids=["whole_wave", "grouped"])
+@pytest.mark.parametrize("name,mk,vmax,gen", CASES, ids=[c[0] for c in CASES])
+def test_grouped_and_whole_wave_kernels(name, mk, vmax, gen, grouped, monkeypatch):
+    """The wave kernel with four keys per wave (16 lanes each) and with one key per wave: keys of
+    every size in one batch -- light ones stay in their group, keys past GROUP_RUNS live runs are
+    re-run from scratch on a whole wave (nfa_wave.h nfa_wave_heavy) -- against the oracle."""
+    monkeypatch.setenv("KCEP_NFA_GROUPED", grouped)
+    rng = np.random.default_rng(hash(name) % 977)
+    if name in ("c4_any", "any_any"):       # skip-till-any: live runs multiply with every record (Q6)
+        lens = np.concatenate([rng.integers(1, 6, 200), rng.integers(10, 15, 60)])
+    else:
+        lens = np.concatenate([rng.integers(1, 6, 200), rng.integers(20, 40, 40), [60, 80]])
+    rng.shuffle(lens)
+    key = np.repeat(np.arange(len(lens), dtype=np.int32), lens)
+    val = (gen(rng, len(key)) if gen is not None else rng.integers(0, vmax, len(key))).astype(np.int32)
+    ir = mk().to_ir(PL.I32)
+    want, got, oerr, gerr = run_both(ir, O.MODE_PROCESSOR, key, [val], [1], lane_nfa=False)
+    assert gerr == oerr
+    assert got == want and len(want) > 0
