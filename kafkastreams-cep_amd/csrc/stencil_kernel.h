@@ -925,7 +925,11 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
     const int32_t b32 = int32_t(base) - (K - 1);  // record index < 2^31 (checked by the launcher)
     for (int w = tid; w < words; w += ST_THREADS) {
       const int m = w / K, s = w - m * K;
+#ifdef ST_NT_STORE
+      __builtin_nontemporal_store(b32 + int32_t(s_match[m]) + s, slot + w);
+#else
       slot[w] = b32 + int32_t(s_match[m]) + s;
+#endif
     }
     slot += words;
     sum += tot;
