@@ -757,7 +757,9 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 // reader from two 17-entry LDS key tables.  The window test is bit-parallel over the thread's 24
 // window records (8 of history + its 16): hit(p) = AND_s B_s(p-K+1+s) AND_d same(p-d), d < K-1.
 // Against the keyed kernel: 4 B instead of 5 B of LDS traffic per record written and 3 instead of
-// 9 LDS reads per window, ~12 KB of LDS per workgroup instead of 25 KB, no 24-key register window.
+// 9 LDS reads per window, ~5 KB of LDS per workgroup instead of 25 KB, no 24-key register window;
+// each thread stores its own matches (no compaction through LDS).
+
 // load_chunk for a tile that lies wholly inside the batch (uniform branch): uniform tile base
 // pointers and 32-bit lane offsets, so every load is one saddr + voffset instruction
 template <class VT, bool TOPIC>
@@ -800,7 +802,6 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
   __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];   // record r at r + 16
   __shared__ int32_t s_lastk[2][17];   // [tile & 1][m]: key of tile record 256m - 1 (m >= 1); [0][0]: before tile 0
   __shared__ int32_t s_firstk[16];     // key of tile record 256m
-  __shared__ uint16_t s_match[ST_TILE];
   __shared__ int32_t s_wsum[2][ST_THREADS / 64];
   __shared__ uint8_t s_tab[64];
   __shared__ uint8_t s_lut[256];
@@ -834,8 +835,8 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
   if (halo_lane && hg >= 0)
     h_mask = mask_of<VT, TOPIC>(P, s_tab, s_nan, h_val, h_top) | (uint32_t(hg > 0 && h_prev == h_key) << 7);
 
-  // per tile: count, then its matches compacted in LDS and written as one run into the super-tile's
-  // slot right away (the next tile's loads are in flight meanwhile)
+  // per tile: count, then its matches written as one run into the super-tile's slot right away (the
+  // next tile's loads are in flight meanwhile)
   int32_t* slot = out + tile0 * int64_t(ST_TILE) * K;
   int64_t sum = 0;
   for (int j = 0; j < ntl; j++) {                 // uniform
@@ -915,21 +916,17 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
       tot += x;
     }
     tot = __builtin_amdgcn_readfirstlane(tot);
+    const int words = tot * K;
+    const int32_t b32 = int32_t(base) - (K - 1);  // record index < 2^31 (checked by the launcher)
+    // each thread stores its own matches at their place in the tile's run of the slot (no LDS
+    // compaction and no third barrier: L2 merges the run's lines; 147.7-150.2 vs 150.8-152.1 us,
+    // profiles/r03_ab_stencil_direct_store.jsonl)
     while (hit) {
       const int i = __ffs(hit) - 1;
       hit &= hit - 1;
-      s_match[o++] = uint16_t(tid * ST_EPT + i);
-    }
-    __syncthreads();                              // (C) the tile's match list
-    const int words = tot * K;
-    const int32_t b32 = int32_t(base) - (K - 1);  // record index < 2^31 (checked by the launcher)
-    for (int w = tid; w < words; w += ST_THREADS) {
-      const int m = w / K, s = w - m * K;
-#ifdef ST_NT_STORE
-      __builtin_nontemporal_store(b32 + int32_t(s_match[m]) + s, slot + w);
-#else
-      slot[w] = b32 + int32_t(s_match[m]) + s;
-#endif
+      int32_t* d = slot + int64_t(o++) * K;
+#pragma unroll
+      for (int s = 0; s < K; s++) d[s] = b32 + tid * ST_EPT + i + s;
     }
     slot += words;
     sum += tot;
