@@ -227,7 +227,9 @@ def main():
             # 8 B/event in (key + i32 value); CSR out: 20 B/match + 12 B/entry
             algo_bytes = 8.0 * n + 20.0 * n_matches + 12.0 * n_ent
         if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
-            roof_ms, roof_kernel = avg_kernel_ms, "stencil_kernel"
+            # the plain kernel runs strict fixed-length patterns of k <= 7 (C2); the keyed one chains (C5)
+            plain = sess.path == N.PATH_STENCIL and pat.info.stencil_k <= 7 and os.environ.get("KCEP_STENCIL_KEYED") != "1"
+            roof_ms, roof_kernel = avg_kernel_ms, "stencil_plain_kernel" if plain else "stencil_kernel"
         else:
             # these paths write their CSR in later launches (runs_write / nfa_compact), so the bytes
             # are divided by the whole step's device time (HIP events around cep_push_batch)
