@@ -218,17 +218,22 @@ def main():
                 exch["gathered_matches"] = int(len(merged["match_record"]))
 
     if rank == 0:
+        plain = (sess.path == N.PATH_STENCIL and pat.info.stencil_k <= 7
+                 and os.environ.get("KCEP_STENCIL_KEYED") != "1")
         if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
             k = pat.info.stencil_k
             algo_bytes = 8.0 * n + 4.0 * k * n_matches          # 8 B/event + 4k B/match
+            # the plain kernel writes one int per match (its first record); stencil_gather writes
+            # the k-int rows: the kernel's own algorithmic bytes are 8 B/event + 4 B/match
+            kernel_bytes = 8.0 * n + 4.0 * n_matches if plain else algo_bytes
         else:
             out = sess.collect(raise_on_error=False)
             n_ent = len(out["ent_record"])
             # 8 B/event in (key + i32 value); CSR out: 20 B/match + 12 B/entry
             algo_bytes = 8.0 * n + 20.0 * n_matches + 12.0 * n_ent
+            kernel_bytes = algo_bytes
         if sess.path in (N.PATH_STENCIL, N.PATH_CHAIN):
             # the plain kernel runs strict fixed-length patterns of k <= 7 (C2); the keyed one chains (C5)
-            plain = sess.path == N.PATH_STENCIL and pat.info.stencil_k <= 7 and os.environ.get("KCEP_STENCIL_KEYED") != "1"
             roof_ms, roof_kernel = avg_kernel_ms, "stencil_plain_kernel" if plain else "stencil_kernel"
         else:
             # these paths write their CSR in later launches (runs_write / nfa_compact), so the bytes
@@ -236,7 +241,7 @@ def main():
             roof_ms = sum(batch_ms) / len(batch_ms)
             roof_kernel = "whole cep_push_batch (" + ("runs_sim + sort + runs_write" if sess.path == N.PATH_RUNS
                                                        else "nfa_kernel + compaction") + ")"
-        achieved = algo_bytes / (roof_ms * 1e-3) / 1e9
+        achieved = kernel_bytes / (roof_ms * 1e-3) / 1e9
         value = tot_events * args.steps / t_max
         line = {
             "metric": METRIC if args.config == "c2" else f"events/sec (whole node), {C['desc']}",
@@ -259,7 +264,8 @@ def main():
                        "forced_path": args.force_path, "nfa_kernel": args.nfa_kernel},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
-                         "kernel": roof_kernel, "kernel_ms": roof_ms, "algo_bytes_per_launch": algo_bytes},
+                         "kernel": roof_kernel, "kernel_ms": roof_ms, "algo_bytes_per_launch": kernel_bytes,
+                         "algo_bytes_per_step": algo_bytes},
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",
         }

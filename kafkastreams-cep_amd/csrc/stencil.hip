@@ -16,14 +16,23 @@ hipError_t stencil_count_k8(const StencilLaunch& L, hipStream_t st);
 // Tiles' match slots -> one contiguous output in record order (the order
 // context.forward sees them, CEPProcessor.java:148): tile t's matches start at
 // the exclusive prefix of the tile counts.  One workgroup per tile.
+// expand: the slot holds one int per match (its first record; the plain kernel's stages are
+// consecutive records), written out as k ints
 __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
                                                       const int64_t* __restrict__ pre, int k, int32_t* __restrict__ out,
-                                                      int64_t out_cap, int sub) {
+                                                      int64_t out_cap, int sub, int expand) {
   const int64_t t = blockIdx.x;                  // super-tile
   const int64_t words = cnt[t] * k, dst = pre[t] * k;
   if (pre[t] + cnt[t] > out_cap) return;
   const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
-  for (int64_t w = threadIdx.x; w < words; w += 256) out[dst + w] = src[w];
+  if (expand) {
+    for (int64_t w = threadIdx.x; w < words; w += 256) {
+      const int64_t m = w / k;
+      out[dst + w] = src[m] + int32_t(w - m * k);
+    }
+  } else {
+    for (int64_t w = threadIdx.x; w < words; w += 256) out[dst + w] = src[w];
+  }
 }
 
 // ---- launcher ------------------------------------------------------------
@@ -90,7 +99,8 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
                                                              const int64_t* __restrict__ cnt, int64_t nt, int k,
                                                              int32_t* __restrict__ out, int64_t out_cap, int sub,
                                                              int64_t* __restrict__ total,
-                                                             unsigned long long* __restrict__ clear_flag) {
+                                                             unsigned long long* __restrict__ clear_flag,
+                                                             int expand) {
   __shared__ int64_t s_pre[SMALL_FINISH + 1];
   __shared__ int64_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -114,7 +124,14 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
     if (pre + m > out_cap) continue;
     const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
     int32_t* dst = out + pre * k;
-    for (int64_t w = lane; w < m * k; w += 64) dst[w] = src[w];
+    if (expand) {
+      for (int64_t w = lane; w < m * k; w += 64) {
+        const int64_t q = w / k;
+        dst[w] = src[q] + int32_t(w - q * k);
+      }
+    } else {
+      for (int64_t w = lane; w < m * k; w += 64) dst[w] = src[w];
+    }
   }
 }
 
@@ -150,14 +167,16 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e == hipSuccess) e = stencil_count(L, st);
   if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
+  // the plain kernel (stencil_kernel.h launch_kts) left one int per match in the slots
+  const int expand = L.plain && !L.carry.hdr && !L.chain && L.k <= 7;
   if (nsuper <= SMALL_FINISH) {
     hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
-                       L.out_cap, sub, L.total, L.clear_flag);
+                       L.out_cap, sub, L.total, L.clear_flag, expand);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
   hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre, L.k,
-                     L.out, L.out_cap, sub);
+                     L.out, L.out_cap, sub, expand);
   return hipGetLastError();
 }
 

@@ -636,8 +636,9 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
     }
   }
 
-  // ================= write phase: the super-tile's matches, compacted, into its slot =================
-  int32_t* const s_match = s_key;
+  // ================= write phase: the super-tile's matches into its slot =================
+  // each thread stores its own matches at their place in the tile's run (record order; per record
+  // oldest start first), K entries each: no compaction through LDS, no barrier
   int32_t* slot = out + tile0 * int64_t(ST_TILE) * K;     // super-tile s_super's slot
   if constexpr (CHAIN && CARRY) {                  // halo runs can exceed a tile's match space: fail the batch
     int64_t sum = 0;
@@ -655,7 +656,6 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
     for (int j = 0; j < SUB; j++) sum += total[j];
     tile_count[s_super] = sum;
   }
-  uint8_t* const s_aux = s_mask;                  // chain: start distance | consumed stages << 2
 #pragma unroll
   for (int j = 0; j < SUB; j++) {
     if (j < ntl) {
@@ -673,6 +673,19 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         for (int d = 1; d < K; d++) any |= ce.e[d];
         any &= 0xFFFF00u;
         if constexpr (CARRY) any |= hb[j] << 8;
+        // one match: completing record rj, started d records before, consumed-stage mask cm; ho: the
+        // segment's records before rj when the run started in the halo (3: it did not)
+        auto put = [&](int32_t rj, uint32_t d, uint32_t cm, int ho) {
+          int32_t* dst = slot + int64_t(o++) * K;
+#pragma unroll
+          for (int s = 0; s < K; s++) {                // skipped optional stages: -1
+            const int rel = -int32_t(d) + __popc(cm & ((1u << s) - 1));
+            int32_t rec = ((cm >> s) & 1) ? rj + rel : -1;
+            if constexpr (CARRY)                       // a halo record: -(1 + records before the segment)
+              if (((cm >> s) & 1) && ho != 3 && rel < -ho) rec = -(1 + (-ho - rel));
+            dst[s] = rec;
+          }
+        };
         while (any) {                                // record order; per record oldest start first
           const int p = __ffs(any) - 1;
           any &= any - 1;
@@ -696,18 +709,15 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
               ho = so;
             }
           }
+          const int32_t rj = int32_t(base + tid * ST_EPT + (p - 8));
           for (int d = K - 1; d >= 1; d--) {
             if ((hends >> d) & 1) {
-              s_match[o] = int32_t(base + tid * ST_EPT + (p - 8));
-              s_aux[o] = uint8_t(d | (hcms[d] << 2) | (ho << 6));
-              o++;
+              put(rj, uint32_t(d), hcms[d], int(ho));
             } else if ((ce.e[d] >> p) & 1) {
               uint32_t cm;
               ChainEnds<K> one;
               one.run(cw, d, p, &cm);
-              s_match[o] = int32_t(base + tid * ST_EPT + (p - 8));
-              s_aux[o] = uint8_t(d | (cm << 2) | (3u << 6));
-              o++;
+              put(rj, uint32_t(d), cm, 3);
             }
           }
         }
@@ -716,33 +726,16 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         while (h) {
           const int i = __ffs(h) - 1;
           h &= h - 1;
-          if constexpr (CARRY) s_aux[o] = uint8_t((bneed[j] >> (4 * i)) & 0xF);
-          s_match[o++] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+          const int32_t rj = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+          int32_t* dst = slot + int64_t(o++) * K;
+          int need = 0;
+          if constexpr (CARRY) need = int((bneed[j] >> (4 * i)) & 0xF);
+#pragma unroll
+          for (int s = 0; s < K; s++)                  // carry: halo stages -(1 + records before the segment)
+            dst[s] = s < need ? -(1 + (need - s)) : rj - (K - 1) + s;
         }
       }
-      __syncthreads();
-      const int words = total[j] * K;              // K ints per match, contiguous across the tile
-      for (int w = tid; w < words; w += ST_THREADS) {
-        const int m = w / K, s = w - m * K;
-        int32_t rec;
-        if constexpr (CHAIN) {                      // skipped optional stages: -1
-          const uint32_t aux = s_aux[m], d = aux & 3u, cm = (aux >> 2) & 15u;
-          const int rel = -int32_t(d) + __popc(cm & ((1u << s) - 1));
-          rec = ((cm >> s) & 1) ? s_match[m] + rel : -1;
-          if constexpr (CARRY) {                     // a halo record: -(1 + records before the segment)
-            const int ho = int(aux >> 6);
-            if (((cm >> s) & 1) && ho != 3 && rel < -ho) rec = -(1 + (-ho - rel));
-          }
-        } else if constexpr (CARRY) {                // halo stages: -(1 + records before the segment)
-          const int need = s_aux[m];
-          rec = s < need ? -(1 + (need - s)) : s_match[m] - (K - 1) + s;
-        } else {
-          rec = s_match[m] - (K - 1) + s;
-        }
-        slot[w] = rec;
-      }
-      slot += words;
-      __syncthreads();
+      slot += total[j] * K;
     }
   }
 }
@@ -916,19 +909,17 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
       tot += x;
     }
     tot = __builtin_amdgcn_readfirstlane(tot);
-    const int words = tot * K;
     const int32_t b32 = int32_t(base) - (K - 1);  // record index < 2^31 (checked by the launcher)
     // each thread stores its own matches at their place in the tile's run of the slot (no LDS
     // compaction and no third barrier: L2 merges the run's lines; 147.7-150.2 vs 150.8-152.1 us,
-    // profiles/r03_ab_stencil_direct_store.jsonl)
+    // profiles/r03_ab_stencil_direct_store.jsonl).  ONE int per match -- its first record: the
+    // stages' records are consecutive here, so stencil_gather expands them to the K-int output
     while (hit) {
       const int i = __ffs(hit) - 1;
       hit &= hit - 1;
-      int32_t* d = slot + int64_t(o++) * K;
-#pragma unroll
-      for (int s = 0; s < K; s++) d[s] = b32 + tid * ST_EPT + i + s;
+      slot[o++] = b32 + tid * ST_EPT + i;
     }
-    slot += words;
+    slot += tot;
     sum += tot;
   }
   if (tid == 0) tile_count[blockIdx.x] = sum;
