@@ -16,22 +16,28 @@ hipError_t stencil_count_k8(const StencilLaunch& L, hipStream_t st);
 // Tiles' match slots -> one contiguous output in record order (the order
 // context.forward sees them, CEPProcessor.java:148): tile t's matches start at
 // the exclusive prefix of the tile counts.  One workgroup per tile.
-// expand: the slot holds one int per match (its first record; the plain kernel's stages are
-// consecutive records), written out as k ints
+// The slot of super-tile t holds one int per match -- the plain kernel: its first record (the
+// stages are consecutive records); the keyed kernel: its completing record, with an aux byte per
+// match after the super-tile's sub x 4096 ints (stencil_row) -- written out as k-int rows.
+struct SlotFormat {
+  int k, plain, chain, carry;
+  __device__ __forceinline__ int32_t entry(const int32_t* src, const uint8_t* aux, int64_t m, int s) const {
+    if (plain) return src[m] + s;
+    return stencil_row(src[m], k > 1 ? aux[m] : 0u, s, k, chain, carry);
+  }
+};
 __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
-                                                      const int64_t* __restrict__ pre, int k, int32_t* __restrict__ out,
-                                                      int64_t out_cap, int sub, int expand) {
+                                                      const int64_t* __restrict__ pre, int32_t* __restrict__ out,
+                                                      int64_t out_cap, int sub, SlotFormat F) {
   const int64_t t = blockIdx.x;                  // super-tile
+  const int k = F.k;
   const int64_t words = cnt[t] * k, dst = pre[t] * k;
   if (pre[t] + cnt[t] > out_cap) return;
   const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
-  if (expand) {
-    for (int64_t w = threadIdx.x; w < words; w += 256) {
-      const int64_t m = w / k;
-      out[dst + w] = src[m] + int32_t(w - m * k);
-    }
-  } else {
-    for (int64_t w = threadIdx.x; w < words; w += 256) out[dst + w] = src[w];
+  const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
+  for (int64_t w = threadIdx.x; w < words; w += 256) {
+    const int64_t m = w / k;
+    out[dst + w] = F.entry(src, aux, m, int(w - m * k));
   }
 }
 
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
                                                              int32_t* __restrict__ out, int64_t out_cap, int sub,
                                                              int64_t* __restrict__ total,
                                                              unsigned long long* __restrict__ clear_flag,
-                                                             int expand) {
+                                                             SlotFormat F) {
   __shared__ int64_t s_pre[SMALL_FINISH + 1];
   __shared__ int64_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -123,14 +129,11 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
     const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
     if (pre + m > out_cap) continue;
     const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
+    const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
     int32_t* dst = out + pre * k;
-    if (expand) {
-      for (int64_t w = lane; w < m * k; w += 64) {
-        const int64_t q = w / k;
-        dst[w] = src[q] + int32_t(w - q * k);
-      }
-    } else {
-      for (int64_t w = lane; w < m * k; w += 64) dst[w] = src[w];
+    for (int64_t w = lane; w < m * k; w += 64) {
+      const int64_t q = w / k;
+      dst[w] = F.entry(src, aux, q, int(w - q * k));
     }
   }
 }
@@ -167,16 +170,16 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e == hipSuccess) e = stencil_count(L, st);
   if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
-  // the plain kernel (stencil_kernel.h launch_kts) left one int per match in the slots
-  const int expand = L.plain && !L.carry.hdr && !L.chain && L.k <= 7;
+  // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
+  const SlotFormat F{L.k, L.plain && !L.carry.hdr && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
   if (nsuper <= SMALL_FINISH) {
     hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
-                       L.out_cap, sub, L.total, L.clear_flag, expand);
+                       L.out_cap, sub, L.total, L.clear_flag, F);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
-  hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre, L.k,
-                     L.out, L.out_cap, sub, expand);
+  hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre,
+                     L.out, L.out_cap, sub, F);
   return hipGetLastError();
 }
 

@@ -397,6 +397,21 @@ __device__ __forceinline__ uint32_t chain_halo_ends(const HaloHead& H, int o, ui
   return res;
 }
 
+// stage s's entry of a keyed-kernel match (completing record rj, aux byte a; see the write phase):
+// the record, -1 for a skipped optional stage, -(1 + d) for a halo record d records before the segment
+__device__ __forceinline__ int32_t stencil_row(int32_t rj, uint32_t a, int s, int k, bool chain, bool carry) {
+  if (chain) {
+    const uint32_t d = a & 3u, cm = (a >> 2) & 15u;
+    const int ho = int(a >> 6);
+    const int rel = -int32_t(d) + __popc(cm & ((1u << s) - 1));
+    if (!((cm >> s) & 1)) return -1;
+    if (carry && ho != 3 && rel < -ho) return -(1 + (-ho - rel));
+    return rj + rel;
+  }
+  const int need = carry ? int(a) : 0;
+  return s < need ? -(1 + (need - s)) : rj - (k - 1) + s;
+}
+
 template <int K, class VT, bool TOPIC, bool CHAIN, bool CARRY, int SUB>
 __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
     const int32_t* __restrict__ key, const VT* __restrict__ val, const int32_t* __restrict__ topic, int64_t n,
@@ -638,8 +653,13 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
 
   // ================= write phase: the super-tile's matches into its slot =================
   // each thread stores its own matches at their place in the tile's run (record order; per record
-  // oldest start first), K entries each: no compaction through LDS, no barrier
-  int32_t* slot = out + tile0 * int64_t(ST_TILE) * K;     // super-tile s_super's slot
+  // oldest start first): no compaction through LDS, no barrier.  One int per match (its completing
+  // record) plus one aux byte (chain: start distance | consumed stages << 2 | halo records << 6;
+  // carry: the stages taken from the halo) after the super-tile's SUB x 4096 ints; stencil_gather
+  // writes the K-int rows (stencil_row)
+  int32_t* const slot = out + tile0 * int64_t(ST_TILE) * K;   // super-tile s_super's slot
+  uint8_t* const aux = reinterpret_cast<uint8_t*>(slot + SUB * ST_TILE);
+  int64_t mbase = 0;                               // matches of the super-tile's earlier tiles
   if constexpr (CHAIN && CARRY) {                  // halo runs can exceed a tile's match space: fail the batch
     int64_t sum = 0;
     bool over = false;
@@ -676,15 +696,9 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         // one match: completing record rj, started d records before, consumed-stage mask cm; ho: the
         // segment's records before rj when the run started in the halo (3: it did not)
         auto put = [&](int32_t rj, uint32_t d, uint32_t cm, int ho) {
-          int32_t* dst = slot + int64_t(o++) * K;
-#pragma unroll
-          for (int s = 0; s < K; s++) {                // skipped optional stages: -1
-            const int rel = -int32_t(d) + __popc(cm & ((1u << s) - 1));
-            int32_t rec = ((cm >> s) & 1) ? rj + rel : -1;
-            if constexpr (CARRY)                       // a halo record: -(1 + records before the segment)
-              if (((cm >> s) & 1) && ho != 3 && rel < -ho) rec = -(1 + (-ho - rel));
-            dst[s] = rec;
-          }
+          slot[mbase + o] = rj;
+          aux[mbase + o] = uint8_t(d | (cm << 2) | (uint32_t(ho) << 6));
+          o++;
         };
         while (any) {                                // record order; per record oldest start first
           const int p = __ffs(any) - 1;
@@ -726,16 +740,13 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         while (h) {
           const int i = __ffs(h) - 1;
           h &= h - 1;
-          const int32_t rj = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
-          int32_t* dst = slot + int64_t(o++) * K;
-          int need = 0;
-          if constexpr (CARRY) need = int((bneed[j] >> (4 * i)) & 0xF);
-#pragma unroll
-          for (int s = 0; s < K; s++)                  // carry: halo stages -(1 + records before the segment)
-            dst[s] = s < need ? -(1 + (need - s)) : rj - (K - 1) + s;
+          slot[mbase + o] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
+          if constexpr (K > 1)                         // carry: the stages taken from the halo
+            aux[mbase + o] = CARRY ? uint8_t((bneed[j] >> (4 * i)) & 0xF) : uint8_t(0);
+          o++;
         }
       }
-      slot += total[j] * K;
+      mbase += total[j];
     }
   }
 }
