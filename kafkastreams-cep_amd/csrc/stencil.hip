@@ -22,8 +22,13 @@ hipError_t stencil_count_k8(const StencilLaunch& L, hipStream_t st);
 struct SlotFormat {
   int k, plain, chain, carry;
   __device__ __forceinline__ int32_t entry(const int32_t* src, const uint8_t* aux, int64_t m, int s) const {
-    if (plain) return src[m] + s;
-    return stencil_row(src[m], k > 1 ? aux[m] : 0u, s, k, chain, carry);
+    const int32_t v = src[m];
+    if (plain) {                                 // first record; carry boundary: -(1 + completing record)
+      if (!carry || v >= 0) return v + s;
+      const int need = aux[m];
+      return s < need ? -(1 + (need - s)) : -(1 + v) - (k - 1) + s;
+    }
+    return stencil_row(v, k > 1 ? aux[m] : 0u, s, k, chain, carry);
   }
 };
 __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
@@ -171,7 +176,7 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
   // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
-  const SlotFormat F{L.k, L.plain && !L.carry.hdr && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
+  const SlotFormat F{L.k, L.plain && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
   if (nsuper <= SMALL_FINISH) {
     hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
                        L.out_cap, sub, L.total, L.clear_flag, F);

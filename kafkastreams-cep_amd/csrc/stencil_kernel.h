@@ -797,13 +797,24 @@ __device__ __forceinline__ void load_tile(Chunk<VT, TOPIC>& c, const int32_t* __
 #ifndef ST_PLAIN_WAVES
 #define ST_PLAIN_WAVES 6                          // waves per SIMD the register budget is cut for (A/B knob)
 #endif
-template <int K, class VT, bool TOPIC, int SUB>
-__global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kernel(
+// Carry sessions (CARRY): the same window test finds the records with K-1 same-key records before
+// them in the batch; the boundary records (the segment's first K-1) and the segments' ends are
+// visited as in stencil_kernel<CARRY> (halo reads, claims, halo writes), with their keys from a
+// sparse LDS key image: the loader stores the key of each record that starts or ends a segment
+// (and of every record whose neighbour lies in another lane), the only keys a visit reads.  A
+// boundary match is stored as -(1 + completing record) with its halo record count in the slot's
+// aux byte (stencil_gather writes the -(1 + d) halo entries); an interior one as its first record.
+#ifndef ST_CARRY_WAVES
+#define ST_CARRY_WAVES 4                          // waves per SIMD the carry variant's registers are cut for
+#endif
+template <int K, class VT, bool TOPIC, int SUB, bool CARRY>
+__global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES) void stencil_plain_kernel(
     const int32_t* __restrict__ key, const VT* __restrict__ val, const int32_t* __restrict__ topic, int64_t n,
     const StencilProgram* __restrict__ P, int32_t* __restrict__ out, int64_t* __restrict__ tile_count,
-    int64_t ntiles) {
+    int64_t ntiles, StencilCarry C) {
   static_assert(K >= 1 && K <= 7, "bit 7 of a record's byte is its same-key bit");
   __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];   // record r at r + 16
+  __shared__ int32_t s_bk[CARRY ? ST_TILE + 16 : 1];   // carry: keys of segment starts/ends, record r at r + 16
   __shared__ int32_t s_lastk[2][17];   // [tile & 1][m]: key of tile record 256m - 1 (m >= 1); [0][0]: before tile 0
   __shared__ int32_t s_firstk[16];     // key of tile record 256m
   __shared__ int32_t s_wsum[2][ST_THREADS / 64];
@@ -838,13 +849,19 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
   uint32_t h_mask = 0;
   if (halo_lane && hg >= 0)
     h_mask = mask_of<VT, TOPIC>(P, s_tab, s_nan, h_val, h_top) | (uint32_t(hg > 0 && h_prev == h_key) << 7);
+  int32_t h_bk = h_key;                           // carry: the history records' keys
+  bool twice = false;                             // carry: a key claimed twice in this batch
 
   // per tile: count, then its matches written as one run into the super-tile's slot right away (the
   // next tile's loads are in flight meanwhile)
   int32_t* slot = out + tile0 * int64_t(ST_TILE) * K;
+  uint8_t* const aux = reinterpret_cast<uint8_t*>(slot + SUB * ST_TILE);   // carry: per match, after the ints
   int64_t sum = 0;
   for (int j = 0; j < ntl; j++) {                 // uniform
     const int64_t base = (tile0 + j) * ST_TILE;
+    int32_t nk = INT32_MIN;                       // carry: the key after the tile (thread 255)
+    if constexpr (CARRY)
+      if (tid == ST_THREADS - 1 && base + ST_TILE < n) nk = key[base + ST_TILE];
     uint32_t packed[4];
     masks_of_chunk<VT, TOPIC>(cur, P, s_tab, s_nan, packed, s_lut);
 #pragma unroll
@@ -861,8 +878,19 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
       *reinterpret_cast<uint32_t*>(&s_mask[16 + local]) = w;
       if (lane == 0) s_firstk[4 * q + wid] = k[0];
       if (lane == 63) s_lastk[j & 1][4 * q + wid + 1] = k[3];
+      if constexpr (CARRY) {                      // the keys a visit may read (see above)
+        const int32_t kn = __builtin_amdgcn_update_dpp(INT32_MIN, k[0], 0x130, 0xF, 0xF, false);   // wave_shl:1
+        // c_e: record e differs from the one before, or lies past the batch end (unloaded key)
+        const bool c1 = k[1] != k[0] || left <= 1, c2 = k[2] != k[1] || left <= 2, c3 = k[3] != k[2] || left <= 3;
+        if (lane == 0 || kp != k[0] || c1) s_bk[16 + local] = k[0];
+        if (c1 || c2) s_bk[16 + local + 1] = k[1];
+        if (c2 || c3) s_bk[16 + local + 2] = k[2];
+        if (c3 || lane == 63 || kn != k[3] || left <= 4) s_bk[16 + local + 3] = k[3];
+      }
     }
     if (tid < 16) s_mask[tid] = halo_lane ? uint8_t(h_mask) : 0;
+    if constexpr (CARRY)
+      if (tid < 16) s_bk[tid] = h_bk;
     if (j == 0 && tid == 0) s_lastk[0][0] = before0;
     // the chunk is consumed: the next tile's loads go out before the barrier, so a wave whose data
     // came early does not hold its refill back until the slowest wave's has arrived
@@ -890,16 +918,104 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
       S = (S & ~(1u << pb)) | (uint32_t(kb == s_firstk[m]) << pb);
     }
     uint32_t h = 0xFFFFFFFFu;
+    uint32_t Bs[K];
 #pragma unroll
     for (int s = 0; s < K; s++) {
       uint32_t B = 0;
 #pragma unroll
       for (int q = 0; q < 3; q++) B |= byte_bits(m8[q], s) << (8 * q);
+      Bs[s] = B;
       h &= B << (K - 1 - s);
     }
 #pragma unroll
     for (int d = 0; d < K - 1; d++) h &= S << d;
     uint32_t hit = (h >> 8) & 0xFFFFu;
+    uint64_t bneed = 0;                           // carry: halo records of each boundary hit (4 bits each)
+    if constexpr (CARRY) {
+      // same-key bit of the record after the thread's last (the next thread's first; thread 255: the
+      // next tile's first, from the key read at the tile's start)
+      const int rn = ST_EPT * tid + 16;
+      uint32_t sn = 0;
+      if ((rn & 255) == 0) {
+        const int m = rn >> 8;
+        sn = m < 16 ? uint32_t(s_lastk[j & 1][m] == s_firstk[m]) : uint32_t(base + ST_TILE < n && nk == s_lastk[j & 1][16]);
+      } else {
+        sn = s_mask[16 + rn] >> 7;
+      }
+      const int64_t g0 = base + ST_EPT * tid;     // batch index of own record 0 (window record 8)
+      if (g0 + ST_EPT >= n) sn = 0;               // the batch's last record ends its segment
+      const int64_t left = n - g0;
+      const uint32_t live = left >= 16 ? 0xFFFFu : left <= 0 ? 0u : (1u << left) - 1u;
+      S &= (live << 8) | 0xFFu;                   // a record past the batch end (table-resolved bit) starts nothing
+      const uint32_t Sown = (S >> 8) & 0xFFFFu;
+      const uint32_t starts = ~Sown & live;
+      const uint32_t ends = ~((S >> 9) | (sn << 15)) & live;
+      // boundary candidates: o < K-1 same-key records before the record in the batch (a segment
+      // start o records back) and stages K-1-o..K-1 on the segment's records; stages 0..K-2-o must
+      // come from the halo
+      uint32_t cand = 0;
+#pragma unroll
+      for (int o = 0; o < K - 1; o++) {
+        uint32_t c = ~S << o;
+#pragma unroll
+        for (int t = 0; t < o; t++) c &= S << t;
+#pragma unroll
+        for (int t = 0; t <= o; t++) c &= Bs[K - 1 - o + t] << (o - t);
+        cand |= c;
+      }
+      cand = (cand >> 8) & live;
+      uint32_t todo = cand | ends | starts;
+      if (todo) {
+        const int lb16 = 16 + ST_EPT * tid;       // s_bk index of own record 0
+        // same-key records before own record i in the batch (capped at K-1)
+        auto before_of = [&](int i) {
+          int o = 0;
+#pragma unroll
+          for (int t = 1; t < K; t++)
+            if (o == t - 1 && ((S >> (8 + i - t + 1)) & 1)) o = t;
+          return o;
+        };
+        auto key_of = [&](int i) {                // a start or end: its own entry; a candidate: its start's
+          const bool own = ((starts | ends) >> i) & 1;
+          return s_bk[lb16 + i - (own ? 0 : before_of(i))];
+        };
+        const int32_t ka = key_of(__ffs(todo) - 1), kb = key_of(31 - __clz(todo));
+        const bool oka = key_ok(C, ka), okb = kb != ka && key_ok(C, kb);
+        const HaloRaw ra = halo_load(C, oka ? ka : 0), rb = halo_load(C, okb ? kb : 0);
+        uint32_t st = starts;
+        while (st) {                              // claims
+          const int i = __ffs(st) - 1;
+          st &= st - 1;
+          const int32_t ks = s_bk[lb16 + i];
+          if (ks >= 0 && ks < C.max_keys) twice |= atomicMax(&C.hdr[ks].claim, C.stamp) == C.stamp;
+        }
+        HaloHead H0, H1;
+        if (oka) halo_pick(C, ka, ra, H0);
+        if (okb) halo_pick(C, kb, rb, H1);
+        todo = cand | ends;
+        while (todo) {
+          const int i = __ffs(todo) - 1;
+          todo &= todo - 1;
+          const int o = before_of(i);
+          const int32_t kj = key_of(i);
+          HaloHead H = kj == H0.key ? H0 : H1;
+          if (!halo_head(C, kj, H)) continue;
+          if ((cand >> i) & 1) {                  // the first stages in the halo
+            const int need = K - 1 - o;
+            if (halo_match<K>(H, need)) {
+              hit |= 1u << i;
+              bneed |= uint64_t(need) << (4 * i);
+            }
+          }
+          if ((ends >> i) & 1) {                  // the segment's last record: the new halo
+            const int sg = o + 1 < K - 1 ? o + 1 : K - 1;
+            uint64_t wmk = 0;
+            for (int t = 0; t < sg; t++) wmk |= uint64_t(s_mask[lb + 8 + i - (sg - 1) + t] & 0x7Fu) << (8 * t);
+            halo_write<K>(C, H, sg, wmk, g0 + i);
+          }
+        }
+      }
+    }
     const int cnt = __popc(hit);
     // the wave's exclusive prefix of the counts (<= 16: five bits) by ballots, no shuffle table
     int before = 0, wtot = 0;
@@ -911,6 +1027,8 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
     }
     if (lane == 0) s_wsum[j & 1][wid] = wtot;
     if (halo_lane) h_mask = s_mask[ST_TILE + tid];   // the next tile's halo: this tile's last records
+    if constexpr (CARRY)
+      if (halo_lane) h_bk = s_bk[ST_TILE + tid];
     __syncthreads();                              // (B) wave sums
     int o = before, tot = 0;
 #pragma unroll
@@ -928,21 +1046,38 @@ __global__ __launch_bounds__(ST_THREADS, ST_PLAIN_WAVES) void stencil_plain_kern
     while (hit) {
       const int i = __ffs(hit) - 1;
       hit &= hit - 1;
+      if constexpr (CARRY) {
+        const uint32_t need = uint32_t(bneed >> (4 * i)) & 0xFu;
+        if (need) {                               // a boundary match: -(1 + completing record), halo count in aux
+          slot[o] = -(1 + int32_t(base) + tid * ST_EPT + i);
+          aux[sum + o] = uint8_t(need);
+          o++;
+          continue;
+        }
+      }
       slot[o++] = b32 + tid * ST_EPT + i;
     }
     slot += tot;
     sum += tot;
   }
   if (tid == 0) tile_count[blockIdx.x] = sum;
+  if constexpr (CARRY)
+    if (twice) atomicOr(C.flags, 2ull);           // a key in two segments of the batch
 }
 
 template <int K, class VT, bool TP, bool CH, int SUB>
 inline void launch_kts(const StencilLaunch& L, int64_t ntiles, hipStream_t st) {
   const int64_t nsuper = (ntiles + SUB - 1) / SUB;
   if constexpr (!CH && K <= 7) {
-    if (!L.carry.hdr && L.plain) {
-      hipLaunchKernelGGL((stencil_plain_kernel<K, VT, TP, SUB>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st, L.key,
-                         static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count, ntiles);
+    if (L.plain) {
+      if (L.carry.hdr)
+        hipLaunchKernelGGL((stencil_plain_kernel<K, VT, TP, SUB, true>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
+                           L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count,
+                           ntiles, L.carry);
+      else
+        hipLaunchKernelGGL((stencil_plain_kernel<K, VT, TP, SUB, false>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
+                           L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count,
+                           ntiles, L.carry);
       return;
     }
   }

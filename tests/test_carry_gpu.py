@@ -390,3 +390,46 @@ def test_runs_carry_rejects_unclean_batches():
     assert ei.value.code == 12
     s.push(4, key, [val], offset=np.arange(4, dtype=np.int64), flags=N.BATCH_OFFSETS_MONOTONE)
     s.collect()
+
+
+def _strict_pattern(k):
+    q = PL.QueryBuilder().select("s0").where(PL.Event.value() == 0)
+    for i in range(1, k):
+        q = q.then().select(f"s{i}").where(PL.Event.value() == (i % 2))
+    return q.build().to_ir(PL.I32)
+
+
+@pytest.mark.parametrize("k", [2, 3, 5, 7])
+def test_stencil_carry_large_batches(k):
+    """Carry batches of many tiles (the plain kernel's carry variant): segments of every length from
+    1 record up cross lane, wave (256-record) and tile (4096-record) boundaries, keys continue across
+    3 batch cuts; against one oracle run of the whole stream."""
+    rng = np.random.default_rng(100 + k)
+    n_keys = 600
+    lens = np.concatenate([rng.integers(1, 8, 200), rng.poisson(400, n_keys - 200) + 1])
+    key = np.repeat(rng.permutation(n_keys).astype(np.int32), lens)
+    rng.shuffle(key)
+    val = rng.integers(0, 2, len(key)).astype(np.int32)
+    ir = _strict_pattern(k)
+    want, _, oerr = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    assert oerr is None and len(want) > 1000
+    cuts = sorted(rng.choice(np.arange(1, len(key)), 3, replace=False).tolist())
+    bounds, order = batches_of(key, cuts)
+    got, sess, err = run_carry(ir, key[order], [val[order]], bounds, max_keys=n_keys)
+    assert sess.path == N.PATH_STENCIL and err is None
+    got = [(int(order[m[0]]), m[1], [(nm, int(order[r])) for nm, r in m[2]]) for m in got]
+    assert sorted(got) == sorted(want)
+
+
+def test_stencil_carry_large_batch_key_in_two_segments():
+    """A key in two segments of one large batch (in different workgroups' tiles) is the
+    interleaved-batch error (CEP_E_ARG at collect), as for a small batch."""
+    ir = synth.c2_pattern().to_ir(PL.I32)
+    key = np.repeat(np.arange(300, dtype=np.int32), 100)
+    key[20000:20100] = 7                                 # key 7 again, ~13k records after its segment
+    s = N.Session(N.CompiledPattern(ir), len(key), carry=True, max_keys=300)
+    assert s.path == N.PATH_STENCIL
+    with pytest.raises(N.CepError) as e:
+        s.push(len(key), key, [np.zeros(len(key), np.int32)])
+        s.collect()
+    assert e.value.code == 11
