@@ -965,6 +965,7 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
       }
       cand = (cand >> 8) & live;
       uint32_t todo = cand | ends | starts;
+      if (C.dbg & 8) todo = 0;                    // A/B probe only: no visits
       if (todo) {
         const int lb16 = 16 + ST_EPT * tid;       // s_bk index of own record 0
         // same-key records before own record i in the batch (capped at K-1)

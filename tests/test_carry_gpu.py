@@ -433,3 +433,39 @@ def test_stencil_carry_large_batch_key_in_two_segments():
         s.push(len(key), key, [np.zeros(len(key), np.int32)])
         s.collect()
     assert e.value.code == 11
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_stencil_carry_partial_last_super_tile(k):
+    """A batch of 8193 tiles runs 4 tiles per workgroup, the last workgroup one tile: its boundary
+    matches' aux bytes lie past its own tile's slot ints (the slot buffer is padded for them).  Keys
+    of the first batch continue in the second batch's last tile, behind 33.5 M filler records that
+    match nothing; the matches equal the oracle's over the first batch plus that tail."""
+    rng = np.random.default_rng(7 + k)
+    nk = 40
+    b1_key = np.repeat(np.arange(nk, dtype=np.int32), 3)
+    b1_val = rng.integers(0, 2, len(b1_key)).astype(np.int32)
+    n2 = 8193 * 4096
+    tail = 2048
+    t_key = np.sort(rng.integers(0, nk, tail)).astype(np.int32)
+    t_val = rng.integers(0, 2, tail).astype(np.int32)
+    f_key = (nk + np.arange(n2 - tail) // 1000).astype(np.int32)     # filler keys, segments of 1000
+    key2 = np.concatenate([f_key, t_key])
+    val2 = np.concatenate([np.full(n2 - tail, 3, np.int32), t_val])
+    ir = _strict_pattern(k)
+    # the oracle over the first batch and the tail (the filler shares no key with them)
+    o_key = np.concatenate([b1_key, t_key])
+    o_val = np.concatenate([b1_val, t_val])
+    want, _, oerr = oracle_run(ir, o_key, [o_val], [1], O.MODE_PROCESSOR)
+    assert oerr is None and len(want) > 20
+    shift = n2 - tail                                  # oracle position p >= len(b1) -> stream position p + shift
+
+    def pos(p):
+        return p if p < len(b1_key) else p + shift
+    want = sorted((pos(m[0]), m[1], [(nm, pos(r)) for nm, r in m[2]]) for m in want)
+    s = N.Session(N.CompiledPattern(ir), n2, carry=True, max_keys=int(key2.max()) + 1)
+    got, s, err = run_carry(ir, np.concatenate([b1_key, key2]), [np.concatenate([b1_val, val2])],
+                            [0, len(b1_key), len(b1_key) + n2], sess=s)
+    assert s.path == N.PATH_STENCIL and err is None
+    assert sorted(got) == want
+    assert any(r < len(b1_key) for m in got for _, r in m[2])   # matches that start in the halo
