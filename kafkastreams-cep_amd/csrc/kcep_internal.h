@@ -170,9 +170,8 @@ struct StencilLaunch {
   int64_t out_cap;                // matches
   int64_t* total;                 // device: number of matches
   StencilCarry carry;             // halo != nullptr: carry session
-  int plain;                      // no chain, k <= 7: the keyless kernel (KCEP_STENCIL_KEYED=1: off)
+  int plain;                      // plain stencil (no carry, no chain, k <= 7): the keyless kernel (KCEP_STENCIL_KEYED=1: off)
   unsigned long long* clear_flag; // carry: the next batch's error-flag word, zeroed by the scan kernel (or null)
-  int fuse_scan = 0;              // set by stencil_launch: the plain kernel's last workgroup scans the counts
 };
 
 // compile.cpp

@@ -48,11 +48,6 @@ __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict_
 
 // ---- launcher ------------------------------------------------------------
 
-static bool getenv_flag_dev(const char* name) {     // A/B knobs (read once per name)
-  const char* v = getenv(name);
-  return v && *v && *v != '0';
-}
-
 int64_t stencil_tiles(int64_t n) { return (n + ST_TILE - 1) / ST_TILE; }
 
 // exclusive prefix of the super-tile counts in one 1024-thread workgroup, plus
@@ -176,23 +171,18 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
   const int sub = stencil_sub(ntiles);
   const int64_t nsuper = (ntiles + sub - 1) / sub;
-  // the kernel that runs (stencil_kernel.h launch_kts) and its slot format; KCEP_STENCIL_FUSED_SCAN=1:
-  // the plain kernel scans the counts itself (scan_tail) instead of tile_scan, unless one workgroup
-  // finishes the batch (stencil_finish_small)
-  const SlotFormat F{L.k, L.plain && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
-  StencilLaunch LK = L;
-  LK.fuse_scan = F.plain && nsuper > SMALL_FINISH && getenv_flag_dev("KCEP_STENCIL_FUSED_SCAN");   // opt-in (A/B)
   hipError_t e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
-  if (e == hipSuccess) e = stencil_count(LK, st);
+  if (e == hipSuccess) e = stencil_count(L, st);
   if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
+  // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
+  const SlotFormat F{L.k, L.plain && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
   if (nsuper <= SMALL_FINISH) {
     hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
                        L.out_cap, sub, L.total, L.clear_flag, F);
     return hipGetLastError();
   }
-  if (!LK.fuse_scan)
-    hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
+  hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
   hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre,
                      L.out, L.out_cap, sub, F);
   return hipGetLastError();

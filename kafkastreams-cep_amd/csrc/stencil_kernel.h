@@ -791,66 +791,6 @@ __device__ __forceinline__ void load_tile(Chunk<VT, TOPIC>& c, const int32_t* __
   }
 }
 
-// The plain kernel's last workgroup (the one whose arrival on `done` completes the grid) scans the
-// super-tile counts into their exclusive prefix and the total -- tile_scan without its own launch.
-// No fences (an agent-scope release writes back the XCD's L2, slots included): each workgroup
-// publishes its count with an agent-scope atomic exchange and waits for it before it arrives; the
-// last one reads the counts with agent-scope atomic loads and re-arms `done` for the next launch.
-struct ScanTail {
-  int64_t* pre;                          // null: no fused scan (tile_scan or stencil_finish_small runs)
-  int64_t* total;
-  unsigned long long* clear_flag;        // carry: the next batch's error-flag word
-  unsigned* done;
-};
-__device__ __forceinline__ void scan_tail(const ScanTail& T, int64_t* cnt, int64_t my, int64_t nt, int tid) {
-  __shared__ int s_last;
-  __shared__ int64_t s_w[ST_THREADS / 64];
-  if (tid == 0) {
-    const int64_t was = __hip_atomic_exchange(cnt + blockIdx.x, my, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // (the exchange has returned -- `was` is read, counts are >= 0 -- before the arrival is issued)
-    s_last = __hip_atomic_fetch_add(T.done, 1u + unsigned(was < 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             unsigned(gridDim.x) - 1u;
-  }
-  __syncthreads();
-  if (!s_last) return;                             // uniform
-  const int lane = tid & 63, wid = tid >> 6;
-  const int64_t per = (nt + ST_THREADS - 1) / ST_THREADS, a = tid * per, b = a + per < nt ? a + per : nt;
-  auto ld = [&](int64_t i) { return __hip_atomic_load(cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  int64_t sum = 0;
-  for (int64_t c = a; c < b; c += 8) {
-    int64_t v[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = c + i < b ? ld(c + i) : 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) sum += v[i];
-  }
-  int64_t incl = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) s_w[wid] = incl;
-  __syncthreads();
-  int64_t run = incl - sum;
-  for (int w = 0; w < wid; w++) run += s_w[w];
-  for (int64_t c = a; c < b; c += 8) {
-    int64_t v[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = c + i < b ? ld(c + i) : 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if (c + i < b) T.pre[c + i] = run;
-      run += v[i];
-    }
-  }
-  if (tid == ST_THREADS - 1) *T.total = run;
-  if (tid == 0) {
-    if (T.clear_flag) *T.clear_flag = 0;
-    *T.done = 0u;                                  // re-armed for the next launch
-  }
-}
-
 #ifndef ST_PLAIN_EARLY
 #define ST_PLAIN_EARLY 1                          // next tile's loads issued before the image barrier (A/B knob)
 #endif
@@ -871,7 +811,7 @@ template <int K, class VT, bool TOPIC, int SUB, bool CARRY>
 __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES) void stencil_plain_kernel(
     const int32_t* __restrict__ key, const VT* __restrict__ val, const int32_t* __restrict__ topic, int64_t n,
     const StencilProgram* __restrict__ P, int32_t* __restrict__ out, int64_t* __restrict__ tile_count,
-    int64_t ntiles, StencilCarry C, ScanTail T) {
+    int64_t ntiles, StencilCarry C) {
   static_assert(K >= 1 && K <= 7, "bit 7 of a record's byte is its same-key bit");
   __shared__ __attribute__((aligned(16))) uint8_t s_mask[ST_TILE + 16];   // record r at r + 16
   __shared__ int32_t s_bk[CARRY ? ST_TILE + 16 : 1];   // carry: keys of segment starts/ends, record r at r + 16
@@ -1121,10 +1061,9 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
     slot += tot;
     sum += tot;
   }
+  if (tid == 0) tile_count[blockIdx.x] = sum;
   if constexpr (CARRY)
     if (twice) atomicOr(C.flags, 2ull);           // a key in two segments of the batch
-  if (T.pre) scan_tail(T, tile_count, sum, int64_t(gridDim.x), tid);
-  else if (tid == 0) tile_count[blockIdx.x] = sum;
 }
 
 template <int K, class VT, bool TP, bool CH, int SUB>
@@ -1132,15 +1071,14 @@ inline void launch_kts(const StencilLaunch& L, int64_t ntiles, hipStream_t st) {
   const int64_t nsuper = (ntiles + SUB - 1) / SUB;
   if constexpr (!CH && K <= 7) {
     if (L.plain) {
-      const ScanTail T{L.fuse_scan ? L.tile_pre : nullptr, L.total, L.clear_flag, reinterpret_cast<unsigned*>(L.scan_tmp)};
       if (L.carry.hdr)
         hipLaunchKernelGGL((stencil_plain_kernel<K, VT, TP, SUB, true>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
                            L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count,
-                           ntiles, L.carry, T);
+                           ntiles, L.carry);
       else
         hipLaunchKernelGGL((stencil_plain_kernel<K, VT, TP, SUB, false>), dim3(unsigned(nsuper)), dim3(ST_THREADS), 0, st,
                            L.key, static_cast<const VT*>(L.val), L.topic, L.n, L.prog_dev, L.slots, L.tile_count,
-                           ntiles, L.carry, T);
+                           ntiles, L.carry);
       return;
     }
   }
