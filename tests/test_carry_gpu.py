@@ -469,3 +469,41 @@ def test_stencil_carry_partial_last_super_tile(k):
     assert s.path == N.PATH_STENCIL and err is None
     assert sorted(got) == want
     assert any(r < len(b1_key) for m in got for _, r in m[2])   # matches that start in the halo
+
+
+@pytest.mark.parametrize("t", ["i32_topic", "i64", "f64"])
+def test_stencil_carry_topic_and_wide_columns(t):
+    """The plain carry kernel's topic and 64-bit value instantiations: multi-tile batches with keys
+    continuing across 3 cuts, against one oracle run of the whole stream."""
+    from kcep import Schema, QueryBuilder, Event, Selected
+    rng = np.random.default_rng(31)
+    n_keys = 300
+    key = np.repeat(rng.permutation(n_keys).astype(np.int32), rng.poisson(150, n_keys) + 1)
+    rng.shuffle(key)
+    n = len(key)
+    kw, ty = {}, 1
+    if t == "i32_topic":
+        val = rng.integers(0, 3, n).astype(np.int32)
+        kw["topic"] = rng.integers(0, 2, n).astype(np.int32)
+        sch = Schema([("value", "i32")], topics=["t0", "t1"])
+        q = (QueryBuilder().select("a", Selected.withStrictContiguity().withTopic("t1")).where(Event.value() == 0)
+             .then().select("b").where(Event.value() != 0).then()
+             .select("c", Selected.withStrictContiguity().withTopic("t0")).where(Event.value() == 2).build())
+    else:
+        raw = rng.integers(-3, 4, n)
+        c = 1_000_000_007 if t == "i64" else 0.5
+        val = (raw * c).astype(np.int64) if t == "i64" else raw.astype(np.float64) * 0.5
+        ty = 2 if t == "i64" else 3
+        sch = Schema([("value", t)])
+        q = (QueryBuilder().select("lo").where(Event.value() < 0).then()
+             .select("hi").where(Event.value() > c).build())
+    ir = q.to_ir(sch)
+    want, _, oerr = oracle_run(ir, key, [val], [ty], O.MODE_PROCESSOR, **kw)
+    assert oerr is None and len(want) > 100
+    cuts = sorted(rng.choice(np.arange(1, n), 3, replace=False).tolist())
+    bounds, order = batches_of(key, cuts)
+    got, sess, err = run_carry(ir, key[order], [val[order]], bounds, max_keys=n_keys,
+                               **{f: v[order] for f, v in kw.items()})
+    assert sess.path == N.PATH_STENCIL and err is None
+    got = [(int(order[m[0]]), m[1], [(nm, int(order[r])) for nm, r in m[2]]) for m in got]
+    assert sorted(got) == sorted(want)
