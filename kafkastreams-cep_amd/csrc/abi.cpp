@@ -57,7 +57,8 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
                               int64_t* ent_record, hipStream_t st);
 hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
                                unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
-                               int64_t* scan_tmp, hipStream_t st);
+                               int64_t* scan_tmp, unsigned long long* max_span, hipStream_t st);
+hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, hipStream_t st);
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
                      size_t* tmp_bytes, hipStream_t st);
 hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,
@@ -487,7 +488,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.err_code = s->r_errcode.as<int32_t>();
   A.segs = s->r_segs.as<uint32_t>();             // the runs' consumed stages, for runs_expand
   A.seg_over = ctl + 3;
-  const unsigned long long init[4] = {0, ~0ull, 0, 0};   // matches, first exception, entries, segment overflow
+  const unsigned long long init[5] = {0, ~0ull, 0, 0, 0};   // matches, first exception, entries, segment overflow, longest span
   HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
   HIPCHECK(runs_sim_launch(A, s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), st,
                            s->jit ? s->jit->runs_sim : nullptr));
@@ -497,7 +498,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int64_t nblk = n / 256 + 2;
   HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->r_endof.as<int32_t>(), n,
                                s->rk.as<unsigned long long>(), s->r_blk.as<int64_t>(), s->r_blk.as<int64_t>() + nblk,
-                               reinterpret_cast<int64_t*>(ctl + 2), s->scan_tmp.as<int64_t>(), st));
+                               reinterpret_cast<int64_t*>(ctl + 2), s->scan_tmp.as<int64_t>(), ctl + 4, st));
   if (rcarry) {                                    // the keys' new tails: from their oldest still-open start
     if (s->rc_c.ensure(size_t(nb + 2) * 8) || s->rc_d.ensure(size_t(nb + 2) * 8))
       return fail(CEP_E_HIP, "allocation failed");
@@ -507,7 +508,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                               s->rpool.as<int64_t>(), s->rtab.as<int64_t>(), st));
   }
   // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow
-  unsigned long long res[4];
+  unsigned long long res[5];
   int64_t top = 0;
   HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(&res[0], scal0 + 3, 8, hipMemcpyDeviceToHost, st));
@@ -540,7 +541,11 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
       s->scan_tmp.ensure(size_t(nm / 1024 + 4) * 8) || s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) ||
       s->o_entoff.ensure(nmb * 8) || s->o_name.ensure(neb * 4) || s->o_entrec.ensure(neb * 8))
     return fail(CEP_E_HIP, "allocation failed");
-  if (nm > 0)
+  // (completing record, start) order: a windowed rank when every run spans <= 1024 records
+  // (runs_order), else rocPRIM's radix sort over the completing record's bits
+  if (nm > 0 && res[4] <= 1024 && !getenv_flag("KCEP_RUNS_RADIX"))
+    HIPCHECK(runs_order_launch(s->rk.as<unsigned long long>(), nm, int(res[4]), s->rk_sorted.as<unsigned long long>(), st));
+  else if (nm > 0)
     HIPCHECK(runs_sort(s->rk.as<unsigned long long>(), s->rk_sorted.as<unsigned long long>(), nm, bits, s->rk_tmp.p,
                        &tmp_bytes, st));
   int64_t* scal = s->scal.as<int64_t>();

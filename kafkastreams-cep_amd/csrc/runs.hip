@@ -43,21 +43,65 @@ __global__ __launch_bounds__(RT) void runs_write(WriteArgs W) { runs_write_body(
 
 // completed runs in start order: key (end << 31 | start); each workgroup's total of their lengths
 // (entries of the CSR) into blk_len[blockIdx] (summed by a scan: no contended atomic)
+// (and the longest run's span e - s, atomicMax into *max_span: it bounds runs_order's window)
 __global__ __launch_bounds__(256) void runs_compact(const int64_t* __restrict__ flag, const int64_t* __restrict__ pos,
                                                     const int32_t* __restrict__ end_of, int64_t n,
-                                                    unsigned long long* __restrict__ out, int64_t* __restrict__ blk_len) {
-  __shared__ int64_t s_w[4];
+                                                    unsigned long long* __restrict__ out, int64_t* __restrict__ blk_len,
+                                                    unsigned long long* __restrict__ max_span) {
+  __shared__ int64_t s_w[4], s_m[4];
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
   int64_t len = 0;
   if (j < n && flag[j]) {
     out[pos[j]] = (unsigned long long)(int64_t(end_of[j]) << 31 | j);
     len = int64_t(end_of[j]) - j + 1;
   }
-  for (int d = 32; d >= 1; d >>= 1) len += __shfl_xor(len, d, 64);
-  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = len;
+  int64_t mx = len;
+  for (int d = 32; d >= 1; d >>= 1) {
+    len += __shfl_xor(len, d, 64);
+    const int64_t y = __shfl_xor(mx, d, 64);
+    mx = y > mx ? y : mx;
+  }
+  if ((threadIdx.x & 63) == 0) { s_w[threadIdx.x >> 6] = len; s_m[threadIdx.x >> 6] = mx; }
   __syncthreads();
-  if (threadIdx.x == 0) blk_len[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  if (threadIdx.x == 0) {
+    blk_len[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    const int64_t m = std::max(std::max(s_m[0], s_m[1]), std::max(s_m[2], s_m[3]));
+    if (m > 0) atomicMax(max_span, (unsigned long long)(m - 1));
+  }
 }
+
+// Completed runs from start order into (completing record, start) order without a device-wide sort.
+// Each start record begins at most one run, so the compacted runs have distinct, increasing starts.
+// Run i's place in the stable order by end: i - #{j < i : e_j > e_i} + #{j > i : e_j < e_i}.  Such a j
+// overlaps run i, so with every run's span e - s <= W: j < i has s_j >= s_i - W, j > i has s_j < e_i <=
+// s_i + W, and (distinct starts) |i - j| <= W.  A workgroup ranks 256 runs against the window of runs
+// [first - W, last + W] staged in LDS (W <= RUNS_ORDER_MAX_W; wider batches take the radix sort).
+constexpr int RUNS_ORDER_MAX_W = 1024;
+__global__ __launch_bounds__(256) void runs_order(const unsigned long long* __restrict__ in, int64_t nm, int w,
+                                                  unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s_r[256 + 2 * RUNS_ORDER_MAX_W];
+  const int64_t b0 = int64_t(blockIdx.x) * 256;
+  const int64_t lo = b0 - w > 0 ? b0 - w : 0, hi = b0 + 256 + w < nm ? b0 + 256 + w : nm;
+  for (int64_t x = lo + threadIdx.x; x < hi; x += 256) s_r[x - lo] = in[x];
+  __syncthreads();
+  const int64_t i = b0 + threadIdx.x;
+  if (i >= nm) return;
+  const unsigned long long me = s_r[i - lo];
+  const int64_t e = int64_t(me >> 31), st = int64_t(me & 0x7FFFFFFFull);
+  int64_t p = i;
+  for (int64_t j = i - 1; j >= lo; j--) {        // earlier starts ending later
+    const unsigned long long r = s_r[j - lo];
+    if (int64_t(r & 0x7FFFFFFFull) < st - w) break;
+    p -= int64_t(r >> 31) > e;
+  }
+  for (int64_t j = i + 1; j < hi; j++) {         // later starts ending earlier
+    const unsigned long long r = s_r[j - lo];
+    if (int64_t(r & 0x7FFFFFFFull) >= e) break;
+    p += int64_t(r >> 31) < e;
+  }
+  out[p] = me;
+}
+
 
 // the CSR of the sorted completed runs from their recorded stage segments (runs_sim with A.segs),
 // entries final stage first (peek, SharedVersionedBufferStoreImpl.java:176-201).  A workgroup owns
@@ -278,12 +322,19 @@ hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hi
 // blk_len: (n + 255) / 256 partial sums, then their exclusive scan in blk_pre with the total in *ent_total
 hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
                                unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
-                               int64_t* scan_tmp, hipStream_t st) {
+                               int64_t* scan_tmp, unsigned long long* max_span, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = (n + 255) / 256;
-  hipLaunchKernelGGL(runs_compact, dim3(unsigned(nb)), dim3(256), 0, st, flag, pos, end_of, n, out, blk_len);
+  hipLaunchKernelGGL(runs_compact, dim3(unsigned(nb)), dim3(256), 0, st, flag, pos, end_of, n, out, blk_len, max_span);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? exclusive_scan(blk_len, nb, blk_pre, ent_total, scan_tmp, st) : e;
+}
+
+hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, hipStream_t st) {
+  if (nm <= 0) return hipSuccess;
+  if (w < 0 || w > RUNS_ORDER_MAX_W) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(runs_order, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, in, nm, w, out);
+  return hipGetLastError();
 }
 
 // order of completed runs: (completing record, start record).  The compacted keys are already in

@@ -70,8 +70,12 @@ def walk(n, seed, lo=-5, hi=6):
     return (100 + np.cumsum(np.random.default_rng(seed).integers(lo, hi, n))).astype(np.int32)
 
 
+@pytest.mark.parametrize("order", ["window", "radix"])
 @pytest.mark.parametrize("nkeys,per_key", [(1, 3000), (300, 40), (5000, 7)])
-def test_c3_stock_random(nkeys, per_key):
+def test_c3_stock_random(nkeys, per_key, order, monkeypatch):
+    """Both orderings of the completed runs: the windowed rank (runs_order, every run spanning at
+    most 1024 records) and rocPRIM's radix sort (KCEP_RUNS_RADIX=1, also taken by wider batches)."""
+    monkeypatch.setenv("KCEP_RUNS_RADIX", "1" if order == "radix" else "0")
     rng = np.random.default_rng(nkeys)
     key = np.repeat(np.arange(nkeys, dtype=np.int32), rng.poisson(per_key, nkeys) + 1)
     val = walk(len(key), nkeys)
