@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict_
   if (pre[t] + cnt[t] > out_cap) return;
   const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
   const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
-  for (int64_t w = threadIdx.x; w < words; w += 256) {
+  for (int64_t w = threadIdx.x; w < words; w += blockDim.x) {
     const int64_t m = w / k;
     out[dst + w] = F.entry(src, aux, m, int(w - m * k));
   }
@@ -183,7 +183,9 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
     return hipGetLastError();
   }
   hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
-  hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, L.tile_pre,
+  static const int gthreads = [] { const char* e = getenv("KCEP_GATHER_THREADS"); const int v = e ? atoi(e) : 0;
+                                   return v == 64 || v == 128 || v == 256 ? v : 256; }();   // A/B knob
+  hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(gthreads), 0, st, L.slots, L.tile_count, L.tile_pre,
                      L.out, L.out_cap, sub, F);
   return hipGetLastError();
 }
