@@ -184,7 +184,7 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   }
   hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
   static const int gthreads = [] { const char* e = getenv("KCEP_GATHER_THREADS"); const int v = e ? atoi(e) : 0;
-                                   return v == 64 || v == 128 || v == 256 ? v : 256; }();   // A/B knob
+                                   return v == 64 || v == 128 || v == 256 ? v : 128; }();   // A/B knob
   hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(gthreads), 0, st, L.slots, L.tile_count, L.tile_pre,
                      L.out, L.out_cap, sub, F);
   return hipGetLastError();
