@@ -125,6 +125,9 @@ typedef struct {
 
 /* Batch flags */
 #define CEP_BATCH_OFFSETS_MONOTONE 1  /* per key and topic, offsets strictly increase (no re-delivery) */
+#define CEP_BATCH_DELIVER 2           /* the caller collects this batch (a processor flush): on stencil / chain
+                                         carry sessions the device hands the matches to pinned host memory as
+                                         part of the push, so cep_collect only waits (one host round trip) */
 
 /* One batch of records, struct-of-arrays, grouped by key (each key's records
  * contiguous and in arrival order).  Replaces a sequence of
@@ -183,6 +186,10 @@ const char* cep_pattern_name(const cep_pattern* p, int32_t name_id);
  * target stage id or -1).  Returns the edge count, or -1 for a bad id. */
 int32_t cep_pattern_stage(const cep_pattern* p, int32_t sid, int32_t* name_id, int32_t* type, int64_t* window_ms,
                           int32_t* ops, int32_t* targets, int32_t cap);
+/* CEP_OK if a session opened with `session_flags` (CEP_SESSION_CARRY for a processor) runs the pattern on
+ * a device path, else CEP_E_UNSUPPORTED with the reason in cep_last_error.  Host-only: the per-query
+ * routing decision of a host (lowerable -> GPU, else the reference CEPProcessor) needs no device. */
+int cep_pattern_check(const cep_pattern* p, int32_t session_flags);
 
 /* --- session: one per stream task (CEPProcessor.init :88-108) --- */
 int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** out);
@@ -220,7 +227,10 @@ int cep_pattern_build_kernels(const cep_pattern* p, int path);
 
 /* --- batch evaluation: replaces NFA.matchPattern per record (NFA.java:134-149) ---
  * Enqueues the match phase on `stream` (a hipStream_t, NULL = default stream)
- * and returns without waiting.  Device-resident batches are read in place. */
+ * and returns without waiting.  Device-resident batches are read in place.  Host batches (CEP_MEM_HOST)
+ * are borrowed only for the call: pageable columns are copied into the session's pinned staging ring
+ * before it returns; columns that are themselves pinned are copied from directly and the call returns
+ * once that copy is done. */
 int cep_push_batch(cep_session* s, const cep_batch* b, void* stream);
 
 /* Number of matches of the last pushed batch, device-resident (int64 on the
@@ -312,6 +322,91 @@ int cep_gather(const void* src, int32_t elem_bytes, const int64_t* perm, int64_t
  * dst (device memory) on `stream`: a per-step slot for an RCCL all-gather of counts that
  * overlaps the next batch (kcep/shard.py CountExchange). */
 int cep_match_count_to(const cep_session* s, int64_t* dst, void* stream);
+
+/* --- IR builder: the lowering of a reference Pattern to the IR cep_compile consumes ---
+ * A host that walks the reference DSL (java/.../pattern/PatternIR.java, over JNI) issues one call per
+ * element of the ancestor chain, first pattern to last, and gets the same bytes kcep/pattern.py
+ * encode_pattern writes for the query:
+ *   cep_irb_select      a Pattern (Pattern.java:42-62: name or NULL for the level's default name
+ *                       Pattern.java:181-183, level, Selected strategy 0..2 or -1 for null
+ *                       Selected.java:48-50, topic or NULL)
+ *   cep_irb_quantifier  StageBuilder.oneOrMore / zeroOrMore / times, PredicateBuilder.optional
+ *   cep_irb_within      PatternBuilder.within (TimeUnit.toMillis)
+ *   cep_irb_where       PredicateBuilder.where / PatternBuilder.and (conj 1) / or (conj 0): pops the
+ *                       top expression (Pattern.andPredicate / orPredicate, Pattern.java:157-169)
+ *   cep_irb_fold        PatternBuilder.fold(state, aggregator): pops the aggregate expression; type 0
+ *                       keeps its static type, else CEP_T_* is the boxed result type
+ * Matcher / aggregator bodies go on an expression stack in postfix order (children first).  Java's
+ * static typing is applied as it is pushed (binary numeric promotion i32 < i64 < f64; booleans only
+ * from comparisons, logic and topic tests): a type error fails that call with CEP_E_BAD_IR.  A body
+ * the host cannot express with these calls (an opaque lambda) never reaches the builder: that query
+ * stays on the reference CPU path. */
+#define CEP_T_BOOL 0
+/* expression operators (cep_irb_op) and event accessors (cep_irb_event) */
+#define CEP_OP_EV_KEY 0x11
+#define CEP_OP_EV_TS 0x12
+#define CEP_OP_EV_OFFSET 0x14
+#define CEP_OP_EV_PARTITION 0x15
+#define CEP_OP_NOT 0x30
+#define CEP_OP_AND 0x31
+#define CEP_OP_OR 0x32
+#define CEP_OP_ADD 0x40
+#define CEP_OP_SUB 0x41
+#define CEP_OP_MUL 0x42
+#define CEP_OP_DIV 0x43     /* Java '/': truncating for integers, ArithmeticException on / 0 */
+#define CEP_OP_REM 0x44
+#define CEP_OP_NEG 0x45
+#define CEP_OP_EQ 0x50
+#define CEP_OP_NE 0x51
+#define CEP_OP_LT 0x52
+#define CEP_OP_LE 0x53
+#define CEP_OP_GT 0x54
+#define CEP_OP_GE 0x55
+/* SequenceMatcher reductions (cep_irb_seq) over the partial Sequence (SequenceMatcher.java:21-26) */
+#define CEP_SEQ_AVG 0       /* IntSummaryStatistics.getAverage over every event */
+#define CEP_SEQ_SUM 1       /* mapToLong(..).sum() / DoubleStream.sum() */
+#define CEP_SEQ_COUNT 2
+#define CEP_SEQ_MIN 3
+#define CEP_SEQ_MAX 4
+#define CEP_SEQ_FIRST 5     /* getByName(stage).getEvents(): the TreeSet's first / last event */
+#define CEP_SEQ_LAST 6
+
+typedef struct cep_irb cep_irb;
+/* A builder over the value schema: n_cols column types (CEP_T_I32 / I64 / F64). */
+int cep_irb_new(const int32_t* col_types, int32_t n_cols, cep_irb** out);
+void cep_irb_free(cep_irb* b);
+/* Interns a topic name (kcep/pattern.py Schema.topic_id: ids in first-use order); returns its id, the
+ * id a host's records of that topic carry in cep_batch.topic.  Negative on error. */
+int32_t cep_irb_topic(cep_irb* b, const char* topic);
+int32_t cep_irb_topic_count(const cep_irb* b);
+const char* cep_irb_topic_name(const cep_irb* b, int32_t id);
+int cep_irb_select(cep_irb* b, const char* name, int32_t level, int32_t strategy, const char* topic);
+int cep_irb_quantifier(cep_irb* b, int32_t one_or_more, int32_t optional, int32_t times);
+int cep_irb_within(cep_irb* b, int64_t window_ms);
+/* constants: type CEP_T_BOOL (i != 0 is true), CEP_T_I32 / CEP_T_I64 (i), CEP_T_F64 (d) */
+int cep_irb_const(cep_irb* b, int32_t type, int64_t i, double d);
+/* Event.value() / a named field: the schema's column `col` */
+int cep_irb_field(cep_irb* b, int32_t col);
+/* Event.timestamp() / offset() / partition() (CEP_OP_EV_*); CEP_OP_EV_KEY reads the batch's key id */
+int cep_irb_event(cep_irb* b, int32_t what);
+/* Event.topic().equals(topic) (Matcher.TopicPredicate, Matcher.java:104-120) */
+int cep_irb_topic_eq(cep_irb* b, const char* topic);
+/* States.get(name) as a boxed `type` (or_else = 0), or States.getOrElse(name, <popped default>)
+ * (States.java:56-73) */
+int cep_irb_state(cep_irb* b, const char* name, int32_t type, int32_t or_else);
+/* the `curr` argument of Aggregator.aggregate (Aggregator.java:27-29) as a boxed `type` */
+int cep_irb_curr(cep_irb* b, int32_t type);
+/* a reduction CEP_SEQ_* over column `col` of the partial sequence, or of one stage's events (stage
+ * NULL: every event; CEP_SEQ_COUNT ignores col) */
+int cep_irb_seq(cep_irb* b, int32_t kind, int32_t col, const char* stage);
+/* pops one (CEP_OP_NOT, CEP_OP_NEG) or two operands (left below right) and pushes the result */
+int cep_irb_op(cep_irb* b, int32_t op);
+/* Java's (int) / (long) / (double) cast of the top */
+int cep_irb_cast(cep_irb* b, int32_t type);
+int cep_irb_where(cep_irb* b, int32_t conj);
+int cep_irb_fold(cep_irb* b, const char* state, int32_t type);
+/* Serialises the chain (buf == NULL: only *needed).  The builder stays valid. */
+int cep_irb_finish(cep_irb* b, uint8_t* buf, size_t cap, size_t* needed);
 
 const char* cep_last_error(void);
 const char* cep_version(void);

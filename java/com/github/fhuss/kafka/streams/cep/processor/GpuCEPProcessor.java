@@ -1,0 +1,366 @@
+/*
+ * GpuCEPProcessor.java -- drop-in for the reference CEPProcessor
+ * (core/src/main/java/com/github/fhuss/kafka/streams/cep/processor/CEPProcessor.java:46-171)
+ * that hands records to libkcep.so (include/kcep.h) in batches through JNI (jni/kcep_jni.c).
+ *
+ * NOT BUILT in this repository: the image has no JDK and no Kafka jars (SURVEY.md §8c).  It is
+ * the Java twin of kafkastreams-cep_amd/kcep/processor.py, which the GPU tests exercise; the JNI
+ * shim it calls is compiled and driven call-for-call, in the order flush() makes the calls, by
+ * tests/test_jni_gpu.py (against a stub jni.h, tests/jni_stub/).  It is written against Kafka
+ * Streams 1.1's Processor API like the reference (pom.xml:58).
+ *
+ * Wiring: org.apache.kafka.streams.kstream.internals.GpuCEPStreamImpl.query (java/org/...) lowers the
+ * query's Pattern with PatternIR.encode (java/.../pattern/PatternIR.java) and, when some device path
+ * runs it, adds () -> new GpuCEPProcessor<>(queryName, ir, topics, schema, ...) instead of the
+ * reference's () -> new CEPProcessor<>(queryName, pattern) (kint/CEPStreamImpl.java:83-84); the three
+ * state stores are not needed (the device keeps every key's NFA between batches, CEP_SESSION_CARRY).
+ * Queries PatternIR cannot lower keep the reference CEPProcessor.
+ *
+ * Record context: matches are forwarded from flush(), so a downstream processor that reads
+ * context().timestamp() / topic() / offset() sees the record or punctuation that triggered the flush,
+ * not the completing record the reference forwards from (CEPProcessor.java:148).  The Sequence itself
+ * carries each event's own (topic, partition, offset, timestamp).
+ */
+package com.github.fhuss.kafka.streams.cep.processor;
+
+import com.github.fhuss.kafka.streams.cep.Event;
+import com.github.fhuss.kafka.streams.cep.Sequence;
+import org.apache.kafka.streams.processor.Processor;
+import org.apache.kafka.streams.processor.ProcessorContext;
+import org.apache.kafka.streams.processor.PunctuationType;
+
+import java.util.ArrayList;
+import java.util.Arrays;
+import java.util.HashMap;
+import java.util.HashSet;
+import java.util.LinkedHashSet;
+import java.util.List;
+import java.util.Map;
+import java.util.Objects;
+import java.util.Set;
+
+public class GpuCEPProcessor<K, V> implements Processor<K, V> {
+
+    static { System.loadLibrary("kcep_jni"); }      // links libkcep.so
+
+    /** Turns a record value into the pattern's typed columns (kcep/ingest.py ColumnDecoder). */
+    public interface ValueDecoder<V> {
+        int columns();
+        /** column types: 1 = int32, 2 = int64, 3 = double (CEP_T_*). */
+        int type(int column);
+        long longField(V value, int column);        // int32 / int64 columns
+        double doubleField(V value, int column);    // double columns
+    }
+
+    // ---- native entry points (jni/kcep_jni.c), one per kcep.h call ----
+    private static native long cepCompile(byte[] ir);                                   // cep_compile
+    private static native String[] cepStageNames(long pattern);                          // cep_pattern_name
+    private static native long cepSessionOpen(long pattern, int device, int mode, long maxEvents,
+                                              int flags, long maxKeys, long maxKeyWords); // cep_session_open
+    private static native int cepSessionPath(long session);                              // cep_session_path
+    /** cep_push_batch + cep_collect (the host arrays are borrowed until the batch is done). */
+    private static native int cepPushBatch(long session, int n, int[] keyId, int[] topic, int[] partition,
+                                           long[] offset, long[] ts, int[] colTypes, Object[] cols, int flags);
+    /** cep_collect of the pushed batch (no device work: the CSR is the one cepPushBatch collected):
+     *  fills the CSR arrays (null to size them), returns n_matches or -(error code). */
+    private static native long cepCollect(long session, long[] sizes, long[] matchRecord, int[] matchKey,
+                                          long[] entOff, int[] entName, long[] entRecord);
+    /** cep_batch_errors: (stream position, code) pairs of every failing key of the last batch. */
+    private static native long[] cepBatchErrors(long session);
+    private static native long cepStreamPosition(long session);                          // cep_stream_position
+    private static native byte[] cepStateExport(long session, int keyLo, int keyHi);     // cep_state_export
+    private static native int cepStateImport(long session, byte[] state);                // cep_state_import
+    private static native byte[][] cepStateEvict(long session, int[] keys);              // cep_state_evict
+    private static native int cepStateImportKeys(long session, byte[][] blobs, int[] keys); // cep_state_import_keys
+    private static native long[] cepStatePositions(byte[] blob);                         // cep_state_positions
+    private static native int cepSetMaxKeyWords(long session, long words);               // cep_session_set_max_key_words
+    private static native void cepSessionClose(long session);
+    private static native void cepPatternFree(long pattern);
+    private static native String cepLastError();
+
+    private static final int CEP_MODE_PROCESSOR = 1, CEP_SESSION_CARRY = 1, CEP_E_RUN_CAPACITY = 9;
+    private static final int CEP_PATH_STENCIL = 1, CEP_PATH_CHAIN = 3, CEP_PATH_RUNS = 4, CEP_BATCH_OFFSETS_MONOTONE = 1;
+    private static final int CEP_BATCH_DELIVER = 2;                // collected at once: matches delivered to host memory
+
+    private final String queryName;
+    private final byte[] ir;
+    private final ValueDecoder<V> decoder;
+    private final int batchSize;
+    private final int maxKeys;
+    private final long maxKeyWords;
+    private ProcessorContext context;
+    private long pattern, session;
+    private int path;
+    private String[] names;
+
+    // key interning: the session holds maxKeys dense ids; the least recently used keys are spilled
+    // to the host (cepStateEvict) and re-admitted under a free id (cepStateImportKeys), so the keys
+    // over the stream's life are unbounded like the reference's NFAStore (NFAStoreImpl.java:34-85)
+    private final Map<K, Integer> keyIds = new HashMap<>();
+    private final Map<Integer, K> idKeys = new HashMap<>();
+    private final List<Integer> freeIds = new ArrayList<>();
+    private int nextId = 0;
+    private long[] lastUsed = new long[0];
+    private long flushes = 0;
+    private final Map<K, byte[]> spilled = new HashMap<>();
+    private final Map<K, long[]> spilledPositions = new HashMap<>();
+    private final Map<String, Integer> topicIds = new HashMap<>();
+    // stencil / chain sessions: CEPProcessor.checkHighWaterMark applied on the host, per (key, topic)
+    private final Map<K, Map<Integer, Long>> highWater = new HashMap<>();
+    // the batch being filled, in arrival order
+    private final List<Event<K, V>> pending = new ArrayList<>();
+    // events carried runs may still reach, by stream position (pruned from cepStatePositions)
+    private final Map<Long, Event<K, V>> log = new HashMap<>();
+    private int pruneAt;
+
+    /** topics: the topic ids the IR uses, in id order (PatternIR.Lowered.topics); records of other topics
+     *  get the next free ids as they arrive. */
+    public GpuCEPProcessor(String queryName, byte[] ir, List<String> topics, ValueDecoder<V> decoder, int batchSize,
+                           int maxKeys, long maxKeyWords) {
+        this.queryName = queryName.toLowerCase().replace("\\s+", "");   // CEPProcessor.java:83, literal replace
+        this.ir = ir;
+        for (String t : topics) topicIds.putIfAbsent(t, topicIds.size());
+        this.decoder = decoder;
+        this.batchSize = batchSize;
+        this.maxKeys = maxKeys;
+        this.maxKeyWords = maxKeyWords;
+        this.pruneAt = Math.max(1 << 20, 2 * batchSize);
+    }
+
+    @Override
+    public void init(ProcessorContext context) {                        // CEPProcessor.init :88-108
+        this.context = context;
+        this.pattern = check(cepCompile(ir));
+        this.names = cepStageNames(pattern);
+        this.session = check(cepSessionOpen(pattern, 0, CEP_MODE_PROCESSOR, batchSize, CEP_SESSION_CARRY,
+                                            maxKeys, maxKeyWords));
+        this.path = cepSessionPath(session);
+        // a flush on the stream-time punctuation, as on commit
+        context.schedule(context.appConfigs().containsKey("commit.interval.ms")
+                         ? Long.parseLong(String.valueOf(context.appConfigs().get("commit.interval.ms"))) : 30_000L,
+                         PunctuationType.STREAM_TIME, ts -> flush());
+    }
+
+    @Override
+    public void process(K key, V value) {                               // CEPProcessor.process :134-150
+        if (key == null || value == null) return;                        // :136-138
+        pending.add(new Event<>(key, value, context.timestamp(), context.topic(), context.partition(),
+                                context.offset()));
+        if (pending.size() >= batchSize) flush();
+    }
+
+    @Override
+    @Deprecated
+    public void punctuate(long timestamp) { flush(); }
+
+    @Override
+    public void close() {                                               // CEPProcessor.close :167-170
+        flush();
+        cepSessionClose(session);
+        cepPatternFree(pattern);
+    }
+
+    /** One match of a push: arrival index of its completing record, device key id, traversal. */
+    private static final class Match {
+        final int arrival, key;
+        final int[] names;
+        final long[] records;
+        Match(int arrival, int key, int[] names, long[] records) {
+            this.arrival = arrival; this.key = key; this.names = names; this.records = records;
+        }
+    }
+
+    /** One cep_push_batch of the records at arrival indices idx (ascending), grouped by key id (stable);
+     *  fills matches (emission order) and errors (arrival index, code) pairs. */
+    private void run(List<Event<K, V>> recs, int[] kid, int[] idx, int flags, List<Match> matches, List<long[]> errors) {
+        final int n = idx.length;
+        Integer[] order = new Integer[n];
+        for (int i = 0; i < n; i++) order[i] = idx[i];
+        Arrays.sort(order, (a, b) -> Integer.compare(kid[a], kid[b]));   // stable: arrival order per key
+        int[] keyId = new int[n], topic = new int[n], part = new int[n];
+        long[] off = new long[n], ts = new long[n];
+        int nc = decoder.columns();
+        int[] types = new int[nc];
+        Object[] cols = new Object[nc];
+        for (int c = 0; c < nc; c++) {
+            types[c] = decoder.type(c);
+            cols[c] = types[c] == 1 ? new int[n] : types[c] == 2 ? (Object) new long[n] : new double[n];
+        }
+        final long base = cepStreamPosition(session);
+        for (int j = 0; j < n; j++) {
+            Event<K, V> e = recs.get(order[j]);
+            keyId[j] = kid[order[j]];
+            topic[j] = topicIds.computeIfAbsent(e.topic(), t -> topicIds.size());
+            part[j] = e.partition();
+            off[j] = e.offset();
+            ts[j] = e.timestamp();
+            for (int c = 0; c < nc; c++) {
+                if (types[c] == 1) ((int[]) cols[c])[j] = (int) decoder.longField(e.value(), c);
+                else if (types[c] == 2) ((long[]) cols[c])[j] = decoder.longField(e.value(), c);
+                else ((double[]) cols[c])[j] = decoder.doubleField(e.value(), c);
+            }
+            log.put(base + j, e);
+        }
+        int rc = cepPushBatch(session, n, keyId, topic, part, off, ts, types, cols, flags | CEP_BATCH_DELIVER);
+        if (rc != 0) throw new IllegalStateException(queryName + ": " + cepLastError());
+        long[] sizes = new long[2];
+        cepCollect(session, sizes, null, null, null, null, null);         // sizes only (no device work)
+        int nm = (int) sizes[0], ne = (int) sizes[1];
+        long[] mrec = new long[nm], eoff = new long[nm + 1], erec = new long[ne];
+        int[] mkey = new int[nm], ename = new int[ne];
+        long r = cepCollect(session, sizes, mrec, mkey, eoff, ename, erec);
+        for (int m = 0; m < nm; m++) {
+            int a = (int) eoff[m], b = (int) eoff[m + 1];
+            matches.add(new Match(order[(int) (mrec[m] - base)], mkey[m], Arrays.copyOfRange(ename, a, b),
+                                  Arrays.copyOfRange(erec, a, b)));
+        }
+        if (r < 0) {
+            long[] errs = cepBatchErrors(session);
+            for (int i = 0; i < errs.length; i += 2)
+                errors.add(new long[] {order[(int) (errs[i] - base)], errs[i + 1]});
+        }
+    }
+
+    /** Device key id of every record; spills the least recently used keys when the ids run out. */
+    private int[] keyIds(List<Event<K, V>> recs) {
+        flushes++;
+        Set<K> want = new LinkedHashSet<>();
+        for (Event<K, V> e : recs) want.add(e.key());
+        if (want.size() > maxKeys)
+            throw new IllegalStateException(queryName + ": one batch holds more distinct keys than maxKeys");
+        List<K> fresh = new ArrayList<>();
+        for (K k : want) if (!keyIds.containsKey(k)) fresh.add(k);
+        int shortBy = fresh.size() - freeIds.size() - (maxKeys - nextId);
+        if (shortBy > 0) spill(Math.max(shortBy, maxKeys / 8), want);
+        List<byte[]> admitBlobs = new ArrayList<>();
+        List<Integer> admitIds = new ArrayList<>();
+        for (K k : fresh) {
+            int id = freeIds.isEmpty() ? nextId++ : freeIds.remove(freeIds.size() - 1);
+            keyIds.put(k, id);
+            idKeys.put(id, k);
+            byte[] blob = spilled.remove(k);
+            spilledPositions.remove(k);
+            if (blob != null) { admitBlobs.add(blob); admitIds.add(id); }
+        }
+        if (!admitIds.isEmpty()) {
+            int[] ids = new int[admitIds.size()];
+            for (int i = 0; i < ids.length; i++) ids[i] = admitIds.get(i);
+            int rc = cepStateImportKeys(session, admitBlobs.toArray(new byte[0][]), ids);
+            if (rc != 0) throw new IllegalStateException(queryName + ": " + cepLastError());
+        }
+        if (lastUsed.length < nextId) lastUsed = Arrays.copyOf(lastUsed, Math.max(nextId, 2 * lastUsed.length));
+        int[] kid = new int[recs.size()];
+        for (int i = 0; i < kid.length; i++) {
+            kid[i] = keyIds.get(recs.get(i).key());
+            lastUsed[kid[i]] = flushes;
+        }
+        return kid;
+    }
+
+    private void spill(int count, Set<K> busy) {
+        List<Integer> cand = new ArrayList<>(idKeys.keySet());
+        cand.removeIf(id -> busy.contains(idKeys.get(id)));
+        cand.sort((a, b) -> a.equals(b) ? 0 : lastUsed[a] != lastUsed[b] ? Long.compare(lastUsed[a], lastUsed[b])
+                                                                          : Integer.compare(a, b));
+        if (cand.size() > count) cand = cand.subList(0, count);
+        if (cand.isEmpty()) return;
+        int[] ids = new int[cand.size()];
+        for (int i = 0; i < ids.length; i++) ids[i] = cand.get(i);
+        byte[][] blobs = cepStateEvict(session, ids);
+        if (blobs == null) throw new IllegalStateException(queryName + ": " + cepLastError());
+        for (int i = 0; i < ids.length; i++) {
+            K k = idKeys.remove(ids[i]);
+            keyIds.remove(k);
+            freeIds.add(ids[i]);
+            if (blobs[i].length > 0) {                                   // a key without state starts afresh anyway
+                spilled.put(k, blobs[i]);
+                spilledPositions.put(k, cepStatePositions(blobs[i]));
+            }
+        }
+    }
+
+    /** One cep_push_batch of the pending records, then forward in arrival order. */
+    public void flush() {
+        if (pending.isEmpty()) return;
+        List<Event<K, V>> recs = new ArrayList<>(pending);
+        pending.clear();
+        int flags = 0;
+        if (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN || path == CEP_PATH_RUNS) {
+            // the stencil / chain / runs paths carry each key's records (its last K-1, or those from
+            // its oldest open run on), not its NFA: the high-water-mark rule
+            // (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the batch
+            // is declared clean.  Every admitted record is processed and moves the mark (a record that
+            // throws fails the task anyway).
+            List<Event<K, V>> kept = new ArrayList<>(recs.size());
+            for (Event<K, V> e : recs) {
+                Map<Integer, Long> hw = highWater.computeIfAbsent(e.key(), k -> new HashMap<>());
+                int t = topicIds.computeIfAbsent(e.topic(), x -> topicIds.size());
+                Long mark = hw.get(t);
+                if (mark != null && e.offset() < mark) continue;
+                hw.put(t, e.offset() + 1);
+                kept.add(e);
+            }
+            recs = kept;
+            flags = CEP_BATCH_OFFSETS_MONOTONE;
+            if (recs.isEmpty()) return;
+        }
+        final int n = recs.size();
+        final int[] kid = keyIds(recs);
+        int[] all = new int[n];
+        for (int i = 0; i < n; i++) all[i] = i;
+        List<Match> matches = new ArrayList<>();
+        List<long[]> errors = new ArrayList<>();
+        run(recs, kid, all, flags, matches, errors);
+        // keys over the per-key workspace cap come back with their state as of the batch start: their
+        // records are pushed again with the cap lifted, so that every record is processed (:134-150)
+        Set<Integer> cap = new HashSet<>();
+        for (long[] e : errors) if (e[1] == CEP_E_RUN_CAPACITY) cap.add(kid[(int) e[0]]);
+        if (!cap.isEmpty()) {
+            matches.removeIf(m -> cap.contains(m.key));
+            errors.removeIf(e -> e[1] == CEP_E_RUN_CAPACITY);
+            int[] idx = Arrays.stream(all).filter(i -> cap.contains(kid[i])).toArray();
+            List<long[]> errors2 = new ArrayList<>();
+            cepSetMaxKeyWords(session, 0L);
+            try {
+                run(recs, kid, idx, flags, matches, errors2);
+            } finally {
+                cepSetMaxKeyWords(session, maxKeyWords);
+            }
+            for (long[] e : errors2)
+                if (e[1] == CEP_E_RUN_CAPACITY)
+                    throw new IllegalStateException(queryName + ": a key outgrew the whole device pool at record " + e[0]);
+            errors.addAll(errors2);
+        }
+        // where the reference would have thrown: the first failing record in arrival order
+        long limit = Long.MAX_VALUE;
+        long code = 0;
+        for (long[] e : errors) if (e[0] < limit) { limit = e[0]; code = e[1]; }
+        // forward in arrival order of the completing record (stable within one record)
+        matches.sort((a, b) -> Integer.compare(a.arrival, b.arrival));
+        for (Match m : matches) {
+            if (m.arrival >= limit) break;
+            Sequence.Builder<K, V> b = Sequence.newBuilder();
+            for (int i = 0; i < m.names.length; i++) b.add(names[m.names[i]], log.get(m.records[i]));
+            context.forward(recs.get(m.arrival).key(), b.build(true));  // Sequence.java:210-223
+        }
+        if (limit != Long.MAX_VALUE)
+            throw new IllegalStateException(queryName + ": reference exception " + code + " at record " + limit);
+        if (log.size() >= pruneAt) prune();
+    }
+
+    /** Drop the records no carried run (on the device or spilled) can reach any more. */
+    private void prune() {
+        byte[] state = cepStateExport(session, 0, Integer.MAX_VALUE);
+        if (state == null) throw new IllegalStateException(queryName + ": " + cepLastError());
+        Set<Long> keep = new HashSet<>();
+        for (long p : cepStatePositions(state)) keep.add(p);
+        for (long[] ps : spilledPositions.values()) for (long p : ps) keep.add(p);
+        log.keySet().removeIf(p -> !keep.contains(p));
+        pruneAt = Math.max(Math.max(1 << 20, 2 * batchSize), 2 * log.size());
+    }
+
+    private static long check(long handle) {
+        if (handle < 0) throw new IllegalStateException(cepLastError());
+        return handle;
+    }
+}

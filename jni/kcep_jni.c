@@ -84,12 +84,16 @@ JNIEXPORT jint JNICALL CLS(cepPushBatch)(JNIEnv* env, jclass c, jlong session, j
   b.mem = CEP_MEM_HOST;
   b.cols = (const void* const*)(ptrs + 5);
   b.flags = (uint32_t)flags;
+  /* cep_push_batch borrows host columns only for the call (it copies them into the session's pinned
+     staging ring before it returns), so the arrays are released -- and the JVM's GC unblocked --
+     before the batch's device work is waited for */
   int rc = cep_push_batch(S(session), &b, NULL);
-  if (rc == CEP_OK) {                      /* the push is asynchronous: the host arrays must outlive it */
+  for (jsize i = 5 + nc - 1; i >= 0; i--) (*env)->ReleasePrimitiveArrayCritical(env, arrs[i], ptrs[i], JNI_ABORT);
+  for (jsize i = 0; i < nc; i++) (*env)->DeleteLocalRef(env, arrs[5 + i]);
+  if (rc == CEP_OK) {
     cep_matches m;
     rc = cep_collect(S(session), &m);      /* waits; the CSR stays library-owned until the next push, and */
   }                                        /* cepCollect's cep_collect calls return it without device work */
-  for (jsize i = 5 + nc - 1; i >= 0; i--) (*env)->ReleasePrimitiveArrayCritical(env, arrs[i], ptrs[i], JNI_ABORT);
   return rc;
 }
 
@@ -168,6 +172,7 @@ JNIEXPORT jobjectArray JNICALL CLS(cepStateEvict)(JNIEnv* env, jclass c, jlong s
       jbyteArray b = (*env)->NewByteArray(env, len);
       (*env)->SetByteArrayRegion(env, b, 0, len, (const jbyte*)(blobs + offs[i]));
       (*env)->SetObjectArrayElement(env, out, i, b);
+      (*env)->DeleteLocalRef(env, b);      /* one live local ref per key would overflow the frame */
     }
   }
   free(offs);
@@ -178,20 +183,31 @@ JNIEXPORT jint JNICALL CLS(cepStateImportKeys)(JNIEnv* env, jclass c, jlong sess
                                                jintArray keys) {
   const jsize n = (*env)->GetArrayLength(env, keys);
   if ((*env)->GetArrayLength(env, blobs) != n) return CEP_E_ARG;
-  jbyteArray* arr = malloc(sizeof(jbyteArray) * (size_t)(n ? n : 1));
-  const void** ptrs = malloc(sizeof(void*) * (size_t)(n ? n : 1));
+  /* the blobs are copied into one buffer, each element's local ref dropped at once (a spill re-admits
+     up to maxKeys / 8 keys: one live ref per key would overflow the JNI local frame) */
   size_t* lens = malloc(sizeof(size_t) * (size_t)(n ? n : 1));
-  if (!arr || !ptrs || !lens) { free(arr); free((void*)ptrs); free(lens); return CEP_E_ARG; }
+  size_t* offs = malloc(sizeof(size_t) * (size_t)(n + 1));
+  const void** ptrs = malloc(sizeof(void*) * (size_t)(n ? n : 1));
+  if (!lens || !offs || !ptrs) { free(lens); free(offs); free((void*)ptrs); return CEP_E_ARG; }
+  offs[0] = 0;
   for (jsize i = 0; i < n; i++) {
-    arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, blobs, i);
-    lens[i] = (size_t)(*env)->GetArrayLength(env, arr[i]);
-    ptrs[i] = (*env)->GetByteArrayElements(env, arr[i], NULL);
+    jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, blobs, i);
+    lens[i] = (size_t)(*env)->GetArrayLength(env, a);
+    offs[i + 1] = offs[i] + lens[i];
+    (*env)->DeleteLocalRef(env, a);
+  }
+  uint8_t* all = malloc(offs[n] ? offs[n] : 1);
+  if (!all) { free(lens); free(offs); free((void*)ptrs); return CEP_E_ARG; }
+  for (jsize i = 0; i < n; i++) {
+    jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, blobs, i);
+    (*env)->GetByteArrayRegion(env, a, 0, (jsize)lens[i], (jbyte*)(all + offs[i]));
+    (*env)->DeleteLocalRef(env, a);
+    ptrs[i] = all + offs[i];
   }
   jint* k = (*env)->GetIntArrayElements(env, keys, NULL);
   int rc = cep_state_import_keys(S(session), ptrs, lens, (const int32_t*)k, n);
   (*env)->ReleaseIntArrayElements(env, keys, k, JNI_ABORT);
-  for (jsize i = 0; i < n; i++) (*env)->ReleaseByteArrayElements(env, arr[i], (jbyte*)ptrs[i], JNI_ABORT);
-  free(arr); free((void*)ptrs); free(lens);
+  free(all); free(lens); free(offs); free((void*)ptrs);
   return rc;
 }
 
@@ -223,3 +239,143 @@ JNIEXPORT void JNICALL CLS(cepPatternFree)(JNIEnv* env, jclass c, jlong pattern)
 }
 
 JNIEXPORT jstring JNICALL CLS(cepLastError)(JNIEnv* env, jclass c) { return (*env)->NewStringUTF(env, cep_last_error()); }
+
+/* ---- PatternIR (java/com/github/fhuss/kafka/streams/cep/pattern/PatternIR.java): the reference DSL
+   lowered through the IR builder of kcep.h (cep_irb_*).  Strings travel as UTF-8 byte[] (null for a
+   null Java string), so the IR carries the bytes String.getBytes(UTF_8) gives, not JNI's modified
+   UTF-8; every call returns a kcep status code. ---- */
+#define IRB(name) Java_com_github_fhuss_kafka_streams_cep_pattern_PatternIR_##name
+
+static cep_irb* B(jlong h) { return (cep_irb*)(intptr_t)h; }
+
+/* a NUL-terminated copy of a UTF-8 byte[] (NULL for null); free() it */
+static char* utf8(JNIEnv* env, jbyteArray a) {
+  if (!a) return NULL;
+  const jsize n = (*env)->GetArrayLength(env, a);
+  char* s = malloc((size_t)n + 1);
+  if (!s) return NULL;
+  (*env)->GetByteArrayRegion(env, a, 0, n, (jbyte*)s);
+  s[n] = 0;
+  return s;
+}
+
+JNIEXPORT jlong JNICALL IRB(irbNew)(JNIEnv* env, jclass c, jintArray col_types) {
+  const jsize n = (*env)->GetArrayLength(env, col_types);
+  jint* t = (*env)->GetIntArrayElements(env, col_types, NULL);
+  cep_irb* b = NULL;
+  int rc = cep_irb_new((const int32_t*)t, n, &b);
+  (*env)->ReleaseIntArrayElements(env, col_types, t, JNI_ABORT);
+  return rc ? -(jlong)rc : (jlong)(intptr_t)b;
+}
+
+JNIEXPORT void JNICALL IRB(irbFree)(JNIEnv* env, jclass c, jlong b) { cep_irb_free(B(b)); }
+
+JNIEXPORT jint JNICALL IRB(irbTopic)(JNIEnv* env, jclass c, jlong b, jbyteArray topic) {
+  char* t = utf8(env, topic);
+  jint id = t ? cep_irb_topic(B(b), t) : -CEP_E_ARG;
+  free(t);
+  return id;
+}
+
+JNIEXPORT jint JNICALL IRB(irbSelect)(JNIEnv* env, jclass c, jlong b, jbyteArray name, jint level, jint strategy,
+                                      jbyteArray topic) {
+  char* n = utf8(env, name);
+  char* t = utf8(env, topic);
+  jint rc = cep_irb_select(B(b), n, level, strategy, t);
+  free(n);
+  free(t);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL IRB(irbQuantifier)(JNIEnv* env, jclass c, jlong b, jint one_or_more, jint optional, jint times) {
+  return cep_irb_quantifier(B(b), one_or_more, optional, times);
+}
+
+JNIEXPORT jint JNICALL IRB(irbWithin)(JNIEnv* env, jclass c, jlong b, jlong ms) { return cep_irb_within(B(b), ms); }
+
+JNIEXPORT jint JNICALL IRB(irbConst)(JNIEnv* env, jclass c, jlong b, jint type, jlong i, jdouble d) {
+  return cep_irb_const(B(b), type, i, d);
+}
+
+JNIEXPORT jint JNICALL IRB(irbField)(JNIEnv* env, jclass c, jlong b, jint col) { return cep_irb_field(B(b), col); }
+
+JNIEXPORT jint JNICALL IRB(irbEvent)(JNIEnv* env, jclass c, jlong b, jint what) { return cep_irb_event(B(b), what); }
+
+JNIEXPORT jint JNICALL IRB(irbTopicEq)(JNIEnv* env, jclass c, jlong b, jbyteArray topic) {
+  char* t = utf8(env, topic);
+  jint rc = cep_irb_topic_eq(B(b), t);
+  free(t);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL IRB(irbState)(JNIEnv* env, jclass c, jlong b, jbyteArray name, jint type, jint or_else) {
+  char* n = utf8(env, name);
+  jint rc = cep_irb_state(B(b), n, type, or_else);
+  free(n);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL IRB(irbCurr)(JNIEnv* env, jclass c, jlong b, jint type) { return cep_irb_curr(B(b), type); }
+
+JNIEXPORT jint JNICALL IRB(irbSeq)(JNIEnv* env, jclass c, jlong b, jint kind, jint col, jbyteArray stage) {
+  char* s = utf8(env, stage);
+  jint rc = cep_irb_seq(B(b), kind, col, s);
+  free(s);
+  return rc;
+}
+
+JNIEXPORT jint JNICALL IRB(irbOp)(JNIEnv* env, jclass c, jlong b, jint op) { return cep_irb_op(B(b), op); }
+
+JNIEXPORT jint JNICALL IRB(irbCast)(JNIEnv* env, jclass c, jlong b, jint type) { return cep_irb_cast(B(b), type); }
+
+JNIEXPORT jint JNICALL IRB(irbWhere)(JNIEnv* env, jclass c, jlong b, jint conj) { return cep_irb_where(B(b), conj); }
+
+JNIEXPORT jint JNICALL IRB(irbFold)(JNIEnv* env, jclass c, jlong b, jbyteArray state, jint type) {
+  char* s = utf8(env, state);
+  jint rc = cep_irb_fold(B(b), s, type);
+  free(s);
+  return rc;
+}
+
+JNIEXPORT jbyteArray JNICALL IRB(irbFinish)(JNIEnv* env, jclass c, jlong b) {
+  size_t need = 0;
+  if (cep_irb_finish(B(b), NULL, 0, &need)) return NULL;
+  uint8_t* buf = malloc(need ? need : 1);
+  jbyteArray out = NULL;
+  if (buf && cep_irb_finish(B(b), buf, need, &need) == CEP_OK) {
+    out = (*env)->NewByteArray(env, (jsize)need);
+    (*env)->SetByteArrayRegion(env, out, 0, (jsize)need, (const jbyte*)buf);
+  }
+  free(buf);
+  return out;
+}
+
+/* the ids the builder gave the topics it met, in id order: the processor's topic ids must agree */
+JNIEXPORT jobjectArray JNICALL IRB(irbTopics)(JNIEnv* env, jclass c, jlong b) {
+  const int32_t n = cep_irb_topic_count(B(b));
+  if (n < 0) return NULL;
+  jobjectArray out = (*env)->NewObjectArray(env, n, (*env)->FindClass(env, "java/lang/String"), NULL);
+  for (int32_t i = 0; i < n; i++) {
+    jstring s = (*env)->NewStringUTF(env, cep_irb_topic_name(B(b), i));
+    (*env)->SetObjectArrayElement(env, out, i, s);
+    (*env)->DeleteLocalRef(env, s);
+  }
+  return out;
+}
+
+/* cep_compile + cep_pattern_check(CEP_SESSION_CARRY): 0 if a GpuCEPProcessor can run the IR, else the
+   status (CEP_E_INVALID_PATTERN, CEP_E_UNSUPPORTED, CEP_E_BAD_IR) with the reason in irbLastError */
+JNIEXPORT jint JNICALL IRB(irbProbe)(JNIEnv* env, jclass c, jbyteArray ir) {
+  const jsize n = (*env)->GetArrayLength(env, ir);
+  jbyte* p = (*env)->GetByteArrayElements(env, ir, NULL);
+  cep_pattern* pat = NULL;
+  int rc = cep_compile((const uint8_t*)p, (size_t)n, &pat);
+  (*env)->ReleaseByteArrayElements(env, ir, p, JNI_ABORT);
+  if (rc == CEP_OK) {
+    rc = cep_pattern_check(pat, CEP_SESSION_CARRY);
+    cep_pattern_free(pat);
+  }
+  return rc;
+}
+
+JNIEXPORT jstring JNICALL IRB(irbLastError)(JNIEnv* env, jclass c) { return (*env)->NewStringUTF(env, cep_last_error()); }

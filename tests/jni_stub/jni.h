@@ -52,6 +52,8 @@ struct JNINativeInterface_ {
   void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
   void* (*GetPrimitiveArrayCritical)(JNIEnv*, jarray, jboolean*);
   void (*ReleasePrimitiveArrayCritical)(JNIEnv*, jarray, void*, jint);
+  void (*GetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, jbyte*);
+  void (*DeleteLocalRef)(JNIEnv*, jobject);
 };
 
 #endif

@@ -62,11 +62,18 @@ static void SetLongArrayRegion(JNIEnv* e, jlongArray a, jsize at, jsize n, const
 static void* GetPrimitiveArrayCritical(JNIEnv* e, jarray a, jboolean* c) { return pin(a); }
 static void ReleasePrimitiveArrayCritical(JNIEnv* e, jarray a, void* p, jint mode) { unpin(); }
 
+static void GetByteArrayRegion(JNIEnv* e, jbyteArray a, jsize at, jsize n, jbyte* dst) {
+  memcpy(dst, (const jbyte*)a->data + at, (size_t)n);
+}
+/* local refs are counted, not freed: the tests read arrays the shim has already dropped */
+static long g_deleted = 0;
+static void DeleteLocalRef(JNIEnv* e, jobject o) { g_deleted++; }
+
 static const struct JNINativeInterface_ g_table = {
     FindClass, GetArrayLength, NewObjectArray, GetObjectArrayElement, SetObjectArrayElement, NewStringUTF,
     NewByteArray, NewLongArray, GetByteArrayElements, ReleaseByteArrayElements, GetIntArrayElements,
     ReleaseIntArrayElements, SetByteArrayRegion, SetIntArrayRegion, SetLongArrayRegion, GetPrimitiveArrayCritical,
-    ReleasePrimitiveArrayCritical};
+    ReleasePrimitiveArrayCritical, GetByteArrayRegion, DeleteLocalRef};
 static JNIEnv g_env = &g_table;
 
 /* ---- helpers for the Python side ---- */
@@ -79,3 +86,4 @@ JNIEXPORT jobject mock_obj_get(jobject a, jsize i) { return ((jobject*)a->data)[
 JNIEXPORT void* mock_data(jobject a) { return a ? a->data : NULL; }
 JNIEXPORT jsize mock_len(jobject a) { return a ? a->len : -1; }
 JNIEXPORT long mock_pins(void) { return g_pins; }
+JNIEXPORT long mock_deleted_refs(void) { return g_deleted; }

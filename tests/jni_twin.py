@@ -1,5 +1,5 @@
 """Drives jni/kcep_jni.c (compiled unchanged against tests/jni_stub/) the way
-java/GpuCEPProcessor.java does -- test infrastructure, no JVM in the image.
+java/com/github/fhuss/kafka/streams/cep/processor/GpuCEPProcessor.java does -- test infrastructure, no JVM in the image.
 
 ``JniLib`` wraps every ``native`` method of GpuCEPProcessor.java as a ctypes call of its
 ``Java_..._GpuCEPProcessor_*`` symbol with a mock ``JNIEnv`` (Java arrays are mock objects over
@@ -27,7 +27,7 @@ NATIVES = ["cepCompile", "cepStageNames", "cepSessionOpen", "cepSessionPath", "c
            "cepLastError"]
 
 CEP_MODE_PROCESSOR, CEP_SESSION_CARRY, CEP_E_RUN_CAPACITY = 1, 1, 9
-CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS, CEP_BATCH_OFFSETS_MONOTONE = 1, 3, 4, 1
+CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS, CEP_BATCH_OFFSETS_MONOTONE, CEP_BATCH_DELIVER = 1, 3, 4, 1, 2
 
 
 class JniLib:
@@ -227,7 +227,8 @@ class JavaTwin:
         base = j.cepStreamPosition(self.session)
         for jj, a in enumerate(order):
             self.log[base + jj] = recs[a]
-        rc = j.cepPushBatch(self.session, n, key_id, topic, part, off, ts, np.array(self.types, np.int32), cols, flags)
+        rc = j.cepPushBatch(self.session, n, key_id, topic, part, off, ts, np.array(self.types, np.int32), cols,
+                            flags | CEP_BATCH_DELIVER)
         self.pushes += 1
         if rc != 0:
             raise RuntimeError(f"cepPushBatch {rc}: {j.cepLastError()}")

@@ -23,7 +23,7 @@ def jl():
 
 
 def test_java_natives_match_the_shim(jl):
-    src = open(os.path.join(ROOT, "java", "GpuCEPProcessor.java")).read()
+    src = open(os.path.join(ROOT, "java", "com", "github", "fhuss", "kafka", "streams", "cep", "processor", "GpuCEPProcessor.java")).read()
     java = re.findall(r"private static native [\w\[\]]+ (\w+)\(", src)
     assert sorted(java) == sorted(NATIVES)
     c = open(os.path.join(ROOT, "jni", "kcep_jni.c")).read()

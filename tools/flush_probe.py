@@ -1,0 +1,67 @@
+"""Where a processor flush's fixed cost goes: a C2-shaped stream pushed from host memory through a
+CEP_SESSION_CARRY session in batches of `per` records, each collected (GpuCEPProcessor.flush's
+cep_push_batch + cep_collect), with the host-side time of the push call and of the collect call
+split, for pinned and for pageable (plain numpy) host input.
+
+Usage: flush_probe.py [per=65536] [batches=200]
+Run under `rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --stats` with KCEP_ROCTX=1
+for the device-side split."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kafkastreams-cep_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from kcep import native as N, synth, Schema  # noqa: E402
+
+per = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
+nb = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+n = per * nb
+K = max(1000, n // 100)
+dev = torch.device("cuda", 0)
+key, val, _ = synth.c2_stream_torch(n, K, dev)
+ir = synth.c2_pattern().to_ir(Schema([("value", "i32")]))
+pat = N.CompiledPattern(ir)
+st = torch.cuda.current_stream(dev)
+pk, pv = key.cpu().pin_memory(), val.cpu().pin_memory()
+hk, hv = key.cpu().numpy().copy(), val.cpu().numpy().copy()
+want = None
+
+
+def one_pass(sess, k_ptr, v_ptr):
+    tp = tc = 0.0
+    tot = 0
+    for i in range(nb):
+        a = i * per
+        t0 = time.perf_counter()
+        sess.push(per, k_ptr + 4 * a, [v_ptr + 4 * a], mem=N.MEM_HOST, stream=st.cuda_stream,
+                  flags=N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER)
+        t1 = time.perf_counter()
+        out = sess.collect()
+        t2 = time.perf_counter()
+        tp += t1 - t0
+        tc += t2 - t1
+        tot += len(out["match_record"])
+    return tp, tc, tot
+
+
+for label, kp, vp in (("pinned", pk.data_ptr(), pv.data_ptr()), ("pageable", hk.ctypes.data, hv.ctypes.data)):
+    s = N.Session(pat, per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K)
+    s.set_timing(False)
+    one_pass(s, kp, vp)
+    best = None
+    for _ in range(3):
+        s.state_clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tp, tc, tot = one_pass(s, kp, vp)
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[0]:
+            best = (dt, tp, tc, tot)
+    dt, tp, tc, tot = best
+    want = tot if want is None else want
+    print(f"{label:9s} per={per} batches={nb}: {dt / nb * 1e6:8.1f} us/batch  push {tp / nb * 1e6:7.1f}  "
+          f"collect {tc / nb * 1e6:7.1f}  {n / dt:.3e} events/s  matches {tot} (same: {tot == want})", flush=True)
+    s.close()
