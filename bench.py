@@ -288,6 +288,13 @@ def main():
                 _carry_stream(pat, n, K, key, cols, stream, 0, n_matches, csum, value / world, reps=1, per=b,
                               host=host, collect=True) for b in args.processor_batch]
             del host
+            # the same from pageable host memory, as a JVM heap array reaches the library through JNI
+            # (GetPrimitiveArrayCritical): cep_push_batch copies it into the session's pinned ring
+            pageable = (key.cpu().numpy(), [c.cpu().numpy() for c in cols])
+            line["processor_batches"] += [
+                _carry_stream(pat, n, K, key, cols, stream, 0, n_matches, csum, value / world, reps=1, per=b,
+                              host=pageable, collect=True) for b in args.processor_batch]
+            del pageable
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS) and args.carry_batches > 1:
             line["carry_stream"] = _carry_stream(pat, n, K, key, cols, stream, args.carry_batches, n_matches, csum,
                                                  value / world)
@@ -342,12 +349,20 @@ def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, r
     cs.set_timing(False)
     src_k, src_c = host if host is not None else (key, cols)
     mem = N.MEM_HOST if host is not None else N.MEM_DEVICE
+    pageable = host is not None and not hasattr(src_k, "data_ptr")     # numpy arrays: pageable memory
+
+    def addr(a):
+        return a.ctypes.data if pageable else a.data_ptr()
+
+    def esize(a):
+        return a.itemsize if pageable else a.element_size()
 
     def one_pass(check):
         tot_m, tot_c = 0, 0
         for a, b in zip(bounds[:-1], bounds[1:]):
-            cs.push(b - a, src_k.data_ptr() + 4 * a, [c.data_ptr() + c.element_size() * a for c in src_c],
-                    mem=mem, stream=stream.cuda_stream, flags=N.BATCH_OFFSETS_MONOTONE)
+            cs.push(b - a, addr(src_k) + 4 * a, [addr(c) + esize(c) * a for c in src_c],
+                    mem=mem, stream=stream.cuda_stream,
+                    flags=N.BATCH_OFFSETS_MONOTONE | (N.BATCH_DELIVER if collect else 0))
             if check:
                 m, c = cs.checksum()
                 tot_m, tot_c = tot_m + m, (tot_c + c) & 0xFFFFFFFFFFFFFFFF
@@ -373,7 +388,8 @@ def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, r
            "parity": bool(m == n_matches and c == csum), "matches": int(m)}
     if host is not None or collect:
         # per-batch cost above streaming the batch's records at the resident rate
-        out.update({"host_memory": "pinned" if host is not None else None, "collect_per_batch": collect,
+        out.update({"host_memory": ("pageable" if pageable else "pinned") if host is not None else None,
+                    "collect_per_batch": collect,
                     "us_per_batch": dt * 1e6 / nbat,
                     "overhead_us_per_batch": (dt - n / resident) * 1e6 / nbat})
     cs.close()

@@ -208,7 +208,8 @@ int cep_session_set_timing(cep_session* s, int on);
    ascending position.  cep_collect reports only the earliest in the batch's key-grouped order; a
    host that re-orders a batch by key (GpuCEPProcessor) uses this list to find the first failure in
    arrival order, which is where the reference's process() throws (CEPProcessor.java:134-149).
-   Call with records = codes = NULL for the count.  The runs path reports its first exception only. */
+   Call with records = codes = NULL for the count.  (The runs path lists up to 2^20 failing runs per batch;
+   past that it reports the batch's first exception only.) */
 int cep_batch_errors(const cep_session* s, int64_t* records, int32_t* codes, int64_t cap, int64_t* n);
 /* CEP_SESSION_PROFILE sessions, after a general-path batch: per key segment {key id, live-run
    high-water mark, run evaluations, kernel wall clock (100 MHz ticks), then shader clocks spent in

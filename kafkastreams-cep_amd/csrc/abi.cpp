@@ -32,6 +32,9 @@ hipError_t stencil_post(const int32_t* key, const int32_t* out, int k, int64_t n
                         const StencilProgram* P, unsigned long long* sum, hipStream_t st);
 hipError_t stencil_resolve_launch(const int32_t* key, const int32_t* out, int k, int64_t nm, const StencilCarry& C,
                                   int64_t* pos, const StencilProgram* P, unsigned long long* sum, hipStream_t st);
+hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k, const int64_t* total, int64_t out_cap,
+                                  const StencilCarry& C, int64_t host_cap, int64_t* hdr, int32_t* hkey, int64_t* hpos,
+                                  int32_t* dkey, int64_t* dpos, hipStream_t st);
 
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf);
 hipError_t nfa_wave_launch(const NfaArgs& A, bool grouped, hipStream_t st, const JitModule* j);
@@ -133,6 +136,7 @@ bool wave_ok(const DevProgram& D) {
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
 constexpr NfaCaps kCaps{16, 64, 32, 32, 8, 16};
 constexpr int kMaxRetry = 8;                       // pool doublings before CEP_E_RUN_CAPACITY
+constexpr int64_t kRunsErrCap = int64_t(1) << 20;  // runs path: failing runs listed per batch (cep_batch_errors)
 }  // namespace
 
 struct cep_pattern {
@@ -154,9 +158,21 @@ struct cep_session {
   DBuf prog, out, status, counter, total, sum, mkey, slots;   // status: tile counts + prefixes; counter: scan scratch
   int64_t out_cap = 0;
   const int32_t* d_key = nullptr;
-  // ---- staging of host-resident batches ----
-  DBuf h_key, h_valid, h_topic, h_part, h_off, h_ts;
-  DBuf h_cols[16];
+  // ---- staging of host-resident batches (stage_host): a pinned ring the caller's columns are copied
+  // into in chunks, each chunk moved by one async copy into one packed device image; caller memory
+  // that is itself pinned is copied from directly and the push waits for that copy ----
+  DBuf dstage, h_topic;
+  void* ring[2] = {nullptr, nullptr};
+  size_t ring_cap[2] = {0, 0};
+  hipEvent_t ring_ev[2] = {nullptr, nullptr};
+  int ring_next = 0;
+  hipEvent_t h2d_ev = nullptr;
+  // ---- CEP_BATCH_DELIVER (carry stencil / chain sessions): the matches handed to pinned host memory by
+  // the device during the push; cep_collect then only waits ----
+  void* dl = nullptr;             // {nm, flags} header, host_cap keys, host_cap * k positions
+  int64_t dl_cap = 0;
+  bool delivered = false;
+  bool h2d_wait = false;          // the push copied from pinned caller memory: wait for h2d_ev
   // ---- general workspace ----
   DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_err, r_errrec, r_carry, ents,
       moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec;
@@ -174,7 +190,7 @@ struct cep_session {
   int64_t halo_base = 0;        // stream position of the last stencil batch's record 0
   int64_t cpool_words = 0, cpool_used = 0;
   // ---- deterministic runs workspace ----
-  DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof, r_segs, r_blk;
+  DBuf rk, rk_sorted, rk_tmp, r_len, r_entoff, r_errcode, r_endof, r_segs, r_blk, r_errlist;
   // kernels compiled for the pattern (jit.cpp); null: the built-in interpreting kernels run
   bool jit_on = false;                     // allowed (not CEP_SESSION_INTERPRET / KCEP_JIT=0)
   std::shared_ptr<const JitModule> jit;    // runs path
@@ -244,6 +260,82 @@ StencilCarry carry_args(const cep_session* s) {
                       s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), 0};
 }
 
+// Host-resident batch columns -> one packed device image (s->dstage), 256-B aligned per column.  The
+// caller's memory is borrowed only for the call (kcep.h cep_push_batch):
+//  - pageable memory (a JVM heap array, a numpy buffer) is copied into the session's pinned ring in
+//    chunks of kRingChunk bytes, each chunk moved by one async copy while the next one is filled; the
+//    call returns once the last chunk is in the ring;
+//  - memory that is itself pinned is copied from directly, and the call waits for that copy (the
+//    kernels are already enqueued behind it).
+struct HostArr {
+  const void* src;
+  size_t bytes;
+  const void** dst;               // receives the device address (null src: left null)
+};
+constexpr size_t kRingChunk = size_t(8) << 20;
+
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();      // pageable memory is unknown to the runtime: not an error
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st) {
+  size_t total = 0;
+  std::vector<size_t> at(size_t(na), 0);
+  bool pinned = true;
+  for (int i = 0; i < na; i++) {
+    if (!arrs[i].src || !arrs[i].bytes) continue;
+    at[size_t(i)] = total;
+    total += (arrs[i].bytes + 255) & ~size_t(255);
+    pinned = pinned && host_pinned(arrs[i].src);
+  }
+  if (!total) return CEP_OK;
+  if (s->dstage.ensure(total)) return fail(CEP_E_HIP, "staging allocation failed");
+  uint8_t* dev = s->dstage.as<uint8_t>();
+  for (int i = 0; i < na; i++)
+    if (arrs[i].src && arrs[i].bytes) *arrs[i].dst = dev + at[size_t(i)];
+  if (pinned) {                                       // DMA straight from the caller's pinned memory
+    for (int i = 0; i < na; i++)
+      if (arrs[i].src && arrs[i].bytes)
+        HIPCHECK(hipMemcpyAsync(dev + at[size_t(i)], arrs[i].src, arrs[i].bytes, hipMemcpyHostToDevice, st));
+    if (!s->h2d_ev) HIPCHECK(hipEventCreateWithFlags(&s->h2d_ev, hipEventDisableTiming));
+    HIPCHECK(hipEventRecord(s->h2d_ev, st));
+    s->h2d_wait = true;                               // cep_push_batch waits for it before returning
+    return CEP_OK;
+  }
+  // pageable: through the pinned ring, in chunks so that the copy of one overlaps the filling of the next
+  static const size_t split = [] { const char* e = getenv("KCEP_RING_SPLIT"); return e ? size_t(atoi(e)) : size_t(1); }();
+  const size_t chunk = std::min(kRingChunk, std::max<size_t>(size_t(64) << 10, ((total / std::max<size_t>(split, 1)) + 4095) & ~size_t(4095)));
+  for (size_t c0 = 0; c0 < total; c0 += chunk) {
+    const size_t c1 = std::min(total, c0 + chunk);
+    const int j = s->ring_next;
+    s->ring_next ^= 1;
+    if (s->ring_ev[j]) HIPCHECK(hipEventSynchronize(s->ring_ev[j]));
+    else HIPCHECK(hipEventCreateWithFlags(&s->ring_ev[j], hipEventDisableTiming));
+    const size_t want = std::min(total, chunk);
+    if (s->ring_cap[j] < want) {
+      if (s->ring[j]) HIPCHECK(hipHostFree(s->ring[j]));
+      s->ring[j] = nullptr;
+      s->ring_cap[j] = 0;
+      HIPCHECK(hipHostMalloc(&s->ring[j], want, hipHostMallocDefault));
+      s->ring_cap[j] = want;
+    }
+    uint8_t* h = static_cast<uint8_t*>(s->ring[j]);
+    for (int i = 0; i < na; i++) {                    // the parts of the columns inside [c0, c1)
+      if (!arrs[i].src || !arrs[i].bytes) continue;
+      const size_t a = std::max(c0, at[size_t(i)]), b = std::min(c1, at[size_t(i)] + arrs[i].bytes);
+      if (a < b) memcpy(h + (a - c0), static_cast<const uint8_t*>(arrs[i].src) + (a - at[size_t(i)]), b - a);
+    }
+    HIPCHECK(hipMemcpyAsync(dev + c0, h, c1 - c0, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipEventRecord(s->ring_ev[j], st));
+  }
+  return CEP_OK;
+}
+
 int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const StencilProgram& SP = s->pat->prog.stencil;
   const void* col = b->n_cols ? b->cols[SP.col] : nullptr;
@@ -251,19 +343,13 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int32_t* topic = SP.use_topic ? b->topic : nullptr;
   const size_t vs = type_size(SP.coltype);
   if (b->mem == CEP_MEM_HOST && b->n > 0) {
-    if (s->h_key.ensure(size_t(b->n) * 4) || s->h_cols[0].ensure(size_t(b->n) * vs) ||
-        (SP.use_topic && s->h_topic.ensure(size_t(b->n) * 4)))
-      return fail(CEP_E_HIP, "staging allocation failed");
-    HIPCHECK(hipMemcpyAsync(s->h_key.p, key, size_t(b->n) * 4, hipMemcpyHostToDevice, st));
-    HIPCHECK(hipMemcpyAsync(s->h_cols[0].p, col, size_t(b->n) * vs, hipMemcpyHostToDevice, st));
-    key = s->h_key.as<int32_t>();
-    col = s->h_cols[0].p;
-    if (SP.use_topic) {
-      if (b->topic) HIPCHECK(hipMemcpyAsync(s->h_topic.p, b->topic, size_t(b->n) * 4, hipMemcpyHostToDevice, st));
-      else HIPCHECK(hipMemsetAsync(s->h_topic.p, 0, size_t(b->n) * 4, st));
-      topic = s->h_topic.as<int32_t>();
-    }
-  } else if (SP.use_topic && !b->topic && b->n > 0) {
+    HostArr arrs[3] = {{key, size_t(b->n) * 4, reinterpret_cast<const void**>(&key)},
+                       {col, size_t(b->n) * vs, &col},
+                       {topic, size_t(b->n) * 4, reinterpret_cast<const void**>(&topic)}};
+    int rc = stage_host(s, arrs, SP.use_topic ? 3 : 2, st);
+    if (rc) return rc;
+  }
+  if (SP.use_topic && !topic && b->n > 0) {          // no topic column: every record on topic id 0
     if (s->h_topic.ensure(size_t(b->n) * 4)) return fail(CEP_E_HIP, "staging allocation failed");
     HIPCHECK(hipMemsetAsync(s->h_topic.p, 0, size_t(b->n) * 4, st));
     topic = s->h_topic.as<int32_t>();
@@ -287,18 +373,28 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     s->halo_base = s->base;
     s->base += b->n;
   }
+  if (s->carry && (b->flags & CEP_BATCH_DELIVER)) {   // the matches to pinned host memory, by the device
+    const int k = SP.k;
+    const int64_t host_cap = std::min<int64_t>(s->out_cap, int64_t(1) << 20);
+    if (!s->dl) {
+      const size_t bytes = 8 * (2 + size_t(host_cap + 1) / 2 + 1) + size_t(host_cap) * size_t(k) * 8;   // see hpos
+      HIPCHECK(hipHostMalloc(&s->dl, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+      s->dl_cap = host_cap;
+    }
+    if (s->out_cap > host_cap &&
+        (s->mkey.ensure(size_t(s->out_cap) * 4) || s->opos.ensure(size_t(s->out_cap) * size_t(k) * 8)))
+      return fail(CEP_E_HIP, "allocation failed");
+    int64_t* hdr = static_cast<int64_t*>(s->dl);
+    L.deliver.hdr = hdr;
+    L.deliver.hkey = reinterpret_cast<int32_t*>(hdr + 2);
+    L.deliver.hpos = hdr + 2 + (s->dl_cap + 1) / 2 + 1;
+    L.deliver.dkey = s->mkey.as<int32_t>();
+    L.deliver.dpos = s->opos.as<int64_t>();
+    L.deliver.host_cap = s->dl_cap;
+    s->delivered = true;
+  }
   HIPCHECK(stencil_launch(L, s->timing ? s->ev0 : nullptr, s->timing ? s->ev1 : nullptr, st));
   if (s->timing) HIPCHECK(hipEventRecord(s->eb1, st));
-  return CEP_OK;
-}
-
-template <class T>
-int stage(cep_session* s, DBuf& buf, const T* src, int64_t n, hipStream_t st, const T** dst) {
-  *dst = src;
-  if (!src || n <= 0) return CEP_OK;
-  if (buf.ensure(size_t(n) * sizeof(T))) return fail(CEP_E_HIP, "staging allocation failed");
-  HIPCHECK(hipMemcpyAsync(buf.p, src, size_t(n) * sizeof(T), hipMemcpyHostToDevice, st));
-  *dst = buf.as<T>();
   return CEP_OK;
 }
 
@@ -341,25 +437,19 @@ int carry_gc(cep_session* s, int64_t min_words, hipStream_t st) {
 int stage_inputs(cep_session* s, const cep_batch* b, hipStream_t st, NfaArgs& A) {
   const Program& P = s->pat->prog;
   const int64_t n = b->n;
-  int rc = CEP_OK;
-  if (b->mem == CEP_MEM_HOST) {
-    if ((rc = stage(s, s->h_key, b->key_id, n, st, &A.key)) || (rc = stage(s, s->h_valid, b->valid, n, st, &A.valid)) ||
-        (rc = stage(s, s->h_topic, b->topic, n, st, &A.topic)) ||
-        (rc = stage(s, s->h_part, b->partition, n, st, &A.partition)) ||
-        (rc = stage(s, s->h_off, b->offset, n, st, &A.offset)) || (rc = stage(s, s->h_ts, b->ts, n, st, &A.ts)))
-      return rc;
-    for (int c = 0; c < b->n_cols; c++) {
-      const size_t w = type_size(P.coltypes[c]);
-      if (n > 0) {
-        if (s->h_cols[c].ensure(size_t(n) * w)) return fail(CEP_E_HIP, "staging allocation failed");
-        HIPCHECK(hipMemcpyAsync(s->h_cols[c].p, b->cols[c], size_t(n) * w, hipMemcpyHostToDevice, st));
-      }
-      A.cols[c] = s->h_cols[c].p;
-    }
-  } else {
-    A.key = b->key_id; A.valid = b->valid; A.topic = b->topic; A.partition = b->partition;
-    A.offset = b->offset; A.ts = b->ts;
-    for (int c = 0; c < b->n_cols; c++) A.cols[c] = b->cols[c];
+  A.key = b->key_id; A.valid = b->valid; A.topic = b->topic; A.partition = b->partition;
+  A.offset = b->offset; A.ts = b->ts;
+  for (int c = 0; c < b->n_cols; c++) A.cols[c] = b->cols[c];
+  if (b->mem == CEP_MEM_HOST && n > 0) {
+    HostArr arrs[6 + 16] = {{A.key, size_t(n) * 4, reinterpret_cast<const void**>(&A.key)},
+                            {A.valid, size_t(n), reinterpret_cast<const void**>(&A.valid)},
+                            {A.topic, size_t(n) * 4, reinterpret_cast<const void**>(&A.topic)},
+                            {A.partition, size_t(n) * 4, reinterpret_cast<const void**>(&A.partition)},
+                            {A.offset, size_t(n) * 8, reinterpret_cast<const void**>(&A.offset)},
+                            {A.ts, size_t(n) * 8, reinterpret_cast<const void**>(&A.ts)}};
+    for (int c = 0; c < b->n_cols; c++)
+      arrs[6 + c] = HostArr{A.cols[c], size_t(n) * type_size(P.coltypes[c]), &A.cols[c]};
+    return stage_host(s, arrs, 6 + b->n_cols, st);
   }
   return CEP_OK;
 }
@@ -469,7 +559,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
       s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 4) * 8) ||
       s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->r_endof.ensure(size_t(n) * 4) ||
-      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) || s->r_blk.ensure(size_t(n / 256 + 2) * 16))
+      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) || s->r_blk.ensure(size_t(n / 256 + 2) * 16) ||
+      s->r_errlist.ensure(size_t(std::min<int64_t>(n, kRunsErrCap)) * 24))
     return fail(CEP_E_HIP, "allocation failed");
   RunsArgs A{};
   A.P = s->dprog.as<DevProgram>();
@@ -488,7 +579,11 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.err_code = s->r_errcode.as<int32_t>();
   A.segs = s->r_segs.as<uint32_t>();             // the runs' consumed stages, for runs_expand
   A.seg_over = ctl + 3;
-  const unsigned long long init[5] = {0, ~0ull, 0, 0, 0};   // matches, first exception, entries, segment overflow, longest span
+  A.err_list = s->r_errlist.as<unsigned long long>();
+  A.err_n = ctl + 5;
+  A.err_cap = std::min<int64_t>(n, kRunsErrCap);
+  // matches, first exception, entries, segment overflow, longest span, failing runs
+  const unsigned long long init[6] = {0, ~0ull, 0, 0, 0, 0};
   HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
   HIPCHECK(runs_sim_launch(A, s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), st,
                            s->jit ? s->jit->runs_sim : nullptr));
@@ -508,7 +603,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                               s->rpool.as<int64_t>(), s->rtab.as<int64_t>(), st));
   }
   // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow
-  unsigned long long res[5];
+  unsigned long long res[6];
   int64_t top = 0;
   HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
   HIPCHECK(hipMemcpyAsync(&res[0], scal0 + 3, 8, hipMemcpyDeviceToHost, st));
@@ -529,8 +624,32 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     if (rcarry) HIPCHECK(hipMemcpy(&at, X.pos + at, 8, hipMemcpyDeviceToHost));   // its stream position
     s->g_err = code;
     s->g_err_rec = at;
-    s->e_rec.push_back(at);                        // the runs path keeps only the first exception
-    s->e_code.push_back(code);
+    const int64_t nerr = int64_t(res[5]);
+    if (nerr <= A.err_cap) {                       // every failing key's first exception (cep_batch_errors)
+      std::vector<unsigned long long> el(size_t(nerr) * 3);
+      HIPCHECK(hipMemcpy(el.data(), A.err_list, el.size() * 8, hipMemcpyDeviceToHost));
+      std::vector<size_t> ord(static_cast<size_t>(nerr));
+      for (size_t q = 0; q < ord.size(); q++) ord[q] = q;
+      // per key the smallest (record << 31 | start): its first failure in the reference's order
+      std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) {
+        const uint32_t kx = uint32_t(el[3 * x + 2] >> 32), ky = uint32_t(el[3 * y + 2] >> 32);
+        return kx != ky ? kx < ky : el[3 * x] < el[3 * y];
+      });
+      std::vector<std::pair<int64_t, int32_t>> first;
+      for (size_t q = 0; q < ord.size(); q++) {
+        const size_t x = ord[q];
+        if (q > 0 && (el[3 * x + 2] >> 32) == (el[3 * ord[q - 1] + 2] >> 32)) continue;
+        first.emplace_back(int64_t(el[3 * x + 1]), int32_t(uint32_t(el[3 * x + 2])));
+      }
+      std::sort(first.begin(), first.end());
+      for (const auto& f : first) {
+        s->e_rec.push_back(f.first);
+        s->e_code.push_back(f.second);
+      }
+    } else {                                       // more failing runs than the list holds: the first only
+      s->e_rec.push_back(at);
+      s->e_code.push_back(code);
+    }
   }
   int bits = 1;                                    // bits of the completing record
   while ((int64_t(1) << bits) <= n) bits++;
@@ -799,6 +918,17 @@ const char* cep_pattern_name(const cep_pattern* p, int32_t id) {
   return p->prog.names[id].c_str();
 }
 
+int cep_pattern_check(const cep_pattern* p, int32_t session_flags) {
+  if (!p) return fail(CEP_E_ARG, "null argument");
+  const Program& P = p->prog;
+  // a carry session keeps its keys' full NFA state on the general path whenever a batch needs it
+  if ((session_flags & CEP_SESSION_CARRY) && !P.general_ok)
+    return fail(CEP_E_UNSUPPORTED, "pattern cannot be lowered to the device NFA: " + P.general_why);
+  if (!P.stencil_ok && !P.runs_ok && !P.general_ok)
+    return fail(CEP_E_UNSUPPORTED, "no device path: " + P.general_why);
+  return CEP_OK;
+}
+
 int32_t cep_pattern_stage(const cep_pattern* p, int32_t sid, int32_t* name_id, int32_t* type, int64_t* window_ms,
                           int32_t* ops, int32_t* targets, int32_t cap) {
   if (!p || sid < 0 || sid >= int32_t(p->prog.stages.size())) return -1;
@@ -926,17 +1056,26 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 
 void cep_session_close(cep_session* s) {
   if (!s) return;
-  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->heavy, &s->h_key, &s->h_valid,
-                  &s->h_topic, &s->h_part, &s->h_off, &s->h_ts, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
+  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->heavy, &s->dstage,
+                  &s->h_topic, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
                   &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_segs, &s->r_blk, &s->r_len, &s->r_entoff,
-                  &s->r_errcode, &s->r_endof, &s->r_prof, &s->rtab, &s->rpool, &s->rpool2, &s->rtop, &s->e_key,
+                  &s->r_errcode, &s->r_errlist, &s->r_endof, &s->r_prof, &s->rtab, &s->rpool, &s->rpool2, &s->rtop, &s->e_key,
                   &s->e_topic, &s->e_part, &s->e_seg, &s->e_off, &s->e_ts, &s->e_pos, &s->rc_a, &s->rc_b, &s->rc_c,
                   &s->rc_d, &s->gc_len, &s->gc_off})
     b->release();
-  for (auto& c : s->h_cols) c.release();
   for (auto& c : s->e_cols) c.release();
+  for (int j = 0; j < 2; j++) {
+    if (s->ring_ev[j]) (void)hipEventSynchronize(s->ring_ev[j]);
+    if (s->ring_ev[j]) (void)hipEventDestroy(s->ring_ev[j]);
+    if (s->ring[j]) (void)hipHostFree(s->ring[j]);
+  }
+  if (s->h2d_ev) (void)hipEventDestroy(s->h2d_ev);
+  if (s->dl) {
+    (void)hipDeviceSynchronize();                   // a delivery may still be writing into it
+    (void)hipHostFree(s->dl);
+  }
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->eb0) (void)hipEventDestroy(s->eb0);
@@ -1013,6 +1152,8 @@ int cep_pattern_build_kernels(const cep_pattern* p, int path) {
   return CEP_OK;
 }
 
+static int push_dispatch(cep_session* s, const cep_batch* b, hipStream_t st, bool stencil_batch);
+
 int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   if (!s || !b) return fail(CEP_E_ARG, "null argument");
   static const char* const kRange[] = {"cep_push_batch", "cep_push_batch:stencil", "cep_push_batch:general",
@@ -1037,6 +1178,18 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   // break contiguity: the stencil only takes batches without them
   const bool stencil_batch = !b->valid && !(s->opts.mode == CEP_MODE_PROCESSOR && b->offset &&
                                             !(b->flags & CEP_BATCH_OFFSETS_MONOTONE));
+  s->h2d_wait = false;
+  s->delivered = false;
+  int rc = push_dispatch(s, b, st, stencil_batch);
+  if (s->h2d_wait) {                               // the caller's pinned columns are borrowed only for the call
+    s->h2d_wait = false;
+    HIPCHECK(hipEventSynchronize(s->h2d_ev));
+  }
+  return rc;
+}
+
+static int push_dispatch(cep_session* s, const cep_batch* b, hipStream_t st, bool stencil_batch) {
+  const Program& P = s->pat->prog;
   if (s->path == CEP_PATH_RUNS && stencil_batch) {
     s->last_path = CEP_PATH_RUNS;
     return push_runs(s, b, st);
@@ -1129,6 +1282,54 @@ int cep_collect(cep_session* s, cep_matches* o) {
     o->err = s->g_err;
     o->err_record = s->g_err_rec;
     if (s->g_err) g_err = "the reference NFA raises an exception on this batch";
+  } else if (s->delivered) {                       // CEP_BATCH_DELIVER: the device wrote the CSR's inputs
+    const StencilProgram& SP = s->pat->prog.stencil;
+    const int k = SP.k;
+    HIPCHECK(hipStreamSynchronize(s->stream));
+    const int64_t* hdr = static_cast<const int64_t*>(s->dl);
+    const int32_t* hkey = reinterpret_cast<const int32_t*>(hdr + 2);
+    const int64_t* hpos = hdr + 2 + (s->dl_cap + 1) / 2 + 1;
+    const int64_t nm = hdr[0];
+    const uint64_t hf = uint64_t(hdr[1]);
+    if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    if (hf & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+    if (hf & 4) return fail(CEP_E_RUN_CAPACITY, "chain carry batch: more runs completing in one tile than its match space");
+    if (nm > s->out_cap) return fail(CEP_E_RUN_CAPACITY, "match output exceeded the session capacity");
+    const int64_t nh = std::min(nm, s->dl_cap);
+    std::vector<int64_t> rest_pos;
+    std::vector<int32_t> rest_key;
+    if (nm > nh) {                                 // past the host buffer: from the device arrays
+      rest_pos.resize(size_t(nm - nh) * k);
+      rest_key.resize(size_t(nm - nh));
+      HIPCHECK(hipMemcpy(rest_pos.data(), s->opos.as<int64_t>() + nh * k, rest_pos.size() * 8, hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(rest_key.data(), s->mkey.as<int32_t>() + nh, rest_key.size() * 4, hipMemcpyDeviceToHost));
+    }
+    s->match_record.resize(size_t(nm));
+    s->match_key.resize(size_t(nm));
+    s->ent_off.resize(size_t(nm) + 1);
+    s->ent_name.resize(size_t(nm) * k);
+    s->ent_record.resize(size_t(nm) * k);
+    int64_t ne = 0;
+    for (int64_t m = 0; m < nm; m++) {             // peek traversal order: final stage first
+      const int64_t* p = m < nh ? hpos + m * k : rest_pos.data() + (m - nh) * k;
+      s->match_key[size_t(m)] = m < nh ? hkey[m] : rest_key[size_t(m - nh)];
+      s->match_record[size_t(m)] = p[k - 1];
+      s->ent_off[size_t(m)] = ne;
+      for (int i = k - 1; i >= 0; i--) {
+        if (p[i] == -1) continue;                   // a skipped optional stage
+        s->ent_name[size_t(ne)] = SP.name[i];
+        s->ent_record[size_t(ne)] = p[i];
+        ne++;
+      }
+    }
+    s->ent_off[size_t(nm)] = ne;
+    s->ent_name.resize(size_t(ne));
+    s->ent_record.resize(size_t(ne));
+    o->n_matches = nm;
+    o->n_entries = ne;
+    o->path = s->last_path;
+    o->err = CEP_OK;
+    o->err_record = -1;
   } else {
     const StencilProgram& SP = s->pat->prog.stencil;
     const int k = SP.k;

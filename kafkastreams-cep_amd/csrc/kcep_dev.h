@@ -174,6 +174,12 @@ struct RunsArgs {
   int64_t match_cap;
   unsigned long long* err_min;    // min over failing runs of (record << 31 | start)
   int32_t* err_code;              // per start record (valid where it failed)
+  // every failing run, appended: {record << 31 | start, stream position of the record, key << 32 | code}
+  // (the host keeps each key's first -- a batch grouped by key fails first in ARRIVAL order at the
+  // smallest of the keys' first failures, cep_batch_errors); err_n counts them, err_cap bounds the list
+  unsigned long long* err_list;
+  unsigned long long* err_n;
+  int64_t err_cap;
   // runs_sim: the stages a run consumed, as up to RUNS_MAX_SEGS segments per start record j:
   // segs[j * RUNS_MAX_SEGS + i] = stage << 24 | offset of the segment's first record from j,
   // terminated by ~0u when shorter (a run's consumed stages never increase, runs.hip); null: off

@@ -155,6 +155,15 @@ KCEP_HD inline int halo_old(const HaloHdr& h, int32_t stamp) {
 }
 
 // ---- launch interfaces shared by abi.cpp and the .hip files ----
+// CEP_BATCH_DELIVER on a carry session: where the device hands the batch's matches to the host
+struct DeliverArgs {
+  int64_t* hdr = nullptr;         // pinned host: {match count, this batch's error flags}; null: no delivery
+  int32_t* hkey = nullptr;        // pinned host: key id per match (the first host_cap matches)
+  int64_t* hpos = nullptr;        // pinned host: k stream positions per match
+  int32_t* dkey = nullptr;        // device: the same past host_cap
+  int64_t* dpos = nullptr;
+  int64_t host_cap = 0;
+};
 struct StencilLaunch {
   const int32_t* key;
   const void* val;
@@ -172,6 +181,7 @@ struct StencilLaunch {
   StencilCarry carry;             // halo != nullptr: carry session
   int plain;                      // plain stencil (no carry, no chain, k <= 7): the keyless kernel (KCEP_STENCIL_KEYED=1: off)
   unsigned long long* clear_flag; // carry: the next batch's error-flag word, zeroed by the scan kernel (or null)
+  DeliverArgs deliver;            // carry sessions' CEP_BATCH_DELIVER batches
 };
 
 // compile.cpp

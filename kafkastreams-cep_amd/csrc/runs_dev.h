@@ -261,6 +261,15 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
           if (res.fail_at >= 0 && !(A.pos && A.pos[res.fail_at] < A.emit_from)) {
             A.err_code[i] = res.err;
             atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
+            if (A.err_list) {
+              const unsigned long long q = atomicAdd(A.err_n, 1ull);
+              if (int64_t(q) < A.err_cap) {
+                unsigned long long* e = A.err_list + 3 * q;
+                e[0] = (unsigned long long)(res.fail_at << 31 | i);
+                e[1] = (unsigned long long)(A.pos ? A.pos[res.fail_at] : res.fail_at);
+                e[2] = (unsigned long long)(uint32_t(A.key[i])) << 32 | uint32_t(res.err);
+              }
+            }
           }
           if (A.segs && res.end >= 0 && !old_end) {
             if (seg_item != i) seg_n = 0;

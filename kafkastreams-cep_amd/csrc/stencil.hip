@@ -143,6 +143,75 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
   }
 }
 
+// Small carry batches collected at once (CEP_BATCH_DELIVER: a processor flush): stencil_finish_small
+// and stencil_deliver in one launch -- the scan of <= 1024 super-tile counts, then one lane per match
+// expands its slot into the k-int row (kept on the device for cep_checksum) and hands the row's stream
+// positions and the match's key to pinned host memory.  One launch fewer on the flush's critical path.
+__global__ __launch_bounds__(1024) void stencil_finish_deliver(const int32_t* __restrict__ slots,
+                                                               const int64_t* __restrict__ cnt, int64_t nt, int k,
+                                                               int32_t* __restrict__ out, int64_t out_cap, int sub,
+                                                               int64_t* __restrict__ total,
+                                                               unsigned long long* __restrict__ clear_flag,
+                                                               SlotFormat F, const int32_t* __restrict__ key,
+                                                               StencilCarry C, int64_t host_cap, int64_t* __restrict__ hdr,
+                                                               int32_t* __restrict__ hkey, int64_t* __restrict__ hpos,
+                                                               int32_t* __restrict__ dkey, int64_t* __restrict__ dpos) {
+  __shared__ int64_t s_pre[SMALL_FINISH + 1];
+  __shared__ int64_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t c = tid < nt ? cnt[tid] : 0;
+  int64_t incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  int64_t run = incl - c;
+  for (int w = 0; w < wid; w++) run += s_w[w];
+  s_pre[tid] = run;
+  if (tid == 1023) {
+    s_pre[SMALL_FINISH] = run + c;
+    *total = run + c;
+    hdr[0] = run + c;
+    hdr[1] = int64_t(*C.flags);                    // this batch's error flags (the kernel is done)
+  }
+  if (tid == 0 && clear_flag) *clear_flag = 0;    // the next batch's error-flag word
+  __syncthreads();
+  for (int64_t t = wid; t < nt; t += 16) {                 // one wave per super-tile, one lane per match
+    const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
+    if (pre + m > out_cap) continue;
+    const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
+    const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
+    for (int64_t q = lane; q < m; q += 64) {
+      const int64_t i = pre + q;
+      int32_t row[STENCIL_MAX_K], last = 0;
+#pragma unroll
+      for (int s = 0; s < STENCIL_MAX_K; s++)
+        if (s < k) {
+          row[s] = F.entry(src, aux, q, s);
+          out[i * k + s] = row[s];
+          last = row[s];
+        }
+      const int32_t kk = key[last];
+      const HaloHdr& h = C.hdr[kk];
+      const int old = halo_old(h, C.stamp);
+      const int64_t* hp = C.pos + (2 * int64_t(kk) + old) * C.km1;
+      const bool host = i < host_cap;
+      int64_t* p = host ? hpos + i * k : dpos + i * k;
+#pragma unroll
+      for (int s = 0; s < STENCIL_MAX_K; s++)
+        if (s < k) {
+          const int32_t r = row[s];
+          p[s] = r >= 0 ? C.base + r : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
+        }
+      if (host) hkey[i] = kk;
+      else dkey[i] = kk;
+    }
+  }
+}
+
 static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
   if (L.chain && L.k != 3 && L.k != 4) return hipErrorInvalidValue;   // an optional stage needs k >= 3; chain k <= 4
   switch (L.k) {
@@ -158,15 +227,24 @@ static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
+hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k, const int64_t* total, int64_t out_cap,
+                                  const StencilCarry& C, int64_t host_cap, int64_t* hdr, int32_t* hkey, int64_t* hpos,
+                                  int32_t* dkey, int64_t* dpos, hipStream_t st);
+
 // stencil_kernel (timed as the dominant kernel between ev0 and ev1), then the
 // tile-count scan and the gather into the contiguous output
 hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st) {
   // null events: timing off (cep_session_set_timing), no event packets in the stream
+  const DeliverArgs& D = L.deliver;
   if (L.n <= 0) {
     hipError_t e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
     if (e == hipSuccess && L.clear_flag) e = hipMemsetAsync(L.clear_flag, 0, 8, st);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
-    return e == hipSuccess ? hipMemsetAsync(L.total, 0, sizeof(int64_t), st) : e;
+    if (e == hipSuccess) e = hipMemsetAsync(L.total, 0, sizeof(int64_t), st);
+    if (e == hipSuccess && D.hdr)                  // an empty delivery: the header only
+      e = stencil_deliver_launch(L.key, L.out, L.k, L.total, 0, L.carry, D.host_cap, D.hdr, D.hkey, D.hpos, D.dkey,
+                                 D.dpos, st);
+    return e;
   }
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
   const int sub = stencil_sub(ntiles);
@@ -177,16 +255,28 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e != hipSuccess) return e;
   // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
   const SlotFormat F{L.k, L.plain && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
+  if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr) {   // a small carry flush: scan, rows and delivery at once
+    hipLaunchKernelGGL(stencil_finish_deliver, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
+                       L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey, D.hpos,
+                       D.dkey, D.dpos);
+    return hipGetLastError();
+  }
   if (nsuper <= SMALL_FINISH) {
     hipLaunchKernelGGL(stencil_finish_small, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
                        L.out_cap, sub, L.total, L.clear_flag, F);
-    return hipGetLastError();
+  } else {
+    hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
+    static const int gthreads = [] { const char* e = getenv("KCEP_GATHER_THREADS"); const int v = e ? atoi(e) : 0;
+                                     return v == 64 || v == 128 || v == 256 ? v : 128; }();   // A/B knob
+    hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(gthreads), 0, st, L.slots, L.tile_count, L.tile_pre,
+                       L.out, L.out_cap, sub, F);
   }
-  hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, st, L.tile_count, nsuper, L.tile_pre, L.total, L.clear_flag);
-  static const int gthreads = [] { const char* e = getenv("KCEP_GATHER_THREADS"); const int v = e ? atoi(e) : 0;
-                                   return v == 64 || v == 128 || v == 256 ? v : 128; }();   // A/B knob
-  hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(gthreads), 0, st, L.slots, L.tile_count, L.tile_pre,
-                     L.out, L.out_cap, sub, F);
+  if (D.hdr) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return stencil_deliver_launch(L.key, L.out, L.k, L.total, L.out_cap, L.carry, D.host_cap, D.hdr, D.hkey, D.hpos,
+                                  D.dkey, D.dpos, st);
+  }
   return hipGetLastError();
 }
 
@@ -237,6 +327,47 @@ __global__ void stencil_resolve(const int32_t* __restrict__ key, const int32_t* 
     pos[i * k + s] = r >= 0 ? C.base + r : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
   }
 }
+// CEP_BATCH_DELIVER (a carry session's flush, GpuCEPProcessor): the batch's matches handed to pinned host
+// memory by the device itself, right after the scan -- the header {match count, this batch's error
+// flags}, then per match its key id and its k entries as stream positions (stencil_resolve's rule) --
+// so that cep_collect is one wait instead of one host round trip per post-processing step.  Matches
+// past host_cap go to the device arrays (dkey / dpos), which cep_collect copies.  The match count is
+// read on the device: the grid strides over the session's capacity.
+__global__ __launch_bounds__(256) void stencil_deliver(const int32_t* __restrict__ key, const int32_t* __restrict__ out,
+                                                       int k, const int64_t* __restrict__ total, int64_t out_cap,
+                                                       StencilCarry C, int64_t host_cap, int64_t* __restrict__ hdr,
+                                                       int32_t* __restrict__ hkey, int64_t* __restrict__ hpos,
+                                                       int32_t* __restrict__ dkey, int64_t* __restrict__ dpos) {
+  const int64_t t = *total, nm = t < out_cap ? t : out_cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    hdr[0] = t;
+    hdr[1] = int64_t(*C.flags);
+  }
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nm; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t last = out[i * k + k - 1];
+    const int32_t kk = key[last];
+    const HaloHdr& h = C.hdr[kk];
+    const int old = halo_old(h, C.stamp);
+    const int64_t* hp = C.pos + (2 * int64_t(kk) + old) * C.km1;
+    const bool host = i < host_cap;
+    int64_t* p = host ? hpos + i * k : dpos + i * k;
+    for (int s = 0; s < k; s++) {
+      const int32_t r = out[i * k + s];
+      p[s] = r >= 0 ? C.base + r : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
+    }
+    if (host) hkey[i] = kk;
+    else dkey[i] = kk;
+  }
+}
+hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k, const int64_t* total, int64_t out_cap,
+                                  const StencilCarry& C, int64_t host_cap, int64_t* hdr, int32_t* hkey, int64_t* hpos,
+                                  int32_t* dkey, int64_t* dpos, hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>((out_cap + 255) / 256, 1024);
+  hipLaunchKernelGGL(stencil_deliver, dim3(unsigned(std::max<int64_t>(blocks, 1))), dim3(256), 0, st, key, out, k, total,
+                     out_cap, C, host_cap, hdr, hkey, hpos, dkey, dpos);
+  return hipGetLastError();
+}
+
 __global__ void stencil_checksum_pos(const int64_t* __restrict__ pos, int k, int64_t nm,
                                      const StencilProgram* __restrict__ P, unsigned long long* __restrict__ sum) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;

@@ -237,7 +237,7 @@ class GpuCEPProcessor:
             self._log[base + i] = r[6]
         try:
             self.session.push(n, self._kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts,
-                              flags=self._flags)
+                              flags=self._flags | N.BATCH_DELIVER)
             out = self.session.collect(raise_on_error=False)
         except N.CepError as e:                           # no state was committed for this batch:
             self._failed = e                              # the task fails, as the reference's does

@@ -328,6 +328,48 @@ def test_stock_demo_random_keys_fail_where_the_reference_fails(seed):
     assert got == want and len(want) > 0
 
 
+def runs_div_pattern():
+    """A runs-path pattern (strict, never branching, a fold) whose second stage divides by (v - 7):
+    ArithmeticException on every key that reaches a 7 after its first stage."""
+    from kcep import QueryBuilder, Event, States
+    return (QueryBuilder().select("a").where(Event.value() > 0).fold("s", Event.value()).then()
+            .select("b").where(States.getInt("s") * 100 / (Event.value() - 7) > 10).then()
+            .select("c").where(Event.value() > 2).build())
+
+
+@pytest.mark.parametrize("seed,batch", [(3, 5000), (4, 5000), (5, 2500), (3, 997)])
+def test_runs_path_keys_fail_where_the_reference_fails(seed, batch):
+    """several keys of one batch throw on the runs path.  cep_batch_errors must list every
+    failing key's first exception, so that the processor (which groups a batch by key) fails at the
+    first exception in ARRIVAL order and forwards exactly what the reference forwarded before it."""
+    rng = np.random.default_rng(seed)
+    n = 5000
+    kid = rng.integers(0, 1000, n).astype(np.int32)
+    val = rng.integers(0, 200, n).astype(np.int32)
+    sch = Schema([("value", "i32")])
+    ir = runs_div_pattern().to_ir(sch)
+    assert N.CompiledPattern(ir).info.runs_ok
+    p = O.OraclePattern(ir)
+    r = O.OracleRun(p, O.MODE_PROCESSOR)
+    with pytest.raises(O.OracleError) as oe:
+        r.process(O.BatchArrays(kid, [val], [1]))
+    recs = [(f"K{kid[i]}", int(val[i]), "t", 0, i, i) for i in range(n)]
+    want = [(recs[m.record][0], seq_view(sequence_from_traversal(
+        m.traversal, p.names, lambda i: Ev(recs[i][0], recs[i][1], i, "t", 0, i))))
+        for m in r.matches(with_groups=False) if m.record < oe.value.record]
+    got = []
+    proc = GpuCEPProcessor("Div", ir, sch, scalar_column(sch), batch_size=batch)
+    proc.init(lambda k, s: got.append((k, seq_view(s))))
+    assert proc.session.path == N.PATH_RUNS
+    with pytest.raises(N.CepError) as ge:
+        for rr in recs:
+            proc.process(*rr)
+        proc.flush()
+    assert (ge.value.code, ge.value.record) == (oe.value.code, oe.value.record) == (5, oe.value.record)
+    assert len(proc.session.batch_errors()[0]) > 1        # several keys failed in the failing batch
+    assert got == want and len(want) > 0
+
+
 def test_record_log_is_pruned_to_carried_events():
     """The host keeps a record only while a carried run can still reach it (positions listed in
     the exported state); pruning must not change the forwarded stream."""
