@@ -285,6 +285,16 @@ int cep_state_import_keys(cep_session* s, const void* const* blobs, const size_t
  * references -- the records a host must keep to build the Sequences of carried runs (the reference
  * keeps them in its buffer store, MatchedEvent.java:29-34).  out == NULL: only *n. */
 int cep_state_positions(const void* blob, size_t len, int64_t* out, int64_t cap, int64_t* n);
+/* A key's carried NFA state -- a single-key "KCST" blob from cep_state_evict, typically of a key handed back
+ * with CEP_E_RUN_CAPACITY -- written in the reference's own terms ("KCRF", layout in abi.cpp): NFA.runs,
+ * the per-topic high-water marks, the run queue (stage, epsilon target, isBranching / isIgnored, sequence,
+ * last event, Dewey digits; ComputationStage.java:30-185, NFAStates.java:33-109), the buffer nodes with
+ * their refs and ordered predecessors (Matched.java:31-66, MatchedEvent.java:27-169) and the aggregates
+ * (AggregatesStoreImpl.java:30-76), over the events the buffer holds.  A host builds the reference's
+ * NFAStates / buffer / aggregate entries from it and continues the key on the reference NFA (SURVEY §8(b):
+ * a key over capacity falls back per key).  Host-only; out == NULL: only *needed. */
+int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, void* out, size_t cap,
+                           size_t* needed);
 /* Changes cep_opts.max_key_words for the next batches: a host re-pushes the records of keys handed
  * back with CEP_E_RUN_CAPACITY with the limit lifted (0 = only the device pool bounds a key). */
 int cep_session_set_max_key_words(cep_session* s, int64_t words);

@@ -12,9 +12,16 @@
  * Wiring: org.apache.kafka.streams.kstream.internals.GpuCEPStreamImpl.query (java/org/...) lowers the
  * query's Pattern with PatternIR.encode (java/.../pattern/PatternIR.java) and, when some device path
  * runs it, adds () -> new GpuCEPProcessor<>(queryName, ir, topics, schema, ...) instead of the
- * reference's () -> new CEPProcessor<>(queryName, pattern) (kint/CEPStreamImpl.java:83-84); the three
- * state stores are not needed (the device keeps every key's NFA between batches, CEP_SESSION_CARRY).
- * Queries PatternIR cannot lower keep the reference CEPProcessor.
+ * reference's () -> new CEPProcessor<>(queryName, pattern) (kint/CEPStreamImpl.java:83-84).  The device
+ * keeps every key's NFA between batches (CEP_SESSION_CARRY); the reference's three state stores are
+ * still attached, for the keys below.  Queries PatternIR cannot lower keep the reference CEPProcessor.
+ *
+ * A key that outgrows the whole device pool (CEP_E_RUN_CAPACITY even with the per-key cap lifted, after
+ * the pool has grown toward free HBM) is NOT a task failure: the reference never runs out of capacity
+ * (NFA.java:134-149 over unbounded stores).  Its state as of the batch start is evicted from the device,
+ * rewritten in the reference's terms (cep_state_to_reference) and loaded into the three stores
+ * (state.internal.ReferenceHandoff); the key then continues on the reference's own CEPProcessor -- this
+ * batch's records replayed with their record context, every later record at once in process().
  *
  * Record context: matches are forwarded from flush(), so a downstream processor that reads
  * context().timestamp() / topic() / offset() sees the record or punctuation that triggered the flush,
@@ -25,9 +32,26 @@ package com.github.fhuss.kafka.streams.cep.processor;
 
 import com.github.fhuss.kafka.streams.cep.Event;
 import com.github.fhuss.kafka.streams.cep.Sequence;
+import com.github.fhuss.kafka.streams.cep.nfa.Stages;
+import com.github.fhuss.kafka.streams.cep.pattern.Pattern;
+import com.github.fhuss.kafka.streams.cep.pattern.StagesFactory;
+import com.github.fhuss.kafka.streams.cep.state.AggregatesStore;
+import com.github.fhuss.kafka.streams.cep.state.NFAStore;
+import com.github.fhuss.kafka.streams.cep.state.QueryStores;
+import com.github.fhuss.kafka.streams.cep.state.SharedVersionedBufferStore;
+import com.github.fhuss.kafka.streams.cep.state.internal.ReferenceHandoff;
+import org.apache.kafka.common.serialization.Serde;
+import org.apache.kafka.streams.StreamsMetrics;
+import org.apache.kafka.streams.processor.Cancellable;
 import org.apache.kafka.streams.processor.Processor;
 import org.apache.kafka.streams.processor.ProcessorContext;
 import org.apache.kafka.streams.processor.PunctuationType;
+import org.apache.kafka.streams.processor.Punctuator;
+import org.apache.kafka.streams.processor.StateRestoreCallback;
+import org.apache.kafka.streams.processor.StateStore;
+import org.apache.kafka.streams.processor.TaskId;
+
+import java.io.File;
 
 import java.util.ArrayList;
 import java.util.Arrays;
@@ -77,12 +101,16 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     private static native void cepSessionClose(long session);
     private static native void cepPatternFree(long pattern);
     private static native String cepLastError();
+    /** cep_state_to_reference: a single-key blob in the reference's terms ("KCRF"), or null */
+    private static native byte[] cepStateToReference(long pattern, byte[] blob);
 
     private static final int CEP_MODE_PROCESSOR = 1, CEP_SESSION_CARRY = 1, CEP_E_RUN_CAPACITY = 9;
     private static final int CEP_PATH_STENCIL = 1, CEP_PATH_CHAIN = 3, CEP_PATH_RUNS = 4, CEP_BATCH_OFFSETS_MONOTONE = 1;
     private static final int CEP_BATCH_DELIVER = 2;                // collected at once: matches delivered to host memory
 
     private final String queryName;
+    private final String rawQueryName;
+    private final Pattern<K, V> referencePattern;
     private final byte[] ir;
     private final ValueDecoder<V> decoder;
     private final int batchSize;
@@ -112,12 +140,19 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     // events carried runs may still reach, by stream position (pruned from cepStatePositions)
     private final Map<Long, Event<K, V>> log = new HashMap<>();
     private int pruneAt;
+    // keys that outgrew the device: continued on the reference CEPProcessor over the reference's stores
+    private final Set<K> cpuKeys = new HashSet<>();
+    private CEPProcessor<K, V> reference;
+    private ReplayContext replay;
+    private Stages<K, V> stages;
 
     /** topics: the topic ids the IR uses, in id order (PatternIR.Lowered.topics); records of other topics
      *  get the next free ids as they arrive. */
-    public GpuCEPProcessor(String queryName, byte[] ir, List<String> topics, ValueDecoder<V> decoder, int batchSize,
-                           int maxKeys, long maxKeyWords) {
+    public GpuCEPProcessor(String queryName, Pattern<K, V> pattern, byte[] ir, List<String> topics,
+                           ValueDecoder<V> decoder, int batchSize, int maxKeys, long maxKeyWords) {
         this.queryName = queryName.toLowerCase().replace("\\s+", "");   // CEPProcessor.java:83, literal replace
+        this.rawQueryName = queryName;
+        this.referencePattern = pattern;
         this.ir = ir;
         for (String t : topics) topicIds.putIfAbsent(t, topicIds.size());
         this.decoder = decoder;
@@ -135,6 +170,11 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         this.session = check(cepSessionOpen(pattern, 0, CEP_MODE_PROCESSOR, batchSize, CEP_SESSION_CARRY,
                                             maxKeys, maxKeyWords));
         this.path = cepSessionPath(session);
+        // the reference processor for keys that outgrow the device, over the reference's own stores
+        this.stages = new StagesFactory<K, V>().make(referencePattern);
+        this.replay = new ReplayContext(context);
+        this.reference = new CEPProcessor<>(rawQueryName, referencePattern);
+        this.reference.init(replay);
         // a flush on the stream-time punctuation, as on commit
         context.schedule(context.appConfigs().containsKey("commit.interval.ms")
                          ? Long.parseLong(String.valueOf(context.appConfigs().get("commit.interval.ms"))) : 30_000L,
@@ -144,6 +184,10 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     @Override
     public void process(K key, V value) {                               // CEPProcessor.process :134-150
         if (key == null || value == null) return;                        // :136-138
+        if (cpuKeys.contains(key)) {                                    // outgrew the device: the reference
+            reference.process(key, value);                              // (live record context, forwards now)
+            return;
+        }
         pending.add(new Event<>(key, value, context.timestamp(), context.topic(), context.partition(),
                                 context.offset()));
         if (pending.size() >= batchSize) flush();
@@ -160,13 +204,18 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         cepPatternFree(pattern);
     }
 
-    /** One match of a push: arrival index of its completing record, device key id, traversal. */
-    private static final class Match {
+    /** One match: arrival index of its completing record, device key id, traversal -- or, for a key on
+     *  the reference, the Sequence its CEPProcessor forwarded. */
+    private final class Match {
         final int arrival, key;
         final int[] names;
         final long[] records;
+        final Sequence<K, V> sequence;
         Match(int arrival, int key, int[] names, long[] records) {
-            this.arrival = arrival; this.key = key; this.names = names; this.records = records;
+            this.arrival = arrival; this.key = key; this.names = names; this.records = records; this.sequence = null;
+        }
+        Match(int arrival, Sequence<K, V> sequence) {
+            this.arrival = arrival; this.key = -1; this.names = null; this.records = null; this.sequence = sequence;
         }
     }
 
@@ -326,10 +375,14 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
             } finally {
                 cepSetMaxKeyWords(session, maxKeyWords);
             }
-            for (long[] e : errors2)
-                if (e[1] == CEP_E_RUN_CAPACITY)
-                    throw new IllegalStateException(queryName + ": a key outgrew the whole device pool at record " + e[0]);
+            Set<Integer> whole = new HashSet<>();                      // outgrew even the whole pool
+            for (long[] e : errors2) if (e[1] == CEP_E_RUN_CAPACITY) whole.add(kid[(int) e[0]]);
+            errors2.removeIf(e -> e[1] == CEP_E_RUN_CAPACITY);
             errors.addAll(errors2);
+            if (!whole.isEmpty()) {
+                matches.removeIf(m -> whole.contains(m.key));
+                handOff(recs, kid, whole, matches, errors);
+            }
         }
         // where the reference would have thrown: the first failing record in arrival order
         long limit = Long.MAX_VALUE;
@@ -339,13 +392,101 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         matches.sort((a, b) -> Integer.compare(a.arrival, b.arrival));
         for (Match m : matches) {
             if (m.arrival >= limit) break;
+            if (m.sequence != null) {                                   // a key on the reference
+                context.forward(recs.get(m.arrival).key(), m.sequence);
+                continue;
+            }
             Sequence.Builder<K, V> b = Sequence.newBuilder();
             for (int i = 0; i < m.names.length; i++) b.add(names[m.names[i]], log.get(m.records[i]));
             context.forward(recs.get(m.arrival).key(), b.build(true));  // Sequence.java:210-223
         }
-        if (limit != Long.MAX_VALUE)
+        if (limit != Long.MAX_VALUE) {
+            if (cpuFailure != null && cpuFailureAt == limit) throw cpuFailure;   // the reference's own exception
             throw new IllegalStateException(queryName + ": reference exception " + code + " at record " + limit);
+        }
         if (log.size() >= pruneAt) prune();
+    }
+
+    private RuntimeException cpuFailure;
+    private long cpuFailureAt = -1;
+
+    /** Keys that outgrew the whole device pool: their state (as of this batch's start) moves into the
+     *  reference's stores and their records of this batch replay on the reference CEPProcessor. */
+    @SuppressWarnings("unchecked")
+    private void handOff(List<Event<K, V>> recs, int[] kid, Set<Integer> keys, List<Match> matches, List<long[]> errors) {
+        final NFAStore<K, V> nfaStore = (NFAStore<K, V>) context.getStateStore(QueryStores.getQueryNFAStoreName(queryName));
+        final SharedVersionedBufferStore<K, V> buffer = (SharedVersionedBufferStore<K, V>)
+                context.getStateStore(QueryStores.getQueryEventBufferStoreName(queryName));
+        final AggregatesStore<K> aggregates = (AggregatesStore<K>)
+                context.getStateStore(QueryStores.getQueryAggregateStatesStoreName(queryName));
+        final List<String> topicName = new ArrayList<>(topicIds.keySet());
+        topicName.sort((a, b) -> Integer.compare(topicIds.get(a), topicIds.get(b)));
+        for (int id : keys) {
+            final K key = idKeys.get(id);
+            byte[][] blobs = cepStateEvict(session, new int[] {id});
+            if (blobs == null) throw new IllegalStateException(queryName + ": " + cepLastError());
+            idKeys.remove(id);
+            keyIds.remove(key);
+            freeIds.add(id);
+            if (blobs[0].length > 0) {                                  // (no state: it starts afresh there)
+                byte[] kcrf = cepStateToReference(pattern, blobs[0]);
+                if (kcrf == null) throw new IllegalStateException(queryName + ": " + cepLastError());
+                ReferenceHandoff.load(kcrf, key, log::get, topicName, stages, nfaStore, buffer, aggregates);
+            }
+            cpuKeys.add(key);
+            for (int i = 0; i < recs.size(); i++) {                     // this batch's records, arrival order
+                if (kid[i] != id) continue;
+                final Event<K, V> e = recs.get(i);
+                final int arrival = i;
+                replay.begin(e, seq -> matches.add(new Match(arrival, (Sequence<K, V>) seq)));
+                try {
+                    reference.process(e.key(), e.value());
+                } catch (RuntimeException ex) {                         // the reference's exception, at this record
+                    if (cpuFailure == null || i < cpuFailureAt) { cpuFailure = ex; cpuFailureAt = i; }
+                    errors.add(new long[] {i, -1});
+                    break;
+                } finally {
+                    replay.end();
+                }
+            }
+        }
+    }
+
+    /** The record context the reference CEPProcessor reads (CEPProcessor.java:141-148): the live one, or,
+     *  while a handed-off key's buffered records replay, the replayed record's; its forwards are captured
+     *  then, and merged into the flush's arrival order. */
+    private static final class ReplayContext implements ProcessorContext {
+        private final ProcessorContext live;
+        private Event<?, ?> at;
+        private java.util.function.Consumer<Object> sink;
+        ReplayContext(ProcessorContext live) { this.live = live; }
+        void begin(Event<?, ?> e, java.util.function.Consumer<Object> forwards) { at = e; sink = forwards; }
+        void end() { at = null; sink = null; }
+        @Override public String applicationId() { return live.applicationId(); }
+        @Override public TaskId taskId() { return live.taskId(); }
+        @Override public Serde<?> keySerde() { return live.keySerde(); }
+        @Override public Serde<?> valueSerde() { return live.valueSerde(); }
+        @Override public File stateDir() { return live.stateDir(); }
+        @Override public StreamsMetrics metrics() { return live.metrics(); }
+        @Override public void register(StateStore store, boolean logging, StateRestoreCallback cb) { live.register(store, logging, cb); }
+        @Override public StateStore getStateStore(String name) { return live.getStateStore(name); }
+        @Override public Cancellable schedule(long intervalMs, PunctuationType type, Punctuator callback) {
+            return live.schedule(intervalMs, type, callback);
+        }
+        @Override @Deprecated public void schedule(long interval) { live.schedule(interval); }
+        @Override public <K1, V1> void forward(K1 key, V1 value) {
+            if (sink != null) sink.accept(value);
+            else live.forward(key, value);
+        }
+        @Override @Deprecated public <K1, V1> void forward(K1 key, V1 value, int childIndex) { live.forward(key, value, childIndex); }
+        @Override @Deprecated public <K1, V1> void forward(K1 key, V1 value, String childName) { live.forward(key, value, childName); }
+        @Override public void commit() { live.commit(); }
+        @Override public String topic() { return at != null ? at.topic() : live.topic(); }
+        @Override public int partition() { return at != null ? at.partition() : live.partition(); }
+        @Override public long offset() { return at != null ? at.offset() : live.offset(); }
+        @Override public long timestamp() { return at != null ? at.timestamp() : live.timestamp(); }
+        @Override public Map<String, Object> appConfigs() { return live.appConfigs(); }
+        @Override public Map<String, Object> appConfigsWithPrefix(String prefix) { return live.appConfigsWithPrefix(prefix); }
     }
 
     /** Drop the records no carried run (on the device or spilled) can reach any more. */

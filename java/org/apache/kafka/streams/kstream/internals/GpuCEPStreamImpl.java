@@ -4,8 +4,9 @@
  * The reference's CEPStreamImpl.query (kint/CEPStreamImpl.java:77-95) always attaches a CEPProcessor
  * and its three stores.  This one first asks PatternIR to lower the pattern over the stream's value
  * schema (SURVEY.md §8(b)):
- *   - lowered, and some device path runs it  -> a GpuCEPProcessor over libkcep.so; no state stores
- *     (every key's NFA state lives on the GPU between batches, CEP_SESSION_CARRY);
+ *   - lowered, and some device path runs it  -> a GpuCEPProcessor over libkcep.so (every key's NFA
+ *     state lives on the GPU between batches, CEP_SESSION_CARRY); the reference's three stores are
+ *     attached as well, for the keys that outgrow the device and continue on the reference NFA;
  *   - an opaque lambda anywhere in the chain, no value schema, an IR no device path takes, or a
  *     pattern the reference rejects (InvalidPatternException) -> the reference CEPProcessor with its
  *     NFA / event-buffer / aggregate stores, exactly as the reference wires it.
@@ -82,9 +83,12 @@ public class GpuCEPStreamImpl<K, V> extends AbstractStream<K> implements CEPStre
             final List<String> topics = lowered.topics;
             final IrSchema<V> decoder = schema;
             final GpuOptions o = options;
-            final ProcessorSupplier<K, V> gpu =
-                () -> new GpuCEPProcessor<>(queryName, ir, topics, decoder, o.batchSize, o.maxKeys, o.maxKeyWords);
+            final ProcessorSupplier<K, V> gpu = () ->
+                new GpuCEPProcessor<>(queryName, pattern, ir, topics, decoder, o.batchSize, o.maxKeys, o.maxKeyWords);
             builder.internalTopologyBuilder.addProcessor(processorName, gpu, this.name);
+            // the reference's stores stay attached: a key that outgrows the device continues on the
+            // reference CEPProcessor over them (GpuCEPProcessor.handOff)
+            attachReferenceStores(processorName, queryName, pattern, queried);
             LOG.info("query {}: NFA on the GPU ({} IR bytes)", queryName, ir.length);
         } else {
             LOG.info("query {}: NFA on the reference CPU path ({})", queryName,
@@ -95,11 +99,15 @@ public class GpuCEPStreamImpl<K, V> extends AbstractStream<K> implements CEPStre
     }
 
     /** The reference's own wiring (CEPStreamImpl.java:83-92): CEPProcessor plus its three stores. */
-    @SuppressWarnings("unchecked")
     private void attachReferenceProcessor(final String processorName, final String queryName,
                                           final Pattern<K, V> pattern, final Queried<K, V> queried) {
         final ProcessorSupplier<K, V> cpu = () -> new CEPProcessor<>(queryName, pattern);
         builder.internalTopologyBuilder.addProcessor(processorName, cpu, this.name);
+        attachReferenceStores(processorName, queryName, pattern, queried);
+    }
+
+    private void attachReferenceStores(final String processorName, final String queryName,
+                                       final Pattern<K, V> pattern, final Queried<K, V> queried) {
         final Serde<K> keys = queried == null ? null : queried.keySerde();
         final Serde<V> values = queried == null ? null : queried.valueSerde();
         final QueryStoreBuilders<K, V> stores = new QueryStoreBuilders<>(queryName, pattern);

@@ -379,3 +379,22 @@ JNIEXPORT jint JNICALL IRB(irbProbe)(JNIEnv* env, jclass c, jbyteArray ir) {
 }
 
 JNIEXPORT jstring JNICALL IRB(irbLastError)(JNIEnv* env, jclass c) { return (*env)->NewStringUTF(env, cep_last_error()); }
+
+/* ---- GpuCEPProcessor: a key that outgrew the device, in the reference's own terms (KCRF) ---- */
+JNIEXPORT jbyteArray JNICALL CLS(cepStateToReference)(JNIEnv* env, jclass c, jlong pattern, jbyteArray blob) {
+  const jsize n = (*env)->GetArrayLength(env, blob);
+  jbyte* p = (*env)->GetByteArrayElements(env, blob, NULL);
+  size_t need = 0;
+  jbyteArray out = NULL;
+  const cep_pattern* pat = (const cep_pattern*)(intptr_t)pattern;
+  if (cep_state_to_reference(pat, p, (size_t)n, NULL, 0, &need) == CEP_OK) {
+    uint8_t* buf = malloc(need ? need : 1);
+    if (buf && cep_state_to_reference(pat, p, (size_t)n, buf, need, &need) == CEP_OK) {
+      out = (*env)->NewByteArray(env, (jsize)need);
+      (*env)->SetByteArrayRegion(env, out, 0, (jsize)need, (const jbyte*)buf);
+    }
+    free(buf);
+  }
+  (*env)->ReleaseByteArrayElements(env, blob, p, JNI_ABORT);
+  return out;
+}

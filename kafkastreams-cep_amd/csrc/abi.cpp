@@ -17,6 +17,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -135,7 +137,7 @@ bool wave_ok(const DevProgram& D) {
 
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
 constexpr NfaCaps kCaps{16, 64, 32, 32, 8, 16};
-constexpr int kMaxRetry = 8;                       // pool doublings before CEP_E_RUN_CAPACITY
+constexpr int kMaxRetry = 24;                      // pool regrowths (each toward free HBM) before CEP_E_RUN_CAPACITY
 constexpr int64_t kRunsErrCap = int64_t(1) << 20;  // runs path: failing runs listed per batch (cep_batch_errors)
 }  // namespace
 
@@ -169,10 +171,13 @@ struct cep_session {
   hipEvent_t h2d_ev = nullptr;
   // ---- CEP_BATCH_DELIVER (carry stencil / chain sessions): the matches handed to pinned host memory by
   // the device during the push; cep_collect then only waits ----
-  void* dl = nullptr;             // {nm, flags} header, host_cap keys, host_cap * k positions
+  void* dl = nullptr;             // dl_layout: header, host_cap keys, host_cap * k positions
   int64_t dl_cap = 0;
+  DBuf dl_ticket;                 // device: workgroups of the delivery kernel done
+  int64_t dl_stamp = 0;           // the last delivery's number
   bool delivered = false;
   bool h2d_wait = false;          // the push copied from pinned caller memory: wait for h2d_ev
+  int zc_slot = -1;               // the push's kernels read ring slot zc_slot in place (zero copy)
   // ---- general workspace ----
   DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_err, r_errrec, r_carry, ents,
       moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec;
@@ -283,7 +288,7 @@ bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st) {
+int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_copy = false) {
   size_t total = 0;
   std::vector<size_t> at(size_t(na), 0);
   bool pinned = true;
@@ -294,6 +299,32 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st) {
     pinned = pinned && host_pinned(arrs[i].src);
   }
   if (!total) return CEP_OK;
+  // zero copy (the stencil path's one streaming pass, small batches): the kernel reads the pinned ring
+  // over the link itself, no copy into HBM first (KCEP_ZERO_COPY=0 turns it off for A/B)
+  static const bool zc_env = [] { const char* e = getenv("KCEP_ZERO_COPY"); return !(e && e[0] == '0'); }();
+  if (zero_copy && zc_env && !pinned && total <= kRingChunk) {
+    const int j = s->ring_next;
+    s->ring_next ^= 1;
+    if (s->ring_ev[j]) HIPCHECK(hipEventSynchronize(s->ring_ev[j]));
+    else HIPCHECK(hipEventCreateWithFlags(&s->ring_ev[j], hipEventDisableTiming));
+    if (s->ring_cap[j] < total) {
+      if (s->ring[j]) HIPCHECK(hipHostFree(s->ring[j]));
+      s->ring[j] = nullptr;
+      s->ring_cap[j] = 0;
+      HIPCHECK(hipHostMalloc(&s->ring[j], std::max(total, size_t(1) << 20), hipHostMallocMapped));
+      s->ring_cap[j] = std::max(total, size_t(1) << 20);
+    }
+    uint8_t* h = static_cast<uint8_t*>(s->ring[j]);
+    void* dptr = nullptr;
+    HIPCHECK(hipHostGetDevicePointer(&dptr, h, 0));
+    for (int i = 0; i < na; i++)
+      if (arrs[i].src && arrs[i].bytes) {
+        memcpy(h + at[size_t(i)], arrs[i].src, arrs[i].bytes);
+        *arrs[i].dst = static_cast<uint8_t*>(dptr) + at[size_t(i)];
+      }
+    s->zc_slot = j;                                   // its event is recorded behind the kernels that read it
+    return CEP_OK;
+  }
   if (s->dstage.ensure(total)) return fail(CEP_E_HIP, "staging allocation failed");
   uint8_t* dev = s->dstage.as<uint8_t>();
   for (int i = 0; i < na; i++)
@@ -336,6 +367,14 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st) {
   return CEP_OK;
 }
 
+// CEP_BATCH_DELIVER host buffer: {match count, error flags, completion stamp, 0}, host_cap keys (int32,
+// padded to 8 bytes), then host_cap x k stream positions
+void dl_layout(const cep_session* s, int64_t*& hdr, int32_t*& hkey, int64_t*& hpos) {
+  hdr = static_cast<int64_t*>(s->dl);
+  hkey = reinterpret_cast<int32_t*>(hdr + 4);
+  hpos = hdr + 4 + (s->dl_cap + 1) / 2 + 1;
+}
+
 int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   const StencilProgram& SP = s->pat->prog.stencil;
   const void* col = b->n_cols ? b->cols[SP.col] : nullptr;
@@ -346,7 +385,7 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     HostArr arrs[3] = {{key, size_t(b->n) * 4, reinterpret_cast<const void**>(&key)},
                        {col, size_t(b->n) * vs, &col},
                        {topic, size_t(b->n) * 4, reinterpret_cast<const void**>(&topic)}};
-    int rc = stage_host(s, arrs, SP.use_topic ? 3 : 2, st);
+    int rc = stage_host(s, arrs, SP.use_topic ? 3 : 2, st, true);
     if (rc) return rc;
   }
   if (SP.use_topic && !topic && b->n > 0) {          // no topic column: every record on topic id 0
@@ -377,20 +416,22 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     const int k = SP.k;
     const int64_t host_cap = std::min<int64_t>(s->out_cap, int64_t(1) << 20);
     if (!s->dl) {
-      const size_t bytes = 8 * (2 + size_t(host_cap + 1) / 2 + 1) + size_t(host_cap) * size_t(k) * 8;   // see hpos
+      const size_t bytes = 8 * (4 + size_t(host_cap + 1) / 2 + 1) + size_t(host_cap) * size_t(k) * 8;   // see dl_layout
       HIPCHECK(hipHostMalloc(&s->dl, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+      memset(s->dl, 0, 32);
       s->dl_cap = host_cap;
+      if (s->dl_ticket.ensure(16)) return fail(CEP_E_HIP, "allocation failed");
+      HIPCHECK(hipMemsetAsync(s->dl_ticket.p, 0, 16, st));
     }
     if (s->out_cap > host_cap &&
         (s->mkey.ensure(size_t(s->out_cap) * 4) || s->opos.ensure(size_t(s->out_cap) * size_t(k) * 8)))
       return fail(CEP_E_HIP, "allocation failed");
-    int64_t* hdr = static_cast<int64_t*>(s->dl);
-    L.deliver.hdr = hdr;
-    L.deliver.hkey = reinterpret_cast<int32_t*>(hdr + 2);
-    L.deliver.hpos = hdr + 2 + (s->dl_cap + 1) / 2 + 1;
+    dl_layout(s, L.deliver.hdr, L.deliver.hkey, L.deliver.hpos);
     L.deliver.dkey = s->mkey.as<int32_t>();
     L.deliver.dpos = s->opos.as<int64_t>();
     L.deliver.host_cap = s->dl_cap;
+    L.deliver.ticket = s->dl_ticket.as<unsigned>();
+    L.deliver.stamp = ++s->dl_stamp;
     s->delivered = true;
   }
   HIPCHECK(stencil_launch(L, s->timing ? s->ev0 : nullptr, s->timing ? s->ev1 : nullptr, st));
@@ -783,6 +824,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.profile = s->r_prof.as<int64_t>();
   }
   bool timed = false;
+  bool pool_at_limit = false;                      // the pool cannot grow further: overflowing keys are handed back
   int64_t tots[2] = {0, 0};                        // matches, entries of the batch
   for (int attempt = 0;; attempt++) {
     if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
@@ -794,7 +836,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.ctab = s->carry ? s->ctab.as<int64_t>() : nullptr;
     A.cpool = s->carry ? s->cpool.as<int32_t>() : nullptr;
     A.cpool_cap = s->carry ? s->cpool_words : 0;
-    A.last_attempt = attempt >= kMaxRetry ? 1 : 0;     // then an overflowing key is handed back per key
+    A.last_attempt = attempt >= kMaxRetry || pool_at_limit ? 1 : 0;   // then an overflowing key is handed back per key
     A.max_key_words = s->opts.max_key_words;
     unsigned long long init[6] = {0, (unsigned long long)s->cpool_used, 0, 0, 0, 0};   // [5]: heavy count
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
@@ -822,11 +864,17 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       if (s->carry) s->cpool_used = int64_t(res[1]);
       break;
     }
-    if (attempt >= kMaxRetry && fl[0]) return fail(CEP_E_RUN_CAPACITY, "the NFA workspace pool cannot grow");
+    if ((attempt >= kMaxRetry || pool_at_limit) && fl[0])
+      return fail(CEP_E_RUN_CAPACITY, "the NFA workspace pool cannot grow");
     if (attempt >= kMaxRetry && fl[1]) return fail(CEP_E_RUN_CAPACITY, "the carried-state pool cannot grow");
-    if (fl[0]) {                                   // workspace pool exhausted: twice the pool, same inputs
-      s->pool.release();
-      s->pool_words *= 2;
+    if (fl[0]) {                                   // workspace pool exhausted: twice the pool, same inputs,
+      s->pool.release();                           // but no more than the device's free HBM allows (keeping
+      size_t free_b = 0, total_b = 0;              // 1/16 of it): only then is a key handed back per key
+      HIPCHECK(hipMemGetInfo(&free_b, &total_b));
+      const int64_t room = int64_t(free_b / 4) - int64_t(free_b / 64);
+      const int64_t want = std::min<int64_t>(s->pool_words * 2, room);
+      if (want <= s->pool_words) pool_at_limit = true;
+      else s->pool_words = want;
     }
     if (fl[1]) {                                   // carry pool exhausted: compact into a larger one
       if ((rc = carry_gc(s, 2 * s->cpool_words, st))) return rc;
@@ -1056,7 +1104,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 
 void cep_session_close(cep_session* s) {
   if (!s) return;
-  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->heavy, &s->dstage,
+  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->heavy, &s->dstage, &s->dl_ticket,
                   &s->h_topic, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
@@ -1180,7 +1228,12 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
                                             !(b->flags & CEP_BATCH_OFFSETS_MONOTONE));
   s->h2d_wait = false;
   s->delivered = false;
+  s->zc_slot = -1;
   int rc = push_dispatch(s, b, st, stencil_batch);
+  if (s->zc_slot >= 0) {                           // the ring slot is free again once the kernels are done
+    HIPCHECK(hipEventRecord(s->ring_ev[s->zc_slot], st));
+    s->zc_slot = -1;
+  }
   if (s->h2d_wait) {                               // the caller's pinned columns are borrowed only for the call
     s->h2d_wait = false;
     HIPCHECK(hipEventSynchronize(s->h2d_ev));
@@ -1285,10 +1338,24 @@ int cep_collect(cep_session* s, cep_matches* o) {
   } else if (s->delivered) {                       // CEP_BATCH_DELIVER: the device wrote the CSR's inputs
     const StencilProgram& SP = s->pat->prog.stencil;
     const int k = SP.k;
-    HIPCHECK(hipStreamSynchronize(s->stream));
-    const int64_t* hdr = static_cast<const int64_t*>(s->dl);
-    const int32_t* hkey = reinterpret_cast<const int32_t*>(hdr + 2);
-    const int64_t* hpos = hdr + 2 + (s->dl_cap + 1) / 2 + 1;
+    int64_t* hdr;
+    int32_t* hkey;
+    int64_t* hpos;
+    dl_layout(s, hdr, hkey, hpos);
+    // the delivery kernel's last workgroup stamps hdr[2] once every row is in host memory: spin on it (a
+    // stream wait sleeps and wakes microseconds late); a stamp that does not come -- a fault -- is left
+    // to the stream wait, which reports it
+    const volatile int64_t* stamp = hdr + 2;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*stamp != s->dl_stamp) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+        HIPCHECK(hipStreamSynchronize(s->stream));
+        if (*stamp != s->dl_stamp) return fail(CEP_E_HIP, "the delivery kernel did not complete");
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
     const int64_t nm = hdr[0];
     const uint64_t hf = uint64_t(hdr[1]);
     if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
@@ -1827,6 +1894,136 @@ int cep_state_evict(cep_session* s, const int32_t* keys, int64_t n, const uint8_
     HIPCHECK(hipMemcpy(s->ctab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
   }
   *blobs = out.data();
+  return CEP_OK;
+}
+
+// A key's carried NFA state (one "KCST" key) in the reference's own terms -- "KCRF", version 1, little
+// endian, strings as i32 length + UTF-8 bytes:
+//   u32 magic, u32 version, i32 key id, i32 n_cols, i64 runs                      NFAStates.runs (NFA.runs)
+//   i32 n, n x {i32 topic id, i64 offset}              NFAStates.latestOffsets: the next record's minimum
+//   i32 n, n x {i64 stream position, i32 topic id, i32 partition, i64 offset, i64 timestamp,
+//               n_cols x i64 value bits}               the events the buffer still holds (MatchedEvent)
+//   i32 n, n x {i32 stage id, i32 epsilon target (-1: the stage itself), i32 flags (1 isBranching,
+//               2 isIgnored), i64 sequence, i32 last event (index above, -1 null), i64 timestamp (-1:
+//               never read -- within() is inert), i32 n_digits, n_digits x i32}
+//                                                      the run queue (ComputationStage, FIFO order)
+//   i32 n, n x {str stage name, i32 stage type, i32 event, i64 refs, i32 n_preds, n_preds x {i32 n_digits,
+//               n_digits x i32, i32 has predecessor, str predecessor stage name, i32 its type, i32 its
+//               event}}                                 buffer nodes Matched -> MatchedEvent, preds in order
+//   i32 n, n x {str state name, i64 sequence, i32 type (1 int, 2 long, 3 double), i64 value bits}
+//                                                      aggregates (record key, state, sequence) -> value
+// Sequences are renumbered densely from 0 (runs sharing one share its aggregates); every new run the
+// reference creates gets ++runs, beyond them.
+int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, void* out, size_t cap,
+                           size_t* needed) {
+  if (!p || !blob || !needed) return fail(CEP_E_ARG, "null argument");
+  const Program& P = p->prog;
+  const uint8_t* in = static_cast<const uint8_t*>(blob);
+  uint32_t magic = 0;
+  int32_t nkeys = 0;
+  if (len < 20) return fail(CEP_E_ARG, "bad state blob");
+  memcpy(&magic, in, 4);
+  memcpy(&nkeys, in + 16, 4);
+  if (magic != kStateMagic) return fail(CEP_E_ARG, "not a general-path (KCST) state blob");
+  if (nkeys != 1) return fail(CEP_E_ARG, "cep_state_to_reference takes a single-key blob (cep_state_evict)");
+  if (len < 28) return fail(CEP_E_ARG, "truncated state blob");
+  int32_t key = 0, w = 0;
+  memcpy(&key, in + 20, 4);
+  memcpy(&w, in + 24, 4);
+  if (w < CB_HDR || 28 + size_t(w) * 4 > len) return fail(CEP_E_ARG, "truncated state blob");
+  std::vector<int32_t> b(static_cast<size_t>(w));
+  memcpy(b.data(), in + 28, size_t(w) * 4);
+  const int nhwm = b[CB_NHWM], qlen = b[CB_QLEN], nev = b[CB_NEV], nnode = b[CB_NNODE], npred = b[CB_NPRED];
+  const int nver = b[CB_NVER], nseq = b[CB_NSEQ], ncols = b[CB_NCOLS], nst = b[CB_NSTATES];
+  const int evw = 8 + 2 * ncols;
+  const int64_t total = int64_t(CB_HDR) + 3 * nhwm + 4 * qlen + int64_t(evw) * nev + 4 * nnode + 4 * npred + nver +
+                        int64_t(3) * nst * nseq;
+  if (ncols != int(P.coltypes.size()) || nst != P.dev.nstates || total != w) return fail(CEP_E_ARG, "state blob does not match the pattern");
+  // buffer-node slot -> (stage name, stage type), as lower_general numbers them (Matched.java:31-35)
+  std::vector<std::pair<int, int>> slot(size_t(P.dev.nslots), {0, 0});
+  for (const auto& st : P.stages) slot[size_t(P.dev.st[st.id].slot)] = {st.name, st.type};
+  const int32_t* hw = b.data() + CB_HDR;
+  const int32_t* q = hw + 3 * nhwm;
+  const int32_t* ev = q + 4 * qlen;
+  const int32_t* nd = ev + int64_t(evw) * nev;
+  const int32_t* pr = nd + 4 * nnode;
+  const int32_t* vs = pr + 4 * npred;
+  const int32_t* ag = vs + nver;
+  auto w64 = [](const int32_t* x) { return int64_t(uint64_t(uint32_t(x[0])) | (uint64_t(uint32_t(x[1])) << 32)); };
+  std::vector<uint8_t> o;
+  auto i32 = [&](int32_t v) { const size_t at = o.size(); o.resize(at + 4); memcpy(o.data() + at, &v, 4); };
+  auto i64 = [&](int64_t v) { const size_t at = o.size(); o.resize(at + 8); memcpy(o.data() + at, &v, 8); };
+  auto str = [&](const std::string& t) { i32(int32_t(t.size())); o.insert(o.end(), t.begin(), t.end()); };
+  auto version = [&](int at) {
+    if (at < 0 || at >= nver || vs[at] < 0 || at + vs[at] >= nver) return false;
+    i32(vs[at]);
+    for (int d = 1; d <= vs[at]; d++) i32(vs[at + d]);
+    return true;
+  };
+  i32(int32_t(0x4652434Bu));                        // "KCRF"
+  i32(1);
+  i32(key);
+  i32(ncols);
+  i64(w64(b.data() + CB_RUNS_LO));
+  i32(nhwm);
+  for (int h = 0; h < nhwm; h++) { i32(hw[3 * h]); i64(w64(hw + 3 * h + 1)); }
+  i32(nev);
+  for (int e = 0; e < nev; e++) {
+    const int32_t* x = ev + int64_t(evw) * e;
+    i64(w64(x)); i32(x[2]); i32(x[3]); i64(w64(x + 4)); i64(w64(x + 6));
+    for (int c = 0; c < ncols; c++) i64(w64(x + 8 + 2 * c));
+  }
+  i32(qlen);
+  for (int r = 0; r < qlen; r++) {
+    const int32_t w0 = q[4 * r];
+    const int sid = w0 & 0xFF, eps = (w0 >> 8) & 0xFF;
+    if (sid >= int(P.stages.size()) || (eps != 0xFF && eps >= int(P.stages.size()))) return fail(CEP_E_ARG, "bad run in state blob");
+    i32(sid);
+    i32(eps == 0xFF ? -1 : eps);
+    i32(((w0 >> 16) & 1) | (((w0 >> 17) & 1) << 1));
+    i64(q[4 * r + 3]);
+    i32(q[4 * r + 2]);
+    i64(-1);
+    if (!version(q[4 * r + 1])) return fail(CEP_E_ARG, "bad version in state blob");
+  }
+  i32(nnode);
+  for (int i = 0; i < nnode; i++) {
+    const int32_t* x = nd + 4 * i;
+    if (x[0] < 0 || x[0] >= P.dev.nslots) return fail(CEP_E_ARG, "bad node in state blob");
+    str(P.names[size_t(slot[size_t(x[0])].first)]);
+    i32(slot[size_t(x[0])].second);
+    i32(x[1]);
+    i64(x[2]);
+    int cnt = 0;
+    for (int pi = x[3]; pi >= 0 && cnt <= npred; pi = pr[4 * pi + 3]) cnt++;
+    if (cnt > npred) return fail(CEP_E_ARG, "bad predecessor list in state blob");
+    i32(cnt);
+    for (int pi = x[3]; pi >= 0; pi = pr[4 * pi + 3]) {
+      const int32_t* y = pr + 4 * pi;
+      if (!version(y[0])) return fail(CEP_E_ARG, "bad version in state blob");
+      const bool has = y[1] >= 0;
+      i32(has ? 1 : 0);
+      str(has ? P.names[size_t(slot[size_t(y[1])].first)] : std::string());
+      i32(has ? slot[size_t(y[1])].second : 0);
+      i32(has ? y[2] : -1);
+    }
+  }
+  int32_t nagg = 0;
+  for (int64_t i = 0; i < int64_t(nst) * nseq; i++) nagg += ag[3 * i] != 0;
+  i32(nagg);
+  for (int sq = 0; sq < nseq; sq++)
+    for (int st = 0; st < nst; st++) {
+      const int32_t* a = ag + (int64_t(sq) * nst + st) * 3;
+      if (!a[0]) continue;                          // unset: States.get would throw
+      str(P.states[size_t(st)]);
+      i64(sq);
+      i32(a[0]);
+      i64(w64(a + 1));
+    }
+  *needed = o.size();
+  if (!out) return CEP_OK;
+  if (cap < o.size()) return fail(CEP_E_ARG, "buffer too small");
+  memcpy(out, o.data(), o.size());
   return CEP_OK;
 }
 

@@ -163,6 +163,8 @@ struct DeliverArgs {
   int32_t* dkey = nullptr;        // device: the same past host_cap
   int64_t* dpos = nullptr;
   int64_t host_cap = 0;
+  unsigned* ticket = nullptr;     // device: workgroups done (the last one stamps hdr[2] = stamp; reset to 0)
+  int64_t stamp = 0;              // this delivery's number: cep_collect spins until hdr[2] holds it
 };
 struct StencilLaunch {
   const int32_t* key;

@@ -143,48 +143,66 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
   }
 }
 
-// Small carry batches collected at once (CEP_BATCH_DELIVER: a processor flush): stencil_finish_small
-// and stencil_deliver in one launch -- the scan of <= 1024 super-tile counts, then one lane per match
-// expands its slot into the k-int row (kept on the device for cep_checksum) and hands the row's stream
-// positions and the match's key to pinned host memory.  One launch fewer on the flush's critical path.
-__global__ __launch_bounds__(1024) void stencil_finish_deliver(const int32_t* __restrict__ slots,
-                                                               const int64_t* __restrict__ cnt, int64_t nt, int k,
-                                                               int32_t* __restrict__ out, int64_t out_cap, int sub,
-                                                               int64_t* __restrict__ total,
-                                                               unsigned long long* __restrict__ clear_flag,
-                                                               SlotFormat F, const int32_t* __restrict__ key,
-                                                               StencilCarry C, int64_t host_cap, int64_t* __restrict__ hdr,
-                                                               int32_t* __restrict__ hkey, int64_t* __restrict__ hpos,
-                                                               int32_t* __restrict__ dkey, int64_t* __restrict__ dpos) {
-  __shared__ int64_t s_pre[SMALL_FINISH + 1];
-  __shared__ int64_t s_w[16];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t c = tid < nt ? cnt[tid] : 0;
-  int64_t incl = c;
+// The end of a delivered batch: the last workgroup to finish (a ticket in device memory) stamps the host
+// header, after every workgroup's writes were made visible to the host -- cep_collect spins on that word
+// instead of waiting for the stream (one wake-up latency fewer per flush).
+__device__ __forceinline__ void deliver_done(unsigned* ticket, unsigned nblocks, int64_t* hdr, int64_t stamp) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    const unsigned prev = atomicAdd(ticket, 1u);
+    if (prev == nblocks - 1) {
+      __threadfence_system();
+      *ticket = 0;                                   // ready for the next batch
+      *reinterpret_cast<volatile int64_t*>(hdr + 2) = stamp;
+    }
+  }
+}
+
+// Small carry batches collected at once (CEP_BATCH_DELIVER: a processor flush, <= 1024 super-tiles):
+// scan, rows and delivery in one launch, one workgroup per super-tile.  Each workgroup sums the counts
+// before its super-tile itself (<= 1024 of them: no separate scan launch), then one thread per match
+// expands the slot into the k-int row (kept on the device for cep_checksum) and hands the row's stream
+// positions and the match's key to pinned host memory.
+__global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __restrict__ slots,
+                                                              const int64_t* __restrict__ cnt, int64_t nt, int k,
+                                                              int32_t* __restrict__ out, int64_t out_cap, int sub,
+                                                              int64_t* __restrict__ total,
+                                                              unsigned long long* __restrict__ clear_flag,
+                                                              SlotFormat F, const int32_t* __restrict__ key,
+                                                              StencilCarry C, int64_t host_cap, int64_t* __restrict__ hdr,
+                                                              int32_t* __restrict__ hkey, int64_t* __restrict__ hpos,
+                                                              int32_t* __restrict__ dkey, int64_t* __restrict__ dpos,
+                                                              unsigned* ticket, int64_t stamp) {
+  __shared__ int64_t s_red[2][4];
+  const int64_t t = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t before = 0, all = 0;
+  for (int64_t i = threadIdx.x; i < nt; i += 256) {
+    const int64_t c = cnt[i];
+    all += c;
+    if (i < t) before += c;
+  }
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
+  for (int d = 32; d >= 1; d >>= 1) {
+    before += __shfl_xor(before, d, 64);
+    all += __shfl_xor(all, d, 64);
   }
-  if (lane == 63) s_w[wid] = incl;
+  if (lane == 0) { s_red[0][wid] = before; s_red[1][wid] = all; }
   __syncthreads();
-  int64_t run = incl - c;
-  for (int w = 0; w < wid; w++) run += s_w[w];
-  s_pre[tid] = run;
-  if (tid == 1023) {
-    s_pre[SMALL_FINISH] = run + c;
-    *total = run + c;
-    hdr[0] = run + c;
-    hdr[1] = int64_t(*C.flags);                    // this batch's error flags (the kernel is done)
+  const int64_t pre = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+  const int64_t tot = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
+  if (t == 0 && threadIdx.x == 0) {
+    *total = tot;
+    hdr[0] = tot;
+    hdr[1] = int64_t(*C.flags);                    // this batch's error flags (the count kernel is done)
+    if (clear_flag) *clear_flag = 0;               // the next batch's error-flag word
   }
-  if (tid == 0 && clear_flag) *clear_flag = 0;    // the next batch's error-flag word
-  __syncthreads();
-  for (int64_t t = wid; t < nt; t += 16) {                 // one wave per super-tile, one lane per match
-    const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
-    if (pre + m > out_cap) continue;
+  const int64_t m = cnt[t];
+  if (pre + m <= out_cap) {
     const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
     const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
-    for (int64_t q = lane; q < m; q += 64) {
+    for (int64_t q = threadIdx.x; q < m; q += 256) {
       const int64_t i = pre + q;
       int32_t row[STENCIL_MAX_K], last = 0;
 #pragma unroll
@@ -210,6 +228,7 @@ __global__ __launch_bounds__(1024) void stencil_finish_deliver(const int32_t* __
       else dkey[i] = kk;
     }
   }
+  deliver_done(ticket, unsigned(gridDim.x), hdr, stamp);
 }
 
 static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
@@ -228,8 +247,7 @@ static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
 }
 
 hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k, const int64_t* total, int64_t out_cap,
-                                  const StencilCarry& C, int64_t host_cap, int64_t* hdr, int32_t* hkey, int64_t* hpos,
-                                  int32_t* dkey, int64_t* dpos, hipStream_t st);
+                                  const StencilCarry& C, const DeliverArgs& D, hipStream_t st);
 
 // stencil_kernel (timed as the dominant kernel between ev0 and ev1), then the
 // tile-count scan and the gather into the contiguous output
@@ -242,8 +260,7 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
     if (e == hipSuccess) e = hipMemsetAsync(L.total, 0, sizeof(int64_t), st);
     if (e == hipSuccess && D.hdr)                  // an empty delivery: the header only
-      e = stencil_deliver_launch(L.key, L.out, L.k, L.total, 0, L.carry, D.host_cap, D.hdr, D.hkey, D.hpos, D.dkey,
-                                 D.dpos, st);
+      e = stencil_deliver_launch(L.key, L.out, L.k, L.total, 0, L.carry, D, st);
     return e;
   }
   const int64_t ntiles = (L.n + ST_TILE - 1) / ST_TILE;
@@ -256,9 +273,9 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
   const SlotFormat F{L.k, L.plain && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
   if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr) {   // a small carry flush: scan, rows and delivery at once
-    hipLaunchKernelGGL(stencil_finish_deliver, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k, L.out,
-                       L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey, D.hpos,
-                       D.dkey, D.dpos);
+    hipLaunchKernelGGL(stencil_finish_deliver, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, nsuper,
+                       L.k, L.out, L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey,
+                       D.hpos, D.dkey, D.dpos, D.ticket, D.stamp);
     return hipGetLastError();
   }
   if (nsuper <= SMALL_FINISH) {
@@ -274,8 +291,7 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (D.hdr) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return stencil_deliver_launch(L.key, L.out, L.k, L.total, L.out_cap, L.carry, D.host_cap, D.hdr, D.hkey, D.hpos,
-                                  D.dkey, D.dpos, st);
+    return stencil_deliver_launch(L.key, L.out, L.k, L.total, L.out_cap, L.carry, D, st);
   }
   return hipGetLastError();
 }
@@ -337,7 +353,8 @@ __global__ __launch_bounds__(256) void stencil_deliver(const int32_t* __restrict
                                                        int k, const int64_t* __restrict__ total, int64_t out_cap,
                                                        StencilCarry C, int64_t host_cap, int64_t* __restrict__ hdr,
                                                        int32_t* __restrict__ hkey, int64_t* __restrict__ hpos,
-                                                       int32_t* __restrict__ dkey, int64_t* __restrict__ dpos) {
+                                                       int32_t* __restrict__ dkey, int64_t* __restrict__ dpos,
+                                                       unsigned* ticket, int64_t stamp) {
   const int64_t t = *total, nm = t < out_cap ? t : out_cap;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     hdr[0] = t;
@@ -358,13 +375,13 @@ __global__ __launch_bounds__(256) void stencil_deliver(const int32_t* __restrict
     if (host) hkey[i] = kk;
     else dkey[i] = kk;
   }
+  deliver_done(ticket, unsigned(gridDim.x), hdr, stamp);
 }
 hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k, const int64_t* total, int64_t out_cap,
-                                  const StencilCarry& C, int64_t host_cap, int64_t* hdr, int32_t* hkey, int64_t* hpos,
-                                  int32_t* dkey, int64_t* dpos, hipStream_t st) {
+                                  const StencilCarry& C, const DeliverArgs& D, hipStream_t st) {
   const int64_t blocks = std::min<int64_t>((out_cap + 255) / 256, 1024);
   hipLaunchKernelGGL(stencil_deliver, dim3(unsigned(std::max<int64_t>(blocks, 1))), dim3(256), 0, st, key, out, k, total,
-                     out_cap, C, host_cap, hdr, hkey, hpos, dkey, dpos);
+                     out_cap, C, D.host_cap, D.hdr, D.hkey, D.hpos, D.dkey, D.dpos, D.ticket, D.stamp);
   return hipGetLastError();
 }
 

@@ -75,7 +75,7 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_batch_errors", "cep_session_set_timing",
            "cep_key_profile", "cep_key_hash", "cep_key_shard", "cep_shard_plan", "cep_partition", "cep_gather",
            "cep_match_count_to", "cep_state_evict", "cep_state_import_keys", "cep_state_positions",
-           "cep_session_set_max_key_words"]
+           "cep_session_set_max_key_words", "cep_state_to_reference", "cep_pattern_check"]
 
 _lib = None
 
@@ -142,6 +142,7 @@ def lib():
         L.cep_state_import_keys.argtypes = [P, P, P, P, C.c_int64]
         L.cep_state_positions.argtypes = [P, C.c_size_t, P, C.c_int64, C.POINTER(C.c_int64)]
         L.cep_session_set_max_key_words.argtypes = [P, C.c_int64]
+    L.cep_state_to_reference.argtypes = [P, C.c_char_p, C.c_size_t, P, C.c_size_t, C.POINTER(C.c_size_t)]
     L.cep_last_error.restype = C.c_char_p
     L.cep_version.restype = C.c_char_p
     _lib = L
@@ -187,6 +188,16 @@ class CompiledPattern:
             ne = L.cep_pattern_stage(self.h, s, C.byref(nm), C.byref(ty), C.byref(w), ops, tg, 16)
             out.append((self.names[nm.value], ty.value, w.value, [(ops[i], tg[i]) for i in range(ne)]))
         return out
+
+    def state_to_reference(self, blob: bytes) -> bytes:
+        """cep_state_to_reference: a single-key KCST blob (Session.state_evict) in the reference's own
+        terms ("KCRF"): NFA.runs, high-water marks, run queue, buffer nodes, aggregates, their events."""
+        L = lib()
+        n = C.c_size_t()
+        check(L.cep_state_to_reference(self.h, blob, len(blob), None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        check(L.cep_state_to_reference(self.h, blob, len(blob), buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
 
     def kernel_source(self, path=PATH_RUNS) -> str:
         """HIP source of the kernels compiled for this pattern (cep_pattern_kernel_source)."""
@@ -271,10 +282,10 @@ class Session:
         check(lib().cep_collect(self.h, C.byref(m)))
         nm, ne = m.n_matches, m.n_entries
 
-        def arr(p, n, dt):
+        def arr(p, n, dt):                                # one copy out of the library-owned CSR
             if n == 0:
                 return np.zeros(0, dt)
-            return np.ctypeslib.as_array(p, shape=(n,)).copy()
+            return np.frombuffer(C.string_at(p, n * np.dtype(dt).itemsize), dt)
 
         out = dict(match_record=arr(m.match_record, nm, np.int64), match_key=arr(m.match_key, nm, np.int32),
                    ent_off=arr(m.ent_off, nm + 1, np.int64), ent_name=arr(m.ent_name, ne, np.int32),

@@ -1298,10 +1298,15 @@ static Inst* get_inst(orc_run* R, int32_t key, int create) {
   return &R->inst.a[R->inst.n - 1];
 }
 
-int orc_run_batch(orc_run* R, const orc_batch* b) {
+static int run_from(orc_run* R, const orc_batch* b, int64_t r0);
+
+int orc_run_batch(orc_run* R, const orc_batch* b) { return run_from(R, b, 0); }
+
+/* CEPProcessor.process for records r0..n-1 of the bound batch (:134-160) */
+static int run_from(orc_run* R, const orc_batch* b, int64_t r0) {
   R->b = b;
   if (R->p->begin < 0) return ORC_E_NPE;
-  for (int64_t r = 0; r < b->n; r++) {
+  for (int64_t r = r0; r < b->n; r++) {
     int proc = R->mode == ORC_MODE_PROCESSOR;
     if (proc && b->valid && !b->valid[r]) continue;   /* CEPProcessor.java:136-138 */
     Inst* I = get_inst(R, b->key[r], 1);
@@ -1327,6 +1332,117 @@ int orc_run_batch(orc_run* R, const orc_batch* b) {
     }
   }
   return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* continuing a key from its state in the reference's terms ("KCRF", libkcep  */
+/* cep_state_to_reference): NFAStates (runs, run queue, latestOffsets), the   */
+/* buffer's MatchedEvent nodes and the aggregates, rebuilt as the reference   */
+/* stores would hold them (NFAStates.java:33-109, MatchedEvent.java:27-169,   */
+/* AggregatesStoreImpl.java:30-76); then CEPProcessor.process per record.     */
+/* ------------------------------------------------------------------------- */
+static int32_t rd_i32(Rd* r) { return (int32_t)rd_u32(r); }
+static char* rd_lstr(Rd* r) {                      /* i32 length + bytes */
+  int32_t n = rd_i32(r);
+  if (n < 0 || !rd_ok(r, (size_t)n)) { r->bad = 1; return NULL; }
+  char* c = xmalloc((size_t)n + 1);
+  memcpy(c, r->p + r->i, (size_t)n); c[n] = 0; r->i += (size_t)n;
+  return c;
+}
+static Dewey* rd_dewey(orc_run* R, Rd* r) {
+  int32_t nd = rd_i32(r);
+  if (nd < 0 || nd > 1 << 20) { r->bad = 1; return NULL; }
+  Dewey* v = dw_new(&R->arena, nd);
+  for (int i = 0; i < nd; i++) v->d[i] = rd_i32(r);
+  return v;
+}
+static int name_id(const orc_pattern* p, const char* s) {
+  for (int64_t i = 0; i < p->names.n; i++) if (!strcmp(p->names.a[i], s)) return (int)i;
+  return -1;
+}
+static int state_id(const orc_pattern* p, const char* s) {
+  for (int64_t i = 0; i < p->states.n; i++) if (!strcmp(p->states.a[i], s)) return (int)i;
+  return -1;
+}
+
+int orc_run_resume(orc_run* R, const orc_batch* b, const uint8_t* st, size_t len) {
+  Rd r = {st, len, 0, 0};
+  R->b = b;
+  if (rd_u32(&r) != 0x4652434Bu || rd_u32(&r) != 1) return ORC_E_BAD_IR;
+  const int32_t key = rd_i32(&r), ncols = rd_i32(&r);
+  const int64_t runs = rd_i64(&r);
+  if (ncols != R->p->ncols) return ORC_E_BAD_IR;
+  Inst* I = get_inst(R, key, 1);
+  VFREE(I->q); memset(&I->q, 0, sizeof I->q);
+  I->runs = runs;
+  I->nh = rd_i32(&r);
+  if (I->nh < 0 || I->nh > 16) return ORC_E_BAD_IR;
+  for (int h = 0; h < I->nh; h++) { I->h_topic[h] = rd_i32(&r); I->h_off[h] = rd_i64(&r); }
+  const int32_t nev = rd_i32(&r);
+  if (nev < 0 || nev > b->n) return ORC_E_BAD_IR;
+  for (int32_t e = 0; e < nev && !r.bad; e++) {    /* the batch starts with exactly these events */
+    rd_i64(&r);
+    const int32_t tp = rd_i32(&r), part = rd_i32(&r);
+    const int64_t off = rd_i64(&r), ts = rd_i64(&r);
+    for (int c = 0; c < ncols; c++) rd_i64(&r);
+    if (b->key[e] != key || ev_topic(b, e) != tp || ev_part(b, e) != part || ev_off(b, e) != off || ev_ts(b, e) != ts)
+      return ORC_E_BAD_IR;
+  }
+  const int32_t qlen = rd_i32(&r);
+  for (int32_t i = 0; i < qlen && !r.bad; i++) {
+    SRef sr;
+    sr.sid = rd_i32(&r); sr.eps = rd_i32(&r);
+    const int32_t flags = rd_i32(&r);
+    const int64_t seq = rd_i64(&r);
+    const int32_t ev = rd_i32(&r);
+    const int64_t ts = rd_i64(&r);
+    Dewey* v = rd_dewey(R, &r);
+    if (r.bad || sr.sid < 0 || sr.sid >= R->p->nstages || sr.eps >= R->p->nstages || ev >= nev) return ORC_E_BAD_IR;
+    VPUSH(I->q, mk_run(sr, v, ev, ts, seq, flags & 1, (flags >> 1) & 1));
+  }
+  const int32_t nnode = rd_i32(&r);
+  for (int32_t i = 0; i < nnode && !r.bad; i++) {
+    char* nm = rd_lstr(&r);
+    const int32_t type = rd_i32(&r), ev = rd_i32(&r);
+    const int64_t refs = rd_i64(&r);
+    const int32_t np = rd_i32(&r);
+    const int id = nm ? name_id(R->p, nm) : -1;
+    free(nm);
+    if (id < 0 || ev < 0 || ev >= nev || np < 0) return ORC_E_BAD_IR;
+    Key4 k = {{((int64_t)id << 8) | type, ev_topic(b, ev), ev_part(b, ev), ev_off(b, ev)}};
+    Node* n = node_new(R, &k, ev, refs);
+    for (int32_t j = 0; j < np && !r.bad; j++) {
+      Dewey* v = rd_dewey(R, &r);
+      const int32_t has = rd_i32(&r);
+      char* pn = rd_lstr(&r);
+      const int32_t ptype = rd_i32(&r), pev = rd_i32(&r);
+      const int pid = has && pn ? name_id(R->p, pn) : -1;
+      free(pn);
+      if (has && (pid < 0 || pev < 0 || pev >= nev)) return ORC_E_BAD_IR;
+      Key4 pk = {{((int64_t)pid << 8) | ptype, has ? ev_topic(b, pev) : 0, has ? ev_part(b, pev) : 0,
+                  has ? ev_off(b, pev) : 0}};
+      n = node_get(R, &k);                            /* (node_new may move the pool) */
+      node_add_pred(n, v, has ? &pk : NULL);
+    }
+  }
+  const int32_t nagg = rd_i32(&r);
+  for (int32_t i = 0; i < nagg && !r.bad; i++) {
+    char* sn = rd_lstr(&r);
+    const int64_t seq = rd_i64(&r);
+    const int32_t t = rd_i32(&r);
+    const int64_t bits = rd_i64(&r);
+    const int sid = sn ? state_id(R->p, sn) : -1;
+    free(sn);
+    if (sid < 0 || t < ORC_T_I32 || t > ORC_T_F64) return ORC_E_BAD_IR;
+    Val v; memset(&v, 0, sizeof v);
+    v.t = (uint8_t)t;
+    if (t == ORC_T_I32) v.u.i = (int32_t)bits;
+    else if (t == ORC_T_I64) v.u.l = bits;
+    else memcpy(&v.u.d, &bits, 8);
+    agg_put(R, key, sid, seq, v);
+  }
+  if (r.bad || r.i != len) return ORC_E_BAD_IR;
+  return run_from(R, b, nev);
 }
 
 int64_t orc_err_record(const orc_run* R) { return R->err_record; }
@@ -1400,6 +1516,8 @@ int orc_svb_get(orc_run* R, int sid, int64_t ev, const char* version, int remove
 typedef struct {
   const orc_pattern* p; const orc_batch* b; int mode; int64_t lo, hi;
   int64_t matches; uint64_t sum; int err;
+  int csr;                                            /* also keep every match, in emission order */
+  VEC(int64_t) mrec; VEC(int32_t) mkey; VEC(int64_t) elen; VEC(int32_t) ename; VEC(int64_t) erec;
 } Shard;
 
 static void* shard_main(void* arg) {
@@ -1436,6 +1554,12 @@ static void* shard_main(void* arg) {
       for (int64_t i = x->eb; i < x->ee; i++)
         h = mix64(h ^ ((uint64_t)(R->ent_ev.a[i] + r) << 8) ^ (uint64_t)R->ent_name.a[i]);
       s->sum += h;
+      if (s->csr) {
+        VPUSH(s->mrec, x->record + r);
+        VPUSH(s->mkey, x->key);
+        VPUSH(s->elen, x->ee - x->eb);
+        for (int64_t i = x->eb; i < x->ee; i++) { VPUSH(s->ename, R->ent_name.a[i]); VPUSH(s->erec, R->ent_ev.a[i] + r); }
+      }
     }
     s->matches += R->m.n;
     orc_run_free(R);
@@ -1445,8 +1569,7 @@ static void* shard_main(void* arg) {
   return NULL;
 }
 
-int64_t orc_baseline(const orc_pattern* p, const orc_batch* b, int mode, int nthreads, uint64_t* checksum, int* err) {
-  if (nthreads < 1) nthreads = 1;
+static Shard* run_shards(const orc_pattern* p, const orc_batch* b, int mode, int nthreads, int csr) {
   Shard* sh = xcalloc((size_t)nthreads, sizeof(Shard));
   pthread_t* th = xcalloc((size_t)nthreads, sizeof(pthread_t));
   int64_t prev = 0;
@@ -1454,17 +1577,59 @@ int64_t orc_baseline(const orc_pattern* p, const orc_batch* b, int mode, int nth
     int64_t hi = t == nthreads - 1 ? b->n : (b->n * (t + 1)) / nthreads;
     if (hi < prev) hi = prev;
     while (hi > 0 && hi < b->n && b->key[hi] == b->key[hi - 1]) hi++;
-    sh[t].p = p; sh[t].b = b; sh[t].mode = mode; sh[t].lo = prev; sh[t].hi = hi;
+    sh[t].p = p; sh[t].b = b; sh[t].mode = mode; sh[t].lo = prev; sh[t].hi = hi; sh[t].csr = csr;
     prev = hi;
   }
   for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, shard_main, &sh[t]);
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(th);
+  return sh;
+}
+
+int64_t orc_baseline(const orc_pattern* p, const orc_batch* b, int mode, int nthreads, uint64_t* checksum, int* err) {
+  if (nthreads < 1) nthreads = 1;
+  Shard* sh = run_shards(p, b, mode, nthreads, 0);
   int64_t total = 0; uint64_t sum = 0; int e = 0;
-  for (int t = 0; t < nthreads; t++) {
-    pthread_join(th[t], NULL);
-    total += sh[t].matches; sum += sh[t].sum; if (sh[t].err) e = sh[t].err;
-  }
-  free(sh); free(th);
+  for (int t = 0; t < nthreads; t++) { total += sh[t].matches; sum += sh[t].sum; if (sh[t].err) e = sh[t].err; }
+  free(sh);
   if (checksum) *checksum = sum;
   if (err) *err = e;
   return total;
+}
+
+/* The same run keeping every match: the batch's CSR in key order (shards are contiguous whole-key
+   ranges), per key in emission order -- the order cep_collect returns for a key-grouped batch. */
+struct orc_csr { Shard* sh; int n; int64_t nm, ne; int err; };
+orc_csr* orc_baseline_csr(const orc_pattern* p, const orc_batch* b, int mode, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  orc_csr* c = xcalloc(1, sizeof(orc_csr));
+  c->sh = run_shards(p, b, mode, nthreads, 1);
+  c->n = nthreads;
+  for (int t = 0; t < nthreads; t++) { c->nm += c->sh[t].mrec.n; c->ne += c->sh[t].ename.n; if (c->sh[t].err) c->err = c->sh[t].err; }
+  return c;
+}
+void orc_csr_sizes(const orc_csr* c, int64_t* n_matches, int64_t* n_entries, int* err) {
+  *n_matches = c->nm; *n_entries = c->ne; *err = c->err;
+}
+void orc_csr_copy(const orc_csr* c, int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
+                  int64_t* ent_record) {
+  int64_t m = 0, e = 0;
+  for (int t = 0; t < c->n; t++) {
+    const Shard* s = &c->sh[t];
+    for (int64_t i = 0; i < s->mrec.n; i++, m++) {
+      match_record[m] = s->mrec.a[i]; match_key[m] = s->mkey.a[i]; ent_off[m] = e; e += s->elen.a[i];
+    }
+    memcpy(ent_name + (e - s->ename.n), s->ename.a, sizeof(int32_t) * (size_t)s->ename.n);
+    memcpy(ent_record + (e - s->erec.n), s->erec.a, sizeof(int64_t) * (size_t)s->erec.n);
+  }
+  ent_off[m] = e;
+}
+void orc_csr_free(orc_csr* c) {
+  if (!c) return;
+  for (int t = 0; t < c->n; t++) {
+    Shard* s = &c->sh[t];
+    VFREE(s->mrec); VFREE(s->mkey); VFREE(s->elen); VFREE(s->ename); VFREE(s->erec);
+  }
+  free(c->sh);
+  free(c);
 }

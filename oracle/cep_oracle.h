@@ -74,6 +74,10 @@ void orc_run_free(orc_run* r);
 /* process the batch records in order; returns ORC_OK or an error code (processing
  * stops at the failing record, like the Java task) */
 int orc_run_batch(orc_run* r, const orc_batch* b);
+/* Continue one key from its carried state in the reference's own terms ("KCRF", written by libkcep's
+ * cep_state_to_reference): the batch's first E records must be the state's E events (in order, same key,
+ * topic, partition, offset, timestamp); records E..n-1 are then processed as orc_run_batch does. */
+int orc_run_resume(orc_run* r, const orc_batch* b, const uint8_t* state, size_t len);
 int64_t orc_err_record(const orc_run* r);
 const char* orc_err_msg(const orc_run* r);
 
@@ -97,6 +101,15 @@ int orc_queue_entry(const orc_run* r, int32_t key, int64_t idx, int32_t* stage_i
  * Returns number of matches; *checksum = order-independent hash of matches. */
 int64_t orc_baseline(const orc_pattern* p, const orc_batch* b, int mode, int nthreads,
                      uint64_t* checksum, int* err);
+
+/* orc_baseline keeping every match: the CSR of the key-grouped batch, key order then per-key emission
+ * order (what cep_collect returns), for element-wise comparison at full size */
+typedef struct orc_csr orc_csr;
+orc_csr* orc_baseline_csr(const orc_pattern* p, const orc_batch* b, int mode, int nthreads);
+void orc_csr_sizes(const orc_csr* c, int64_t* n_matches, int64_t* n_entries, int* err);
+void orc_csr_copy(const orc_csr* c, int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
+                  int64_t* ent_record);
+void orc_csr_free(orc_csr* c);
 
 /* SharedVersionedBufferTest (SharedVersionedBufferTest.java:50-87): buffer puts and gets on the
  * events of a bound batch.  psid < 0 selects the 3-arg put.  orc_svb_get appends the traversal

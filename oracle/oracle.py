@@ -51,6 +51,12 @@ def lib():
         L.orc_run_new.restype = P
         L.orc_run_free.argtypes = [P]
         L.orc_run_batch.argtypes = [P, P]
+        L.orc_run_resume.argtypes = [P, P, C.c_char_p, C.c_size_t]
+        L.orc_baseline_csr.argtypes = [P, P, C.c_int, C.c_int]
+        L.orc_baseline_csr.restype = P
+        L.orc_csr_sizes.argtypes = [P, C.POINTER(I64), C.POINTER(I64), C.POINTER(C.c_int)]
+        L.orc_csr_copy.argtypes = [P, P, P, P, P, P]
+        L.orc_csr_free.argtypes = [P]
         L.orc_err_record.argtypes = [P]
         L.orc_err_record.restype = I64
         L.orc_err_msg.argtypes = [P]
@@ -172,6 +178,15 @@ class OracleRun:
         if rc:
             raise OracleError(rc, L.orc_err_msg(self.h).decode(), L.orc_err_record(self.h))
 
+    def resume(self, batch: BatchArrays, state: bytes):
+        """Continue one key from its state in the reference's terms ("KCRF", cep_state_to_reference):
+        the batch's first records are the state's events, the rest are processed."""
+        self._keep.append(batch)
+        L = lib()
+        rc = L.orc_run_resume(self.h, C.byref(batch.s), state, len(state))
+        if rc:
+            raise OracleError(rc, L.orc_err_msg(self.h).decode(), L.orc_err_record(self.h))
+
     def matches(self, with_groups=True):
         L = lib()
         out = []
@@ -247,6 +262,27 @@ def baseline(pattern: OraclePattern, batch: BatchArrays, mode=MODE_PROCESSOR, th
     if err.value:
         raise OracleError(err.value, "baseline failed")
     return n, cs.value
+
+
+def baseline_csr(pattern: OraclePattern, batch: BatchArrays, mode=MODE_PROCESSOR, threads=1):
+    """The baseline run keeping every match: dict of numpy arrays in cep_collect's layout and order
+    (key order of the grouped batch, per key in emission order)."""
+    import numpy as np
+    L = lib()
+    h = L.orc_baseline_csr(pattern.h, C.byref(batch.s), mode, threads)
+    try:
+        nm, ne, err = C.c_int64(), C.c_int64(), C.c_int()
+        L.orc_csr_sizes(h, C.byref(nm), C.byref(ne), C.byref(err))
+        if err.value:
+            raise OracleError(err.value, "baseline failed")
+        out = dict(match_record=np.zeros(nm.value, np.int64), match_key=np.zeros(nm.value, np.int32),
+                   ent_off=np.zeros(nm.value + 1, np.int64), ent_name=np.zeros(ne.value, np.int32),
+                   ent_record=np.zeros(ne.value, np.int64))
+        L.orc_csr_copy(h, *[out[k].ctypes.data for k in ("match_record", "match_key", "ent_off", "ent_name",
+                                                           "ent_record")])
+        return out
+    finally:
+        L.orc_csr_free(h)
 
 
 def dewey_compatible(a, b):

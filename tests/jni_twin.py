@@ -24,7 +24,7 @@ PFX = "Java_com_github_fhuss_kafka_streams_cep_processor_GpuCEPProcessor_"
 NATIVES = ["cepCompile", "cepStageNames", "cepSessionOpen", "cepSessionPath", "cepPushBatch", "cepCollect",
            "cepBatchErrors", "cepStreamPosition", "cepStateExport", "cepStateImport", "cepStateEvict",
            "cepStateImportKeys", "cepStatePositions", "cepSetMaxKeyWords", "cepSessionClose", "cepPatternFree",
-           "cepLastError"]
+           "cepLastError", "cepStateToReference"]
 
 CEP_MODE_PROCESSOR, CEP_SESSION_CARRY, CEP_E_RUN_CAPACITY = 1, 1, 9
 CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS, CEP_BATCH_OFFSETS_MONOTONE, CEP_BATCH_DELIVER = 1, 3, 4, 1, 2
@@ -69,6 +69,7 @@ class JniLib:
             "cepSessionClose": (None, [C.c_int64]),
             "cepPatternFree": (None, [C.c_int64]),
             "cepLastError": (P, []),
+            "cepStateToReference": (P, [C.c_int64, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, PFX + name)
@@ -158,6 +159,11 @@ class JniLib:
 
     def cepPatternFree(self, pattern):
         self._cepPatternFree(self.env, None, pattern)
+
+    def cepStateToReference(self, pattern, blob: bytes):
+        a = self.to_np(self._cepStateToReference(self.env, None, pattern, self.arr(np.frombuffer(blob, np.int8))),
+                       np.int8)
+        return None if a is None else a.tobytes()
 
     def cepLastError(self) -> str:
         return self.string(self._cepLastError(self.env, None))

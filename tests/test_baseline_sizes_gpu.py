@@ -5,6 +5,7 @@ hash them identically).  C2: 1 M keys x 100 M events; C3: 100 k stock keys x 100
 12 (skip-till-any run explosion); C5: 1.25 M keys x 100 (one GPU's share of the node-wide 10 M)."""
 import os
 
+import numpy as np
 import pytest
 import torch
 
@@ -44,3 +45,29 @@ def test_full_size_checksum(name):
     b = O.BatchArrays(hk, [hv], [1], offset=ht if name == "c2" else None, ts=ht)
     om, ocs = O.baseline(O.OraclePattern(ir), b, O.MODE_PROCESSOR, min(THREADS, os.cpu_count() or 1))
     assert gm == om and gcs == ocs and gm > 0
+
+
+@pytest.mark.parametrize("name", ["c2", "c5"])
+def test_full_size_ordered_csr(name):
+    """Element by element, not only the order-independent checksum: every match's emitting record, key
+    and traversal (stage name, record), in the CSR's order -- key order of the grouped batch, per key
+    the reference's emission order (CEPProcessor.java:148, SharedVersionedBufferStoreImpl.peek) -- at
+    the full C2 / C5 sizes, against the oracle's run of the same records."""
+    key, val, ts, pat, path = _cfg(name)
+    n = key.numel()
+    ir = pat.to_ir(I32)
+    s = N.Session(N.CompiledPattern(ir), n, mode=N.MODE_PROCESSOR)
+    assert s.path == path
+    st = torch.cuda.current_stream()
+    s.push(n, key.data_ptr(), [val.data_ptr()], mem=N.MEM_DEVICE, stream=st.cuda_stream,
+           ts=ts.data_ptr() if name != "c2" else None)
+    got = s.collect()
+    hk, hv, ht = key.cpu().numpy(), val.cpu().numpy(), ts.cpu().numpy()
+    del key, val, ts
+    b = O.BatchArrays(hk, [hv], [1], offset=ht if name == "c2" else None, ts=ht)
+    want = O.baseline_csr(O.OraclePattern(ir), b, O.MODE_PROCESSOR, min(THREADS, os.cpu_count() or 1))
+    assert len(want["match_record"]) > 1_000_000
+    for f in ("match_record", "match_key", "ent_off", "ent_name", "ent_record"):
+        assert got[f].shape == want[f].shape, f
+        bad = np.flatnonzero(got[f] != want[f])
+        assert len(bad) == 0, (f, bad[:5], got[f][bad[:5]], want[f][bad[:5]])
