@@ -4,9 +4,13 @@ cep_push_batch + cep_collect), with the host-side time of the push call and of t
 split, for pinned and for pageable (plain numpy) host input.
 
 Usage: flush_probe.py [per=65536] [batches=200]
+The "C loop" lines run the same loop in C (tools/flush_loop.c, built here with gcc): the C-ABI's own
+cost per flush, without Python in the loop, as the JNI shim sees it.
 Run under `rocprofv3 --kernel-trace --memory-copy-trace --marker-trace --stats` with KCEP_ROCTX=1
 for the device-side split."""
+import ctypes as C
 import os
+import subprocess
 import sys
 import time
 
@@ -65,3 +69,30 @@ for label, kp, vp in (("pinned", pk.data_ptr(), pv.data_ptr()), ("pageable", hk.
     print(f"{label:9s} per={per} batches={nb}: {dt / nb * 1e6:8.1f} us/batch  push {tp / nb * 1e6:7.1f}  "
           f"collect {tc / nb * 1e6:7.1f}  {n / dt:.3e} events/s  matches {tot} (same: {tot == want})", flush=True)
     s.close()
+
+
+so = os.path.join("/tmp", "libflush_loop_%d.so" % os.getpid())
+subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools", "flush_loop.c"),
+                "-I", os.path.join(ROOT, "include"), "-L", os.path.dirname(N.LIB_PATH), "-l:libkcep.so",
+                "-Wl,-rpath," + os.path.dirname(N.LIB_PATH)], check=True)
+fl = C.CDLL(so)
+fl.flush_loop.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                          C.POINTER(C.c_double)]
+for label, kp, vp in (("pinned", pk.data_ptr(), pv.data_ptr()), ("pageable", hk.ctypes.data, hv.ctypes.data)):
+    s = N.Session(pat, per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K)
+    s.set_timing(False)
+    best = None
+    for _ in range(4):
+        s.state_clear()
+        torch.cuda.synchronize()
+        o = (C.c_double * 4)()
+        rc = fl.flush_loop(s.h, nb, per, kp, vp, N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER, st.cuda_stream, o)
+        assert rc == 0, rc
+        if best is None or o[0] < best[0]:
+            best = list(o)
+    dt, tp, tc, tot = best
+    print(f"C loop {label:9s} per={per} batches={nb}: {dt / nb:8.1f} us/batch  push {tp / nb:7.1f}  "
+          f"collect {tc / nb:7.1f}  {n / (dt * 1e-6):.3e} events/s  matches {int(tot)} (same: {int(tot) == want})",
+          flush=True)
+    s.close()
+os.unlink(so)
