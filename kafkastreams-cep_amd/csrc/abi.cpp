@@ -60,9 +60,10 @@ hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hi
 hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, const int64_t* ent_off,
                               int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st);
-hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
-                               unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
-                               int64_t* scan_tmp, unsigned long long* max_span, hipStream_t st);
+hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64_t n, int32_t chunk, int64_t* pre,
+                               unsigned long long* out, int64_t* tot_cnt, int64_t* tot_len, int64_t* scan_tmp,
+                               hipStream_t st);
+int64_t runs_sim_waves(int64_t n, int32_t chunk);
 hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, hipStream_t st);
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
                      size_t* tmp_bytes, hipStream_t st);
@@ -291,18 +292,18 @@ bool host_pinned(const void* p) {
 int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_copy = false) {
   size_t total = 0;
   std::vector<size_t> at(size_t(na), 0);
-  bool pinned = true;
   for (int i = 0; i < na; i++) {
     if (!arrs[i].src || !arrs[i].bytes) continue;
     at[size_t(i)] = total;
     total += (arrs[i].bytes + 255) & ~size_t(255);
-    pinned = pinned && host_pinned(arrs[i].src);
   }
   if (!total) return CEP_OK;
   // zero copy (the stencil path's one streaming pass, small batches): the kernel reads the pinned ring
-  // over the link itself, no copy into HBM first (KCEP_ZERO_COPY=0 turns it off for A/B)
+  // over the link itself, no copy into HBM first (KCEP_ZERO_COPY=0 turns it off for A/B).  Pinned
+  // caller memory takes it too: one host memcpy beats waiting for a DMA before the call may return
+  // (r04 flush probe, 64 k records: 55.8 us per flush pageable through the ring, 67-69 us pinned by DMA)
   static const bool zc_env = [] { const char* e = getenv("KCEP_ZERO_COPY"); return !(e && e[0] == '0'); }();
-  if (zero_copy && zc_env && !pinned && total <= kRingChunk) {
+  if (zero_copy && zc_env && total <= kRingChunk) {
     const int j = s->ring_next;
     s->ring_next ^= 1;
     if (s->ring_ev[j]) HIPCHECK(hipEventSynchronize(s->ring_ev[j]));
@@ -325,6 +326,9 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
     s->zc_slot = j;                                   // its event is recorded behind the kernels that read it
     return CEP_OK;
   }
+  bool pinned = true;
+  for (int i = 0; i < na && pinned; i++)
+    if (arrs[i].src && arrs[i].bytes) pinned = host_pinned(arrs[i].src);
   if (s->dstage.ensure(total)) return fail(CEP_E_HIP, "staging allocation failed");
   uint8_t* dev = s->dstage.as<uint8_t>();
   for (int i = 0; i < na; i++)
@@ -599,8 +603,9 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   }
   if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
       s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 4) * 8) ||
-      s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->r_endof.ensure(size_t(n) * 4) ||
-      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) || s->r_blk.ensure(size_t(n / 256 + 2) * 16) ||
+      s->flag.ensure(size_t(2 * runs_sim_waves(n, runs_chunk(n)) + 8) * 8) ||
+      s->idx.ensure(size_t(2 * runs_sim_waves(n, runs_chunk(n)) + 8) * 8) || s->r_endof.ensure(size_t(n) * 4) ||
+      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) ||
       s->r_errlist.ensure(size_t(std::min<int64_t>(n, kRunsErrCap)) * 24))
     return fail(CEP_E_HIP, "allocation failed");
   RunsArgs A{};
@@ -623,6 +628,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.err_list = s->r_errlist.as<unsigned long long>();
   A.err_n = ctl + 5;
   A.err_cap = std::min<int64_t>(n, kRunsErrCap);
+  A.max_span = ctl + 4;
   // matches, first exception, entries, segment overflow, longest span, failing runs
   const unsigned long long init[6] = {0, ~0ull, 0, 0, 0, 0};
   HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
@@ -630,11 +636,9 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                            s->jit ? s->jit->runs_sim : nullptr));
   HIPCHECK(hipEventRecord(s->ev1, st));
   int64_t* scal0 = s->scal.as<int64_t>();
-  HIPCHECK(exclusive_scan(s->flag.as<int64_t>(), n, s->idx.as<int64_t>(), scal0 + 3, s->scan_tmp.as<int64_t>(), st));
-  const int64_t nblk = n / 256 + 2;
-  HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->r_endof.as<int32_t>(), n,
-                               s->rk.as<unsigned long long>(), s->r_blk.as<int64_t>(), s->r_blk.as<int64_t>() + nblk,
-                               reinterpret_cast<int64_t*>(ctl + 2), s->scan_tmp.as<int64_t>(), ctl + 4, st));
+  HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), n, A.chunk, s->idx.as<int64_t>(),
+                               s->rk.as<unsigned long long>(), scal0 + 3, reinterpret_cast<int64_t*>(ctl + 2),
+                               s->scan_tmp.as<int64_t>(), st));
   if (rcarry) {                                    // the keys' new tails: from their oldest still-open start
     if (s->rc_c.ensure(size_t(nb + 2) * 8) || s->rc_d.ensure(size_t(nb + 2) * 8))
       return fail(CEP_E_HIP, "allocation failed");
@@ -709,19 +713,20 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     HIPCHECK(runs_sort(s->rk.as<unsigned long long>(), s->rk_sorted.as<unsigned long long>(), nm, bits, s->rk_tmp.p,
                        &tmp_bytes, st));
   int64_t* scal = s->scal.as<int64_t>();
+  // the entry offsets are scanned straight into the output's ent_off (runs_expand reads them there)
   HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
-                             s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
+                             s->o_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
                              nullptr, nullptr, nullptr, st, true,
                              s->jit ? s->jit->runs_write : nullptr));
   if (!res[3] && !getenv_flag("KCEP_RUNS_REWALK")) {
     // the traversals from the stage segments runs_sim recorded
-    HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_entoff.as<int64_t>(), ne,
+    HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->o_entoff.as<int64_t>(), ne,
                                 s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
                                 s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
   } else {                                         // a run beyond RUNS_MAX_SEGS segments: walk every run again
     A.segs = nullptr;
     HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
-                               s->r_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), s->o_record.as<int64_t>(),
+                               s->o_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), s->o_record.as<int64_t>(),
                                s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
                                s->o_entrec.as<int64_t>(), st, false,
                                s->jit ? s->jit->runs_write : nullptr));

@@ -623,6 +623,12 @@ struct CodeGen {
     const int off = eop == OP_ADD ? 0 : eop == OP_SUB ? 1 : eop == OP_MUL ? 2 : eop == OP_DIV ? 3 : eop == OP_REM ? 4 : 5;
     op(uint8_t(base[k] + off));
   }
+  // x itself when it is an int, or the int under a cast of an int to double; else null
+  static ExprP int32_operand(const ExprP& x) {
+    if (x->t == T_I32) return x;
+    if (x->op == OP_CAST && x->ct == T_F64 && x->a && x->a->t == T_I32) return x->a;
+    return nullptr;
+  }
   void gen(const ExprP& e) {
     if (!ok) return;
     switch (e->op) {
@@ -670,8 +676,16 @@ struct CodeGen {
           break;
         }
         const uint8_t t = std::max(e->a->t, e->b->t);
-        gen(e->a); cvt(e->a->t, t); gen(e->b); cvt(e->b->t, t);
         const int off = e->op - OP_EQ;
+        // two int values compared as doubles (e.g. `(sum / count).asDouble() >= value`): every int fits a
+        // double exactly, so the int comparison gives the same answer without the two conversions
+        const ExprP ia = int32_operand(e->a), ib = int32_operand(e->b);
+        if (t == T_F64 && ia && ib) {
+          gen(ia); gen(ib);
+          op(uint8_t(BC_EQ_I + off));
+          break;
+        }
+        gen(e->a); cvt(e->a->t, t); gen(e->b); cvt(e->b->t, t);
         op(uint8_t((t == T_F64 ? BC_EQ_F : BC_EQ_I) + off));
         break;
       }

@@ -190,6 +190,7 @@ struct RunsArgs {
   const int64_t* pos;
   int64_t emit_from;
   int32_t chunk;                  // items per wave (a power of two <= RUNS_CHUNK; runs_chunk)
+  unsigned long long* max_span;   // runs_sim: the longest completed run's span (end - start), atomicMax
 };
 constexpr int RUNS_MAX_SEGS = 8;
 constexpr int RUNS_CHUNK = 1024;

@@ -41,33 +41,66 @@ __global__ __launch_bounds__(RT) void runs_sim(RunsArgs A, int64_t* __restrict__
 
 __global__ __launch_bounds__(RT) void runs_write(WriteArgs W) { runs_write_body(InterpTab{W.R.P}, W); }
 
-// completed runs in start order: key (end << 31 | start); each workgroup's total of their lengths
-// (entries of the CSR) into blk_len[blockIdx] (summed by a scan: no contended atomic)
-// (and the longest run's span e - s, atomicMax into *max_span: it bounds runs_order's window)
-__global__ __launch_bounds__(256) void runs_compact(const int64_t* __restrict__ flag, const int64_t* __restrict__ pos,
-                                                    const int32_t* __restrict__ end_of, int64_t n,
-                                                    unsigned long long* __restrict__ out, int64_t* __restrict__ blk_len,
-                                                    unsigned long long* __restrict__ max_span) {
-  __shared__ int64_t s_w[4], s_m[4];
-  const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  int64_t len = 0;
-  if (j < n && flag[j]) {
-    out[pos[j]] = (unsigned long long)(int64_t(end_of[j]) << 31 | j);
-    len = int64_t(end_of[j]) - j + 1;
+// completed runs in start order, key (end << 31 | start): one workgroup per runs_sim chunk, placed at
+// the exclusive scan of the chunks' counts (pre), each thread's items contiguous so that a block scan
+// of the per-thread counts ranks them
+__global__ __launch_bounds__(256) void runs_compact(const int32_t* __restrict__ end_of, int64_t n, int chunk,
+                                                    const int64_t* __restrict__ pre, unsigned long long* __restrict__ out) {
+  __shared__ int32_t s_w[4];
+  const int ipt = chunk > 256 ? chunk >> 8 : 1;
+  const int64_t c0 = int64_t(blockIdx.x) * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+  const int64_t a = c0 + int64_t(threadIdx.x) * ipt;
+  int32_t e[4];
+  int cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    e[q] = -1;
+    if (q < ipt && a + q < c1) e[q] = end_of[a + q];
+    cnt += e[q] >= 0;
   }
-  int64_t mx = len;
-  for (int d = 32; d >= 1; d >>= 1) {
-    len += __shfl_xor(len, d, 64);
-    const int64_t y = __shfl_xor(mx, d, 64);
-    mx = y > mx ? y : mx;
+  int inc = cnt;                                    // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(inc, d, 64);
+    if ((threadIdx.x & 63) >= d) inc += y;
   }
-  if ((threadIdx.x & 63) == 0) { s_w[threadIdx.x >> 6] = len; s_m[threadIdx.x >> 6] = mx; }
+  if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    blk_len[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    const int64_t m = std::max(std::max(s_m[0], s_m[1]), std::max(s_m[2], s_m[3]));
-    if (m > 0) atomicMax(max_span, (unsigned long long)(m - 1));
+  int64_t at = pre[blockIdx.x] + inc - cnt;
+  for (int w = 0; w < int(threadIdx.x >> 6); w++) at += s_w[w];
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+    if (e[q] >= 0) out[at++] = (unsigned long long)(int64_t(e[q]) << 31 | (a + q));
+}
+
+// exclusive scans of the chunks' run counts and lengths (stat[w], stat[W + w]) in one workgroup:
+// pre[w], pre[W + w]; the totals into *tot_cnt / *tot_len
+__global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restrict__ stat, int64_t nw, int64_t W,
+                                                        int64_t* __restrict__ pre, int64_t* __restrict__ tot_cnt,
+                                                        int64_t* __restrict__ tot_len) {
+  __shared__ int64_t s_c[16], s_l[16];
+  __shared__ int64_t s_carry[2];
+  if (threadIdx.x == 0) { s_carry[0] = 0; s_carry[1] = 0; }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t b = 0; b < nw; b += 1024) {
+    const int64_t w = b + threadIdx.x;
+    const int64_t c = w < nw ? stat[w] : 0, l = w < nw ? stat[W + w] : 0;
+    int64_t ic = c, il = l;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t yc = __shfl_up(ic, d, 64), yl = __shfl_up(il, d, 64);
+      if (lane >= d) { ic += yc; il += yl; }
+    }
+    if (lane == 63) { s_c[wv] = ic; s_l[wv] = il; }
+    __syncthreads();
+    int64_t oc = s_carry[0], ol = s_carry[1];
+    for (int q = 0; q < wv; q++) { oc += s_c[q]; ol += s_l[q]; }
+    if (w < nw) { pre[w] = oc + ic - c; pre[W + w] = ol + il - l; }
+    __syncthreads();
+    if (threadIdx.x == 1023) { s_carry[0] = oc + ic; s_carry[1] = ol + il; }
+    __syncthreads();
   }
+  if (threadIdx.x == 0) { *tot_cnt = s_carry[0]; *tot_len = s_carry[1]; }
 }
 
 // Completed runs from start order into (completing record, start) order without a device-wide sort.
@@ -76,23 +109,55 @@ __global__ __launch_bounds__(256) void runs_compact(const int64_t* __restrict__ 
 // overlaps run i, so with every run's span e - s <= W: j < i has s_j >= s_i - W, j > i has s_j < e_i <=
 // s_i + W, and (distinct starts) |i - j| <= W.  A workgroup ranks 256 runs against the window of runs
 // [first - W, last + W] staged in LDS (W <= RUNS_ORDER_MAX_W; wider batches take the radix sort).
+static_assert(RUNS_MAX_SEGS == 8, "runs_expand loads a run's segments as two uint4");
 constexpr int RUNS_ORDER_MAX_W = 1024;
+constexpr int RUNS_ORDER_WIN = 256 + 2 * RUNS_ORDER_MAX_W;
+// The backward count stops early: s_pm[x] = the latest end among the window's runs up to x, so once
+// s_pm[j] <= e no run at or before j ends after run i (the scan over [i - W, i) took ~50 steps per
+// run on C3, where most runs are short and W is set by the longest).
 __global__ __launch_bounds__(256) void runs_order(const unsigned long long* __restrict__ in, int64_t nm, int w,
                                                   unsigned long long* __restrict__ out) {
-  __shared__ unsigned long long s_r[256 + 2 * RUNS_ORDER_MAX_W];
+  __shared__ unsigned long long s_r[RUNS_ORDER_WIN];
+  __shared__ int32_t s_pm[RUNS_ORDER_WIN];
+  __shared__ int32_t s_w[4];
   const int64_t b0 = int64_t(blockIdx.x) * 256;
   const int64_t lo = b0 - w > 0 ? b0 - w : 0, hi = b0 + 256 + w < nm ? b0 + 256 + w : nm;
-  for (int64_t x = lo + threadIdx.x; x < hi; x += 256) s_r[x - lo] = in[x];
+  const int L = int(hi - lo);
+  for (int x = threadIdx.x; x < L; x += 256) s_r[x] = in[lo + x];
+  __syncthreads();
+  {                                                // prefix max of the ends: per thread a contiguous run
+    const int per = (L + 255) >> 8, x0 = int(threadIdx.x) * per, x1 = x0 + per < L ? x0 + per : L;
+    int32_t m = -1;
+    for (int x = x0; x < x1; x++) {
+      const int32_t e = int32_t(s_r[x] >> 31);
+      m = e > m ? e : m;
+    }
+    int32_t inc = m;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t y = __shfl_up(inc, d, 64);
+      if ((threadIdx.x & 63) >= d) inc = y > inc ? y : inc;
+    }
+    if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = inc;
+    int32_t before = __shfl_up(inc, 1, 64);
+    if ((threadIdx.x & 63) == 0) before = -1;
+    __syncthreads();
+    for (int q = 0; q < int(threadIdx.x >> 6); q++) before = s_w[q] > before ? s_w[q] : before;
+    for (int x = x0; x < x1; x++) {
+      const int32_t e = int32_t(s_r[x] >> 31);
+      before = e > before ? e : before;
+      s_pm[x] = before;
+    }
+  }
   __syncthreads();
   const int64_t i = b0 + threadIdx.x;
   if (i >= nm) return;
   const unsigned long long me = s_r[i - lo];
-  const int64_t e = int64_t(me >> 31), st = int64_t(me & 0x7FFFFFFFull);
+  const int64_t e = int64_t(me >> 31);
   int64_t p = i;
   for (int64_t j = i - 1; j >= lo; j--) {        // earlier starts ending later
-    const unsigned long long r = s_r[j - lo];
-    if (int64_t(r & 0x7FFFFFFFull) < st - w) break;
-    p -= int64_t(r >> 31) > e;
+    if (s_pm[j - lo] <= e) break;
+    p -= int64_t(s_r[j - lo] >> 31) > e;
   }
   for (int64_t j = i + 1; j < hi; j++) {         // later starts ending earlier
     const unsigned long long r = s_r[j - lo];
@@ -112,7 +177,7 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
                                                    const unsigned long long* __restrict__ sorted, int64_t nm,
                                                    const int64_t* __restrict__ ent_off, int64_t ne, int64_t base,
                                                    int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
-                                                   int64_t* __restrict__ ent_off_out, int32_t* __restrict__ ent_name,
+                                                   int64_t* ent_off_out, int32_t* __restrict__ ent_name,
                                                    int64_t* __restrict__ ent_record) {
   __shared__ int64_t s_at[257];
   __shared__ int64_t s_j[256], s_e[256];
@@ -129,9 +194,13 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
     s_e[tid] = e;
     match_record[m] = pos ? pos[e] : base + e;
     match_key[m] = key[j];
-    ent_off_out[m] = at;
-#pragma unroll
-    for (int i = 0; i < RUNS_MAX_SEGS; i++) s_seg[tid][i] = segs[j * RUNS_MAX_SEGS + i];
+    if (ent_off_out != ent_off) ent_off_out[m] = at;
+    // the segments as two 16-B vectors, the second only when the first holds no terminator
+    const uint4* sv = reinterpret_cast<const uint4*>(segs + j * RUNS_MAX_SEGS);
+    const uint4 a = sv[0];
+    const uint4 b = a.w == ~0u ? make_uint4(~0u, ~0u, ~0u, ~0u) : sv[1];
+    s_seg[tid][0] = a.x; s_seg[tid][1] = a.y; s_seg[tid][2] = a.z; s_seg[tid][3] = a.w;
+    s_seg[tid][4] = b.x; s_seg[tid][5] = b.y; s_seg[tid][6] = b.z; s_seg[tid][7] = b.w;
   }
   if (tid == 0) s_at[cnt] = m0 + cnt < nm ? ent_off[m0 + cnt] : ne;
   __syncthreads();
@@ -319,16 +388,26 @@ hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hi
   return hipGetLastError();
 }
 
-// blk_len: (n + 255) / 256 partial sums, then their exclusive scan in blk_pre with the total in *ent_total
-hipError_t runs_compact_launch(const int64_t* flag, const int64_t* pos, const int32_t* end_of, int64_t n,
-                               unsigned long long* out, int64_t* blk_len, int64_t* blk_pre, int64_t* ent_total,
-                               int64_t* scan_tmp, unsigned long long* max_span, hipStream_t st) {
+// stat: runs_sim's per-chunk counts / lengths (W = the sim launch's waves); pre: 2 W entries of scratch;
+// the completed runs into out in start order, their count into *tot_cnt, their total length *tot_len
+hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64_t n, int32_t chunk, int64_t* pre,
+                               unsigned long long* out, int64_t* tot_cnt, int64_t* tot_len, int64_t* scan_tmp,
+                               hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const int64_t nb = (n + 255) / 256;
-  hipLaunchKernelGGL(runs_compact, dim3(unsigned(nb)), dim3(256), 0, st, flag, pos, end_of, n, out, blk_len, max_span);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? exclusive_scan(blk_len, nb, blk_pre, ent_total, scan_tmp, st) : e;
+  const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
+  if (chunk > RUNS_CHUNK || chunk < 64) return hipErrorInvalidValue;
+  if (nw <= (int64_t(1) << 16)) {
+    hipLaunchKernelGGL(runs_chunk_scan, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
+  } else {
+    hipError_t e = exclusive_scan(stat, nw, pre, tot_cnt, scan_tmp, st);
+    if (e == hipSuccess) e = exclusive_scan(stat + W, nw, pre + W, tot_len, scan_tmp, st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(runs_compact, dim3(unsigned(nw)), dim3(256), 0, st, end_of, n, chunk, pre, out);
+  return hipGetLastError();
 }
+
+int64_t runs_sim_waves(int64_t n, int32_t chunk) { return n <= 0 ? 0 : int64_t(runs_blocks(n, chunk)) * (RT / 64); }
 
 hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, hipStream_t st) {
   if (nm <= 0) return hipSuccess;

@@ -233,14 +233,17 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
   }
 }
 
-// end_of[j] = completing record of the run started at record j (flag[j] = 1), else flag 0
-// ... and, with A.segs, the run's consumed stages as segments (so runs_expand writes the traversal
-// without walking the run again).  Both are staged in LDS: a lane's segments while its run is open
-// (stored once, as two 16-B vectors, when the run completes -- and not at all when it dies), the
-// chunk's results until the wave has finished the chunk (then stored coalesced).  Stored as they
-// came, every segment word and every result was a partial-line write of its own.
+// end_of[j] = completing record of the run started at record j (-1 none, -2 open at the key's last
+// carried record), and per wave chunk w its completed runs and their total length, stat[w] and
+// stat[W + w] (W = the launch's waves: runs_compact places the chunk's runs at the scan of the
+// counts, so no per-record flag array and no device-wide scan over it); the longest completed span
+// into *A.max_span.  With A.segs, also the run's consumed stages as segments (so runs_expand writes
+// the traversal without walking the run again).  Both are staged in LDS: a lane's segments while its
+// run is open (stored once, as two 16-B vectors, when the run completes -- and not at all when it
+// dies), the chunk's results until the wave has finished the chunk (then stored coalesced).  Stored
+// as they came, every segment word and every result was a partial-line write of its own.
 template <class Tab>
-__device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, int64_t* __restrict__ flag,
+__device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, int64_t* __restrict__ stat,
                                               int32_t* __restrict__ end_of) {
   __shared__ __attribute__((aligned(16))) uint32_t s_seg[RT][RUNS_MAX_SEGS];
   __shared__ int32_t s_end[RT / 64][RUNS_CHUNK];
@@ -291,10 +294,33 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
         });
   }
   __syncthreads();                                              // (every wave reaches it)
+  int64_t cnt = 0, len = 0, span = 0;
   for (int64_t k = lane; k < i1 - i0; k += 64) {
     const int32_t e = s_end[wv][k];
-    flag[i0 + k] = e >= 0 ? 1 : 0;
     end_of[i0 + k] = e;                                         // (-2: open, carried)
+    if (e >= 0) {
+      const int64_t d = int64_t(e) - (i0 + k);
+      cnt++;
+      len += d + 1;
+      span = d > span ? d : span;
+    }
+  }
+  if (i0 >= A.n) return;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    cnt += __shfl_xor(cnt, d, 64);
+    len += __shfl_xor(len, d, 64);
+    const int64_t y = __shfl_xor(span, d, 64);
+    span = y > span ? y : span;
+  }
+  if (lane == 0) {
+    const int64_t W = int64_t(gridDim.x) * (RT / 64);
+    stat[wave] = cnt;
+    stat[W + wave] = len;
+    // the longest span: a plain read first, so that the chunks agreeing with it add no contended atomic
+    // (one atomicMax per 256 records on one word cost runs_compact ~400 us at 10 M records)
+    if (span > 0 && (unsigned long long)span > __hip_atomic_load(A.max_span, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(A.max_span, (unsigned long long)span);
   }
 }
 
