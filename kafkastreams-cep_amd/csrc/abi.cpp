@@ -64,7 +64,10 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
                                unsigned long long* out, int64_t* tot_cnt, int64_t* tot_len, int64_t* scan_tmp,
                                hipStream_t st);
 int64_t runs_sim_waves(int64_t n, int32_t chunk);
-hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, hipStream_t st);
+hipError_t runs_results_launch(const unsigned long long* ctl, const int64_t* nm, const int64_t* top, int64_t* h,
+                               hipStream_t st);
+hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, int64_t* len,
+                             hipStream_t st);
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
                      size_t* tmp_bytes, hipStream_t st);
 hipError_t runs_write_launch(const RunsArgs& R, const unsigned long long* sorted, int64_t nm, int64_t* len,
@@ -220,6 +223,7 @@ struct cep_session {
   DBuf rtab, rpool, rpool2, rtop, e_key, e_topic, e_part, e_seg, e_off, e_ts, e_pos, rc_a, rc_b, rc_c, rc_d, gc_len, gc_off;
   DBuf e_cols[16];
   int64_t rpool_cap = 0, rpool_used = 0;   // tail records (5 + ncols int64 words each)
+  int64_t* h_res = nullptr;                // runs path: the batch's counts, written by the device into pinned memory
   bool collected = false;                  // the CSR above is the last batch's: a second collect re-uses it
   cep_matches last{};
   std::vector<uint8_t> evict_buf;          // cep_state_evict's blobs
@@ -647,13 +651,16 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                               s->rc_d.as<int64_t>(), scal0 + 6, s->scan_tmp.as<int64_t>(), s->rtop.as<int64_t>(),
                               s->rpool.as<int64_t>(), s->rtab.as<int64_t>(), st));
   }
-  // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow
-  unsigned long long res[6];
-  int64_t top = 0;
-  HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipMemcpyAsync(&res[0], scal0 + 3, 8, hipMemcpyDeviceToHost, st));
-  if (rcarry) HIPCHECK(hipMemcpyAsync(&top, s->rtop.p, 8, hipMemcpyDeviceToHost, st));
+  // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow (one
+  // small kernel writes them into pinned host memory: no copy commands, which cost ~25 us of gaps)
+  if (!s->h_res) HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&s->h_res), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  int64_t* h_res_dev = nullptr;
+  HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_res_dev), s->h_res, 0));
+  HIPCHECK(runs_results_launch(ctl, scal0 + 3, rcarry ? s->rtop.as<int64_t>() : nullptr, h_res_dev, st));
   HIPCHECK(hipStreamSynchronize(st));
+  unsigned long long res[6];
+  for (int q = 0; q < 6; q++) res[q] = (unsigned long long)s->h_res[q];
+  const int64_t top = s->h_res[6];
   if (rcarry) {
     s->rpool_used = top;
     s->base += nb;
@@ -707,17 +714,22 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     return fail(CEP_E_HIP, "allocation failed");
   // (completing record, start) order: a windowed rank when every run spans <= 1024 records
   // (runs_order), else rocPRIM's radix sort over the completing record's bits
-  if (nm > 0 && res[4] <= 1024 && !getenv_flag("KCEP_RUNS_RADIX"))
-    HIPCHECK(runs_order_launch(s->rk.as<unsigned long long>(), nm, int(res[4]), s->rk_sorted.as<unsigned long long>(), st));
-  else if (nm > 0)
-    HIPCHECK(runs_sort(s->rk.as<unsigned long long>(), s->rk_sorted.as<unsigned long long>(), nm, bits, s->rk_tmp.p,
-                       &tmp_bytes, st));
   int64_t* scal = s->scal.as<int64_t>();
-  // the entry offsets are scanned straight into the output's ent_off (runs_expand reads them there)
-  HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
-                             s->o_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
-                             nullptr, nullptr, nullptr, st, true,
-                             s->jit ? s->jit->runs_write : nullptr));
+  // the entry offsets are scanned straight into the output's ent_off (runs_expand reads them there);
+  // runs_order writes the sorted runs' lengths itself
+  if (nm > 0 && res[4] <= 1024 && !getenv_flag("KCEP_RUNS_RADIX")) {
+    HIPCHECK(runs_order_launch(s->rk.as<unsigned long long>(), nm, int(res[4]), s->rk_sorted.as<unsigned long long>(),
+                               s->r_len.as<int64_t>(), st));
+    HIPCHECK(exclusive_scan(s->r_len.as<int64_t>(), nm, s->o_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), st));
+  } else {
+    if (nm > 0)
+      HIPCHECK(runs_sort(s->rk.as<unsigned long long>(), s->rk_sorted.as<unsigned long long>(), nm, bits, s->rk_tmp.p,
+                         &tmp_bytes, st));
+    HIPCHECK(runs_write_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->r_len.as<int64_t>(),
+                               s->o_entoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), nullptr, nullptr,
+                               nullptr, nullptr, nullptr, st, true,
+                               s->jit ? s->jit->runs_write : nullptr));
+  }
   if (!res[3] && !getenv_flag("KCEP_RUNS_REWALK")) {
     // the traversals from the stage segments runs_sim recorded
     HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->o_entoff.as<int64_t>(), ne,
@@ -1125,6 +1137,7 @@ void cep_session_close(cep_session* s) {
     if (s->ring[j]) (void)hipHostFree(s->ring[j]);
   }
   if (s->h2d_ev) (void)hipEventDestroy(s->h2d_ev);
+  if (s->h_res) (void)hipHostFree(s->h_res);
   if (s->dl) {
     (void)hipDeviceSynchronize();                   // a delivery may still be writing into it
     (void)hipHostFree(s->dl);

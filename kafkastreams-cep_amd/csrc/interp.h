@@ -46,22 +46,34 @@ __device__ __forceinline__ int bc_bin(int op, int64_t x, int64_t y, int64_t& z) 
     case BC_SUB_I32: z = bc_sx32(x - y); break;
     case BC_MUL_I32: z = bc_sx32(int64_t(uint64_t(x) * uint64_t(y))); break;
     // int operands are sign-extended 32-bit values: a 32-bit divide (the 64-bit one is a long
-    // software sequence); y == -1 is a negation (Integer.MIN_VALUE / -1 wraps, JLS 15.17.2)
-    case BC_DIV_I32: if (y == 0) return CEP_E_ARITHMETIC; z = y == -1 ? bc_sx32(0 - x) : int64_t(int32_t(x) / int32_t(y)); break;
-    case BC_REM_I32: if (y == 0) return CEP_E_ARITHMETIC; z = y == -1 ? 0 : int64_t(int32_t(x) % int32_t(y)); break;
+    // software sequence); y == -1 is a negation (Integer.MIN_VALUE / -1 wraps, JLS 15.17.2).  The
+    // divisor is made safe instead of branching around the divide, so a predicate's failure checks
+    // stay branch-free (jit.cpp)
+    case BC_DIV_I32: {
+      const int32_t yy = (y == 0 || y == -1) ? 1 : int32_t(y);
+      z = y == 0 ? 0 : y == -1 ? bc_sx32(0 - x) : int64_t(int32_t(x) / yy);
+      return y == 0 ? CEP_E_ARITHMETIC : 0;
+    }
+    case BC_REM_I32: {
+      const int32_t yy = (y == 0 || y == -1) ? 1 : int32_t(y);
+      z = (y == 0 || y == -1) ? 0 : int64_t(int32_t(x) % yy);
+      return y == 0 ? CEP_E_ARITHMETIC : 0;
+    }
     case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
     case BC_SUB_I64: z = int64_t(uint64_t(x) - uint64_t(y)); break;
     case BC_MUL_I64: z = int64_t(uint64_t(x) * uint64_t(y)); break;
     // long operands that fit 32 bits (the common case) take the 32-bit divide too
-    case BC_DIV_I64:
-      if (y == 0) return CEP_E_ARITHMETIC;
-      z = y == -1 ? int64_t(0ull - uint64_t(x))
-          : (bc_sx32(x) == x && bc_sx32(y) == y) ? int64_t(int32_t(x) / int32_t(y)) : x / y;
-      break;
-    case BC_REM_I64:
-      if (y == 0) return CEP_E_ARITHMETIC;
-      z = y == -1 ? 0 : (bc_sx32(x) == x && bc_sx32(y) == y) ? int64_t(int32_t(x) % int32_t(y)) : x % y;
-      break;
+    case BC_DIV_I64: {
+      const int64_t yy = (y == 0 || y == -1) ? 1 : y;
+      z = y == 0 ? 0 : y == -1 ? int64_t(0ull - uint64_t(x))
+          : (bc_sx32(x) == x && bc_sx32(yy) == yy) ? int64_t(int32_t(x) / int32_t(yy)) : x / yy;
+      return y == 0 ? CEP_E_ARITHMETIC : 0;
+    }
+    case BC_REM_I64: {
+      const int64_t yy = (y == 0 || y == -1) ? 1 : y;
+      z = (y == 0 || y == -1) ? 0 : (bc_sx32(x) == x && bc_sx32(yy) == yy) ? int64_t(int32_t(x) % int32_t(yy)) : x % yy;
+      return y == 0 ? CEP_E_ARITHMETIC : 0;
+    }
     case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;
     case BC_SUB_F64: z = bc_b(bc_f(x) - bc_f(y)); break;
     case BC_MUL_F64: z = bc_b(bc_f(x) * bc_f(y)); break;

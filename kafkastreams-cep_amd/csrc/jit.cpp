@@ -86,13 +86,20 @@ std::string program_table(const DevProgram& d) {
 std::string sv(int i) { return "s" + std::to_string(i); }
 
 // one predicate / fold body starting at pc0, as template <class Env> bool jf_<pc0>(Env&, int64_t&)
-bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
+// branchfree (the runs kernels, whose Env.state never fails): a body without sequence reads keeps its
+// first failure in a register and tests it once at the end, instead of a divergent branch per check
+// (state tag, Curr, division by zero) -- the ops after a failure compute discarded values and have no
+// side effects, so the result and the reported failure are the same; && / || jumps stay branches, so
+// what they skip never runs (Java's short circuit)
+bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why, bool branchfree) {
   auto word = [&](int pc) { return pc >= 0 && pc < NFA_MAX_CODE ? d.code[pc] : 0; };
   std::set<int> labels;
+  bool has_seq = false;
   for (int pc = pc0;;) {                        // pass 1: jump targets
     if (pc < 0 || pc >= NFA_MAX_CODE) { why = "code out of range"; return false; }
     const int op = word(pc) & 0xFF;
     pc++;
+    if (op == BC_SEQ_AVG || op == BC_SEQ_AGG) has_seq = true;
     if (op == BC_END) break;
     if (op == BC_PUSH) pc += 2;
     else if (op == BC_TOPIC_EQ || op == BC_SEQ_AGG) pc++;
@@ -101,6 +108,7 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
       pc++;
     }
   }
+  const bool bf = branchfree && !has_seq;      // (a jump stays a branch: the ops it skips never run)
   std::string b;
   char buf[256];
   int depth = 0, maxd = 0;
@@ -117,6 +125,7 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
     switch (op) {
       case BC_END:
         if (!need(1)) return false;
+        if (bf) b += "if (e) { env.fail(e); return false; }\n";
         b += "r = " + top + "; return true;\n";
         goto done;
       case BC_PUSH: {
@@ -137,6 +146,15 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
         pc++;
         break;
       case BC_STATE_GET:
+        if (bf) {
+          snprintf(buf, sizeof buf,
+                   "{ int32_t tg; int64_t v; env.state(%d, tg, v); "
+                   "e = e ? e : tg == 0 ? CEP_E_UNKNOWN_AGGREGATE : tg != %d ? CEP_E_CLASS_CAST : 0; %s = v; }\n",
+                   a, c, sv(depth).c_str());
+          b += buf;
+          depth++;
+          break;
+        }
         snprintf(buf, sizeof buf,
                  "{ int32_t tg; int64_t v; if (!env.state(%d, tg, v)) return false; "
                  "if (tg == 0) { env.fail(CEP_E_UNKNOWN_AGGREGATE); return false; } "
@@ -147,6 +165,15 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
         break;
       case BC_STATE_GET_OR_ELSE: {               // set: push and skip the default's code
         const int target = pc + 1 + word(pc);
+        if (bf) {
+          snprintf(buf, sizeof buf,
+                   "{ int32_t tg; int64_t v; env.state(%d, tg, v); if (tg != 0) { "
+                   "e = e ? e : tg != %d ? CEP_E_CLASS_CAST : 0; %s = v; goto L%d; } }\n",
+                   a, c, sv(depth).c_str(), target);
+          b += buf;
+          pc++;
+          break;
+        }
         snprintf(buf, sizeof buf,
                  "{ int32_t tg; int64_t v; if (!env.state(%d, tg, v)) return false; if (tg != 0) { "
                  "if (tg != %d) { env.fail(CEP_E_CLASS_CAST); return false; } %s = v; goto L%d; } }\n",
@@ -156,6 +183,15 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
         break;
       }
       case BC_FOLD_CURR:
+        if (bf) {
+          snprintf(buf, sizeof buf,
+                   "e = e ? e : (!env.in_fold || env.curr_tag == 0) ? CEP_E_NPE : env.curr_tag != %d ? CEP_E_CLASS_CAST : 0; "
+                   "%s = env.curr;\n",
+                   c, sv(depth).c_str());
+          b += buf;
+          depth++;
+          break;
+        }
         snprintf(buf, sizeof buf,
                  "if (!env.in_fold || env.curr_tag == 0) { env.fail(CEP_E_NPE); return false; } "
                  "if (env.curr_tag != %d) { env.fail(CEP_E_CLASS_CAST); return false; } %s = env.curr;\n",
@@ -196,8 +232,12 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
       default: {
         if (op < BC_ADD_I32 || op > BC_NE_B) { why = "unknown opcode " + std::to_string(op); return false; }
         if (!need(2)) return false;
-        snprintf(buf, sizeof buf, "{ int64_t z; const int e = bc_bin(%d, %s, %s, z); if (e) { env.fail(e); return false; } %s = z; }\n",
-                 op, sv(depth - 2).c_str(), sv(depth - 1).c_str(), sv(depth - 2).c_str());
+        if (bf)
+          snprintf(buf, sizeof buf, "{ int64_t z; const int ee = bc_bin(%d, %s, %s, z); e = e ? e : ee; %s = z; }\n",
+                   op, sv(depth - 2).c_str(), sv(depth - 1).c_str(), sv(depth - 2).c_str());
+        else
+          snprintf(buf, sizeof buf, "{ int64_t z; const int e = bc_bin(%d, %s, %s, z); if (e) { env.fail(e); return false; } %s = z; }\n",
+                   op, sv(depth - 2).c_str(), sv(depth - 1).c_str(), sv(depth - 2).c_str());
         b += buf;
         depth--;
       }
@@ -206,6 +246,7 @@ bool gen_entry(const DevProgram& d, int pc0, std::string& o, std::string& why) {
   }
 done:
   o += "template <class Env>\n__device__ __forceinline__ bool jf_" + std::to_string(pc0) + "(Env& env, int64_t& r) {\n";
+  if (bf) o += "  int e = 0;\n";
   if (maxd > 0) {
     o += "  int64_t ";
     for (int i = 0; i < maxd; i++) o += (i ? ", " : "") + sv(i) + " = 0";
@@ -216,7 +257,7 @@ done:
 }
 
 // the generated part shared by every kernel family: program table, predicates, JitTab
-bool gen_program(const Program& P, std::string& o, std::string& why) {
+bool gen_program(const Program& P, std::string& o, std::string& why, bool branchfree = false) {
   const DevProgram& d = P.dev;
   std::set<int> entries;
   for (int s = 0; s < d.nstages; s++) {
@@ -229,7 +270,7 @@ bool gen_program(const Program& P, std::string& o, std::string& why) {
   o += "namespace kcep {\n";
   o += "constexpr DevProgram kcep_prog = " + program_table(d) + ";\n";
   for (int pc : entries)
-    if (!gen_entry(d, pc, o, why)) return false;
+    if (!gen_entry(d, pc, o, why, branchfree)) return false;
   o += "template <class Env>\n__device__ __forceinline__ bool jit_eval(int pc, Env& env, int64_t& r) {\n  switch (pc) {\n";
   for (int pc : entries) o += "    case " + std::to_string(pc) + ": return jf_" + std::to_string(pc) + "(env, r);\n";
   o += "  }\n  env.fail(CEP_E_BAD_IR);\n  return false;\n}\n";
@@ -315,7 +356,7 @@ JitModule::~JitModule() {}
 
 std::string jit_source_runs(const Program& P, std::string& why) {
   std::string o = "#include \"interp.h\"\n";
-  if (!gen_program(P, o, why)) return "";
+  if (!gen_program(P, o, why, true)) return "";
   o += R"(#include "runs_dev.h"
 extern "C" __global__ __launch_bounds__(kcep::RT) void kcep_runs_sim(kcep::RunsArgs A, int64_t* __restrict__ flag,
                                                                      int32_t* __restrict__ end_of) {

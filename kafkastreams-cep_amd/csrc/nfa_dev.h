@@ -23,7 +23,14 @@ namespace kcep {
 
 
 constexpr int32_t EPS_NONE = 0xFF;
-constexpr int MAXD = NFA_MAX_FRAMES;          // PROCEED/SKIP_PROCEED recursion depth (checked by the compiler)
+// PROCEED/SKIP_PROCEED recursion depth (checked by the compiler).  The per-pattern kernels size the
+// suspended-frame stack (scratch memory) by the pattern's own depth (+1 spare): C4 88 B per lane
+// instead of 704
+#ifdef KCEP_JIT
+constexpr int MAXD = ::kcep::kcep_prog.maxdepth + 1 < NFA_MAX_FRAMES ? ::kcep::kcep_prog.maxdepth + 1 : NFA_MAX_FRAMES;
+#else
+constexpr int MAXD = NFA_MAX_FRAMES;
+#endif
 constexpr int NW = 4;                      // node words: refs, first pred, last pred, flags
 constexpr int32_t NF_EXISTS = 1, NF_MARK = 2, NF_NEED = 4;
 constexpr int PW = 6;                      // pred words: version, prev slot, prev event, next, |version|, version[0]

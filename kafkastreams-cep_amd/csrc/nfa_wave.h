@@ -31,11 +31,15 @@
 namespace kcep {
 
 constexpr int WAVE = 64;
+// LDS per key-wave: WAVE_ARENA words of workspace + 64 x WAVE_PRIV words of private run lists and
+// operation logs, sized together for 3 waves per SIMD.  C4 sweep (profiles/r04_c4_lds_sweep.log,
+// ms per step): arena 2048 + lists in the pool 8.43; 1024 + 16 7.78; 1024 + 12 8.02; 1024 + 20 8.23;
+// 1280 + 16 8.22; 768 + 16 9.75; 512 + 32 10.9; 4 waves per SIMD 11.2
 #ifndef WAVE_ARENA
-#define WAVE_ARENA 2048                    // LDS words per key workspace (KCEP_WAVE_ARENA A/B: 0 = pool only)
+#define WAVE_ARENA 1024                    // LDS words per key workspace (KCEP_WAVE_ARENA A/B: 0 = pool only)
 #endif
 #ifndef WAVE_PRIV
-#define WAVE_PRIV 0                        // LDS words per lane for its private run list + operation log
+#define WAVE_PRIV 16                       // LDS words per lane for its private run list + operation log
 #endif                                     // (KCEP_WAVE_PRIV A/B; 0 = in the pool)
 #ifndef GROUP_LANES
 #define GROUP_LANES 16                     // lanes per key of the grouped kernel (4 keys per wave)
@@ -496,9 +500,9 @@ __device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL
   l.slm = 0; l.sle = 0; l.flen = 0; l.tlen = 0;
   ws_to_lane(l, w);
   // private run lists and operation logs: written by every evaluation and read back by the commit
-  // and the queue placement.  In the pool by default (2 runs per lane, growing on demand): a slice of
-  // LDS per lane (WAVE_PRIV words) cut the kernel's HBM writes but cost occupancy, C4 9.39 vs 8.34 ms
-  // (profiles/r03_ab_s5.jsonl)
+  // and the queue placement.  A slice of LDS per lane (WAVE_PRIV words: 2 runs + 2 log entries, growing
+  // into the pool on demand).  Next to the full 2048-word arena it cost occupancy (C4 9.39 vs 8.34 ms,
+  // profiles/r03_ab_s5.jsonl); with the arena halved it is the faster build (7.78 vs 8.43 ms, r04)
   const int q0 = 2;
 #if WAVE_PRIV > 0
   constexpr int priv_stride = WAVE_PRIV, log0 = (WAVE_PRIV - 4 * q0) / WL;

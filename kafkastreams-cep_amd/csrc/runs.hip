@@ -112,59 +112,48 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
 static_assert(RUNS_MAX_SEGS == 8, "runs_expand loads a run's segments as two uint4");
 constexpr int RUNS_ORDER_MAX_W = 1024;
 constexpr int RUNS_ORDER_WIN = 256 + 2 * RUNS_ORDER_MAX_W;
-// The backward count stops early: s_pm[x] = the latest end among the window's runs up to x, so once
-// s_pm[j] <= e no run at or before j ends after run i (the scan over [i - W, i) took ~50 steps per
-// run on C3, where most runs are short and W is set by the longest).
+// The backward count skips whole groups of 16 window entries whose latest end is <= e: no run there
+// ends after run i.  Most runs are short (C3: mean span 5, p99 35, max 91), so only the few groups
+// holding a long run are scanned; a plain scan over [i - W, i) took ~100 steps per run (131 us at C3).
 __global__ __launch_bounds__(256) void runs_order(const unsigned long long* __restrict__ in, int64_t nm, int w,
-                                                  unsigned long long* __restrict__ out) {
+                                                  unsigned long long* __restrict__ out, int64_t* __restrict__ len) {
   __shared__ unsigned long long s_r[RUNS_ORDER_WIN];
-  __shared__ int32_t s_pm[RUNS_ORDER_WIN];
-  __shared__ int32_t s_w[4];
+  __shared__ int32_t s_gm[RUNS_ORDER_WIN / 16 + 1];
   const int64_t b0 = int64_t(blockIdx.x) * 256;
   const int64_t lo = b0 - w > 0 ? b0 - w : 0, hi = b0 + 256 + w < nm ? b0 + 256 + w : nm;
   const int L = int(hi - lo);
   for (int x = threadIdx.x; x < L; x += 256) s_r[x] = in[lo + x];
   __syncthreads();
-  {                                                // prefix max of the ends: per thread a contiguous run
-    const int per = (L + 255) >> 8, x0 = int(threadIdx.x) * per, x1 = x0 + per < L ? x0 + per : L;
+  for (int g = threadIdx.x; g < (L + 15) / 16; g += 256) {
     int32_t m = -1;
-    for (int x = x0; x < x1; x++) {
+    const int x1 = g * 16 + 16 < L ? g * 16 + 16 : L;
+    for (int x = g * 16; x < x1; x++) {
       const int32_t e = int32_t(s_r[x] >> 31);
       m = e > m ? e : m;
     }
-    int32_t inc = m;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t y = __shfl_up(inc, d, 64);
-      if ((threadIdx.x & 63) >= d) inc = y > inc ? y : inc;
-    }
-    if ((threadIdx.x & 63) == 63) s_w[threadIdx.x >> 6] = inc;
-    int32_t before = __shfl_up(inc, 1, 64);
-    if ((threadIdx.x & 63) == 0) before = -1;
-    __syncthreads();
-    for (int q = 0; q < int(threadIdx.x >> 6); q++) before = s_w[q] > before ? s_w[q] : before;
-    for (int x = x0; x < x1; x++) {
-      const int32_t e = int32_t(s_r[x] >> 31);
-      before = e > before ? e : before;
-      s_pm[x] = before;
-    }
+    s_gm[g] = m;
   }
   __syncthreads();
   const int64_t i = b0 + threadIdx.x;
   if (i >= nm) return;
-  const unsigned long long me = s_r[i - lo];
-  const int64_t e = int64_t(me >> 31);
+  const int il = int(i - lo);
+  const unsigned long long me = s_r[il];
+  const int32_t e = int32_t(me >> 31);
   int64_t p = i;
-  for (int64_t j = i - 1; j >= lo; j--) {        // earlier starts ending later
-    if (s_pm[j - lo] <= e) break;
-    p -= int64_t(s_r[j - lo] >> 31) > e;
+  int x = il - 1;                                  // earlier starts ending later
+  for (; x >= 0 && (x & 15) != 15; x--) p -= int32_t(s_r[x] >> 31) > e;
+  for (; x >= 0; x -= 16) {
+    if (s_gm[x >> 4] <= e) continue;
+#pragma unroll
+    for (int q = 0; q < 16; q++) p -= int32_t(s_r[x - q] >> 31) > e;
   }
-  for (int64_t j = i + 1; j < hi; j++) {         // later starts ending earlier
-    const unsigned long long r = s_r[j - lo];
-    if (int64_t(r & 0x7FFFFFFFull) >= e) break;
-    p += int64_t(r >> 31) < e;
+  for (int y = il + 1; y < L; y++) {               // later starts ending earlier
+    const unsigned long long r = s_r[y];
+    if (int64_t(r & 0x7FFFFFFFull) >= int64_t(e)) break;
+    p += int32_t(r >> 31) < e;
   }
   out[p] = me;
+  len[p] = int64_t(e) - int64_t(me & 0x7FFFFFFFull) + 1;     // its entries (runs_lengths, fused)
 }
 
 
@@ -407,12 +396,27 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
   return hipGetLastError();
 }
 
+// the host's view of a runs batch, into pinned host memory h: {completed runs, first exception, entries,
+// segment overflow, longest span, failing runs, tail pool top}
+__global__ void runs_results(const unsigned long long* __restrict__ ctl, const int64_t* __restrict__ nm,
+                             const int64_t* __restrict__ top, int64_t* __restrict__ h) {
+  const int t = threadIdx.x;
+  if (t < 7) h[t] = t == 0 ? *nm : t == 6 ? (top ? *top : 0) : int64_t(ctl[t]);
+}
+hipError_t runs_results_launch(const unsigned long long* ctl, const int64_t* nm, const int64_t* top, int64_t* h,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(runs_results, dim3(1), dim3(64), 0, st, ctl, nm, top, h);
+  return hipGetLastError();
+}
+
 int64_t runs_sim_waves(int64_t n, int32_t chunk) { return n <= 0 ? 0 : int64_t(runs_blocks(n, chunk)) * (RT / 64); }
 
-hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, hipStream_t st) {
+// len: each sorted run's entry count (what runs_lengths computes)
+hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, int64_t* len,
+                             hipStream_t st) {
   if (nm <= 0) return hipSuccess;
   if (w < 0 || w > RUNS_ORDER_MAX_W) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(runs_order, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, in, nm, w, out);
+  hipLaunchKernelGGL(runs_order, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, in, nm, w, out, len);
   return hipGetLastError();
 }
 
