@@ -102,7 +102,12 @@ typedef struct {
                                 patterns (with or without optional() stages) stay on the stencil / chain path,
                                 which carries only each key's last K-1 records; patterns of the
                                 deterministic-runs path stay on it and carry each key's records from its oldest
-                                still-open run on (the runs are simulated again over them).  Both then take
+                                still-open run on (the runs are simulated again over them; a run that stays open
+                                for R records therefore keeps R records of its key carried and re-simulated per
+                                batch -- bounded only by the 2^31 records of an extended batch, past which the push
+                                fails with CEP_E_RUN_CAPACITY; such patterns, e.g. an unbounded oneOrMore that keeps
+                                matching, are better carried on the general path: cep_opts.force_path =
+                                CEP_PATH_GENERAL).  Both then take
                                 batches without null records (valid) and with per-key increasing offsets
                                 (CEP_BATCH_OFFSETS_MONOTONE; the host applies the high-water-mark rule); every
                                 other pattern carries its full NFA state on the general path. */

@@ -110,10 +110,20 @@ struct Lane {
 
 // ---- pool ----
 // every allocation is a multiple of 16 bytes (queues are read as int4)
+// the wave kernel's per-key counters live in LDS (WaveShared): LDS atomics, not flat ones (a flat atomic
+// waits on both the vector-memory and the LDS counters)
+typedef int32_t __attribute__((address_space(3))) lds_i32;
+typedef unsigned long long __attribute__((address_space(3))) lds_u64;
+__device__ __forceinline__ int32_t lds_add(int32_t* p, int32_t v) {
+  return __hip_atomic_fetch_add((lds_i32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned long long lds_add(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_fetch_add((lds_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words) {
   const int64_t w = (words + 3) & ~int64_t(3);
   if (l.wpool) {                                   // wave mode: one counter for the key
-    const int64_t was = int64_t(atomicAdd(l.wpool, (unsigned long long)w));
+    const int64_t was = int64_t(lds_add(l.wpool, (unsigned long long)w));
     if (l.A->max_key_words > 0 && was + w > l.A->max_key_words) { l.overflow = 1; l.cap_hit = 1; return nullptr; }
   } else if (l.A->max_key_words > 0 && l.pool_words + w > l.A->max_key_words) {
     l.overflow = 1; l.cap_hit = 1; return nullptr;
@@ -155,7 +165,7 @@ __device__ __forceinline__ bool is_fwd_final(const Lane& l, int sid, int eps) { 
 // ---- heap: versions and predecessor pointers ----
 __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
   if (l.wave) {                                    // versions are immutable: any allocation order will do
-    const int at = atomicAdd(l.wtop, words);
+    const int at = lds_add(l.wtop, words);
     if (at + words > l.heapcap) { l.wgrow = 1; l.overflow = 1; return -1; }
     return at;
   }
@@ -165,12 +175,22 @@ __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
   l.heap_top += words;
   return at;
 }
+// a version's digits copied to a fresh allocation: 4 loads issued before their 4 stores (the compiler
+// cannot tell the two ranges apart, so a load-store-load chain would pay one memory latency per digit)
+__device__ __forceinline__ void dw_copy(int32_t* h, int dst, int src, int len) {
+  int i = 0;
+  for (; i + 4 <= len; i += 4) {
+    const int32_t a = h[src + i], b = h[src + i + 1], c = h[src + i + 2], d = h[src + i + 3];
+    h[dst + i] = a; h[dst + i + 1] = b; h[dst + i + 2] = c; h[dst + i + 3] = d;
+  }
+  for (; i < len; i++) h[dst + i] = h[src + i];
+}
 __device__ __forceinline__ int dw_add_stage_(Lane& l, int v) {            // DeweyVersion.addStage :95-97
   const int len = l.heap[v];
   const int n = heap_alloc(l, len + 2);
   if (n < 0) return -1;
   l.heap[n] = len + 1;
-  for (int i = 0; i < len; i++) l.heap[n + 1 + i] = l.heap[v + 1 + i];
+  dw_copy(l.heap, n + 1, v + 1, len);
   l.heap[n + 1 + len] = 0;
   return n;
 }
@@ -180,9 +200,10 @@ __device__ __forceinline__ int dw_add_run_(Lane& l, int v, int off) {     // Dew
   if (idx < 0 || idx >= len) { l.err = CEP_E_INDEX; return -1; }
   const int n = heap_alloc(l, len + 1);
   if (n < 0) return -1;
+  const int32_t bumped = int32_t(uint32_t(l.heap[v + 1 + idx]) + 1u);
   l.heap[n] = len;
-  for (int i = 0; i < len; i++) l.heap[n + 1 + i] = l.heap[v + 1 + i];
-  l.heap[n + 1 + idx] = int32_t(uint32_t(l.heap[n + 1 + idx]) + 1u);
+  dw_copy(l.heap, n + 1, v + 1, len);
+  l.heap[n + 1 + idx] = bumped;
   return n;
 }
 __device__ __forceinline__ int dw_add_stage(Lane& l, int v) {
