@@ -75,32 +75,38 @@ __global__ __launch_bounds__(256) void runs_compact(const int32_t* __restrict__ 
 
 // exclusive scans of the chunks' run counts and lengths (stat[w], stat[W + w]) in one workgroup:
 // pre[w], pre[W + w]; the totals into *tot_cnt / *tot_len
+// (each thread sums a contiguous run of chunks, one block scan of the thread sums, then the thread
+// writes its run's prefixes: one pass, two barriers)
 __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restrict__ stat, int64_t nw, int64_t W,
                                                         int64_t* __restrict__ pre, int64_t* __restrict__ tot_cnt,
                                                         int64_t* __restrict__ tot_len) {
   __shared__ int64_t s_c[16], s_l[16];
-  __shared__ int64_t s_carry[2];
-  if (threadIdx.x == 0) { s_carry[0] = 0; s_carry[1] = 0; }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int64_t b = 0; b < nw; b += 1024) {
-    const int64_t w = b + threadIdx.x;
-    const int64_t c = w < nw ? stat[w] : 0, l = w < nw ? stat[W + w] : 0;
-    int64_t ic = c, il = l;
+  const int64_t per = (nw + 1023) / 1024, w0 = int64_t(threadIdx.x) * per, w1 = w0 + per < nw ? w0 + per : nw;
+  int64_t c = 0, l = 0;
+  for (int64_t w = w0; w < w1; w++) { c += stat[w]; l += stat[W + w]; }
+  int64_t ic = c, il = l;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int64_t yc = __shfl_up(ic, d, 64), yl = __shfl_up(il, d, 64);
-      if (lane >= d) { ic += yc; il += yl; }
-    }
-    if (lane == 63) { s_c[wv] = ic; s_l[wv] = il; }
-    __syncthreads();
-    int64_t oc = s_carry[0], ol = s_carry[1];
-    for (int q = 0; q < wv; q++) { oc += s_c[q]; ol += s_l[q]; }
-    if (w < nw) { pre[w] = oc + ic - c; pre[W + w] = ol + il - l; }
-    __syncthreads();
-    if (threadIdx.x == 1023) { s_carry[0] = oc + ic; s_carry[1] = ol + il; }
-    __syncthreads();
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t yc = __shfl_up(ic, d, 64), yl = __shfl_up(il, d, 64);
+    if (lane >= d) { ic += yc; il += yl; }
   }
-  if (threadIdx.x == 0) { *tot_cnt = s_carry[0]; *tot_len = s_carry[1]; }
+  if (lane == 63) { s_c[wv] = ic; s_l[wv] = il; }
+  __syncthreads();
+  int64_t oc = ic - c, ol = il - l;
+  for (int q = 0; q < wv; q++) { oc += s_c[q]; ol += s_l[q]; }
+  for (int64_t w = w0; w < w1; w++) {
+    pre[w] = oc;
+    pre[W + w] = ol;
+    oc += stat[w];
+    ol += stat[W + w];
+  }
+  if (threadIdx.x == 1023) {
+    int64_t tc = 0, tl = 0;
+    for (int q = 0; q < 16; q++) { tc += s_c[q]; tl += s_l[q]; }
+    *tot_cnt = tc;
+    *tot_len = tl;
+  }
 }
 
 // Completed runs from start order into (completing record, start) order without a device-wide sort.

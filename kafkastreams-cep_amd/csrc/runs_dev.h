@@ -279,8 +279,8 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
             for (int q = seg_n; q < RUNS_MAX_SEGS; q++) myseg[q] = ~0u;   // terminator (and padding)
             uint4* d = reinterpret_cast<uint4*>(A.segs + i * RUNS_MAX_SEGS);
             const uint4* sp = reinterpret_cast<const uint4*>(myseg);
-#pragma unroll
-            for (int q = 0; q < RUNS_MAX_SEGS / 4; q++) d[q] = sp[q];
+            d[0] = sp[0];
+            if (seg_n >= 4) d[1] = sp[1];      // runs_expand reads the second vector only then (C3: never)
           }
         },
         [&](int64_t i, int64_t r, int stage) {
