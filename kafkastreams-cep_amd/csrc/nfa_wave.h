@@ -97,9 +97,17 @@ __device__ __forceinline__ void wave_sync() {
 
 }  // namespace kcep
 
+// Whole-wave keys first in the LDS mode (KCEP_WAVE_LDSM=1).  Off by default: on C4 about half the keys
+// outgrow the arena and pay for a wasted first attempt -- 8.95 vs 7.63 ms, and 9.7-10.5 ms with a
+// 1536-3072-word arena (profiles/r04_c4_ldsm_ab.log)
+#ifndef WAVE_LDSM
+#define WAVE_LDSM 0
+#endif
+
 // the LDS-pointer mode of the engine (nfa_dev.h): a key whose workspace fits the arena runs on ds
 // instructions; one that outgrows it is re-run in the generic mode above
 namespace kcep {
+#if WAVE_LDSM
 namespace ldsm {
 typedef lds_i32* kp_t;
 typedef const lds_i32* kcp_t;
@@ -112,16 +120,17 @@ typedef const i4v __attribute__((address_space(3)))* kcp4_t;
 #undef KCEP_NS
 #undef KCEP_LDSM
 }  // namespace ldsm
-
-#ifndef WAVE_LDSM
-#define WAVE_LDSM 1                        // whole-wave keys try the LDS mode first (KCEP_WAVE_LDSM=0: A/B)
 #endif
+
+
 
 // the key descriptor of either mode (one lives at a time)
 template <int GL>
 union WaveSharedU {
   WaveShared<GL> g;
+#if WAVE_LDSM
   ldsm::WaveShared<GL> l;
+#endif
 };
 
 // One whole-wave key: in the LDS mode while its workspace fits the arena, else (re-run from the
