@@ -283,6 +283,9 @@ struct HostArr {
   const void** dst;               // receives the device address (null src: left null)
 };
 constexpr size_t kRingChunk = size_t(8) << 20;
+// zero copy only pays for small batches: the kernel then reads the batch over the link itself, which
+// for an 8 MB batch (1 M records) cost 706 us per flush against ~280 us by DMA (r04 bench)
+constexpr size_t kZeroCopyMax = size_t(1) << 20;
 
 bool host_pinned(const void* p) {
   hipPointerAttribute_t a;
@@ -307,7 +310,7 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
   // caller memory takes it too: one host memcpy beats waiting for a DMA before the call may return
   // (r04 flush probe, 64 k records: 55.8 us per flush pageable through the ring, 67-69 us pinned by DMA)
   static const bool zc_env = [] { const char* e = getenv("KCEP_ZERO_COPY"); return !(e && e[0] == '0'); }();
-  if (zero_copy && zc_env && total <= kRingChunk) {
+  if (zero_copy && zc_env && total <= kZeroCopyMax) {
     const int j = s->ring_next;
     s->ring_next ^= 1;
     if (s->ring_ev[j]) HIPCHECK(hipEventSynchronize(s->ring_ev[j]));
