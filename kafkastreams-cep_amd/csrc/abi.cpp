@@ -350,8 +350,11 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
     return CEP_OK;
   }
   // pageable: through the pinned ring, in chunks so that the copy of one overlaps the filling of the next
-  static const size_t split = [] { const char* e = getenv("KCEP_RING_SPLIT"); return e ? size_t(atoi(e)) : size_t(1); }();
-  const size_t chunk = std::min(kRingChunk, std::max<size_t>(size_t(64) << 10, ((total / std::max<size_t>(split, 1)) + 4095) & ~size_t(4095)));
+  // (2 MB chunks: the copy of chunk i overlaps the filling of chunk i + 1; a smaller batch is one chunk.
+  // KCEP_RING_SPLIT=k: k equal chunks instead, A/B)
+  static const size_t split = [] { const char* e = getenv("KCEP_RING_SPLIT"); return e ? size_t(atoi(e)) : size_t(0); }();
+  const size_t chunk = split ? std::min(kRingChunk, std::max<size_t>(size_t(64) << 10, ((total / split) + 4095) & ~size_t(4095)))
+                             : std::min(total, size_t(2) << 20);
   for (size_t c0 = 0; c0 < total; c0 += chunk) {
     const size_t c1 = std::min(total, c0 + chunk);
     const int j = s->ring_next;
