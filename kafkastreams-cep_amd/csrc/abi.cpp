@@ -821,7 +821,10 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   // first-allocation words of every key (NfaCaps) plus the events carried into the batch
   const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base;
   const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 3 * D.nstates;
-  const int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
+  int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
+  // the grouped wave kernel re-runs a key that outgrew its group from scratch on a whole wave, and the
+  // bump pool cannot give back what the first attempt took: count such keys twice
+  if (s->wave && s->grouped) est *= 2;
   s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
   A.cap = cap;
   A.carry = s->carry ? 1 : 0;
