@@ -400,8 +400,6 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
     const int pw = atoi(penv);
     o += "#define WAVE_PRIV " + std::to_string(pw <= 0 ? 0 : std::min(64, std::max(12, (pw + 3) & ~3))) + "\n";
   }
-  // whole-wave keys first in the LDS-pointer mode (KCEP_WAVE_LDSM=0: generic pointers only, A/B)
-  if (const char* lenv = getenv("KCEP_WAVE_LDSM")) o += std::string("#define WAVE_LDSM ") + (atoi(lenv) ? "1" : "0") + "\n";
   const std::string agg = wave_stateful(P.dev) || P.has_seq ? "true" : "false";
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
        "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {

@@ -91,59 +91,662 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-#define KCEP_LDSM 0
-#include "nfa_wave_body.h"
-#undef KCEP_LDSM
-
-}  // namespace kcep
-
-// Whole-wave keys first in the LDS mode (KCEP_WAVE_LDSM=1).  Off by default: on C4 about half the keys
-// outgrow the arena and pay for a wasted first attempt -- 8.95 vs 7.63 ms, and 9.7-10.5 ms with a
-// 1536-3072-word arena (profiles/r04_c4_ldsm_ab.log)
-#ifndef WAVE_LDSM
-#define WAVE_LDSM 0
-#endif
-
-// the LDS-pointer mode of the engine (nfa_dev.h): a key whose workspace fits the arena runs on ds
-// instructions; one that outgrows it is re-run in the generic mode above
-namespace kcep {
-#if WAVE_LDSM
-namespace ldsm {
-typedef lds_i32* kp_t;
-typedef const lds_i32* kcp_t;
-typedef i4v __attribute__((address_space(3)))* kp4_t;
-typedef const i4v __attribute__((address_space(3)))* kcp4_t;
-#define KCEP_LDSM 1
-#define KCEP_NS kcep::ldsm
-#include "nfa_dev_body.h"
-#include "nfa_wave_body.h"
-#undef KCEP_NS
-#undef KCEP_LDSM
-}  // namespace ldsm
-#endif
-
-
-
-// the key descriptor of either mode (one lives at a time)
+// the key's shared workspace descriptor (LDS); lanes keep register copies in their Lane
 template <int GL>
-union WaveSharedU {
-  WaveShared<GL> g;
-#if WAVE_LDSM
-  ldsm::WaveShared<GL> l;
-#endif
+struct WaveShared {
+  int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm, *aggs;
+  int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs, seqcap;
+  int64_t nmatch;
+  unsigned long long pool_words;   // the key's pool words (every lane allocates for the key)
+  int32_t err, overflow, cap_hit;
+  int32_t* logp[GL];
+  int32_t logn[GL], errc[GL];
+  int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
+  int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
+  int32_t *arena, arena_used, arena_cap;   // the key's LDS arena, its bump pointer (re-allocations go there first), size
+  // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
+  int32_t ms_slot[GL], ms_e[GL], ms_pv[GL], ms_cnt[GL], ms_done[GL], ms_err[GL];
+  int32_t conf[2 * GL];            // stateful rounds: each lane's run sequence, whether it wrote it
 };
 
-// One whole-wave key: in the LDS mode while its workspace fits the arena, else (re-run from the
-// batch start of the key: nothing of the first attempt was committed) in the generic mode
-template <bool AGG>
-__device__ __forceinline__ int wave_key_any(const NfaArgs& A, int seg, const Grp<WAVE>& gp, WaveSharedU<WAVE>& w,
-                                            int32_t* s_arena, int arena_words, int32_t*& s_priv) {
-#if WAVE_LDSM
-  const int r = ldsm::wave_key<AGG, WAVE>(A, seg, gp, w.l, s_arena, arena_words, s_priv);
-  if (r != 2) return r;
+template <class W>
+__device__ __forceinline__ void ws_to_lane(Lane& l, const W& w) {
+  l.nodes = w.nodes; l.heap = w.heap; l.qa = w.qa; l.qb = w.qb; l.fq = w.fq; l.out = w.out; l.hwm = w.hwm;
+  l.aggs = w.aggs; l.seqcap = w.seqcap;
+  l.heapcap = w.heapcap; l.heap_top = w.heap_top; l.qa_cap = w.qa_cap; l.qb_cap = w.qb_cap; l.fq_cap = w.fq_cap;
+  l.qlen = w.qlen; l.outcap = w.outcap; l.out_top = w.out_top; l.nhwm = w.nhwm; l.runs = w.runs;
+  l.nmatch = w.nmatch; l.err = w.err; l.overflow = w.overflow; l.cap_hit = w.cap_hit;
+}
+template <class W>
+__device__ __forceinline__ void lane_to_ws(W& w, const Lane& l) {
+  w.nodes = l.nodes; w.heap = l.heap; w.qa = l.qa; w.qb = l.qb; w.fq = l.fq; w.out = l.out; w.hwm = l.hwm;
+  w.aggs = l.aggs; w.seqcap = l.seqcap;
+  w.heapcap = l.heapcap; w.heap_top = l.heap_top; w.qa_cap = l.qa_cap; w.qb_cap = l.qb_cap; w.fq_cap = l.fq_cap;
+  w.qlen = l.qlen; w.outcap = l.outcap; w.out_top = l.out_top; w.nhwm = l.nhwm; w.runs = l.runs;
+  w.nmatch = l.nmatch; w.err = l.err; w.overflow = l.overflow; w.cap_hit = l.cap_hit;
+}
+
+// A shared array of `cap` words (used up to `used`) re-allocated at >= need words: lane 0 draws it
+// from the pool, the group copies.  Returns the new array (nullptr: pool exhausted -> w.overflow).
+// lds_ok: the array may move into the key's LDS arena (not the match output, read after the kernel)
+template <int GL>
+__device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int32_t* a, int32_t& cap, int64_t used,
+                                                int64_t need, const Grp<GL>& g, bool lds_ok = true) {
+  int64_t nc = int64_t(cap) * 2;
+  if (nc < need) nc = need;
   wave_sync();
+  if (g.gl == 0) {
+    if (lds_ok && w.arena_used + nc <= w.arena_cap) {   // room left in the LDS arena
+      w.grown = w.arena + w.arena_used;
+      w.arena_used += int32_t((nc + 3) & ~int64_t(3));
+    } else {
+      w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc);
+    }
+    if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
+  }
+  wave_sync();
+  int32_t* na = w.grown;
+  if (!na) return nullptr;
+  for (int64_t i = g.gl; i < used; i += GL) na[i] = a[i];
+  cap = int32_t(nc);
+  wave_sync();
+  return na;
+}
+
+template <int GL>
+__device__ __forceinline__ bool wave_heap_reserve(Lane& l, WaveShared<GL>& w, int64_t need_top, const Grp<GL>& g) {
+  if (need_top <= w.heapcap) return true;
+  int32_t cap = w.heapcap;
+  int32_t* na = wave_regrow(l, w, w.heap, cap, w.heap_top, need_top, g);
+  if (!na) return false;
+  if (g.gl == 0) { w.heap = na; w.heapcap = cap; }
+  wave_sync();
+  return true;
+}
+
+// the round's buffer operations, none of which can see another's effect (see the header): branch
+// walks with atomic refcounts and the existence checks, then the current record's nodes.  Returns
+// the reference exception of the first failing operation in queue order (CEP_OK if none).
+template <int GL>
+__device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int r) {
+  const auto& P = KCEP_PROG(l);
+  const int ns = P.nslots;
+  // (1) existence of every 5-arg put's predecessor node; branch walks (refs++)
+  int my_err = 0;
+  for (int k = 0; k < l.log_n && !my_err; k++) {
+    const int32_t* o = l.log + k * WL;
+    const int kind = o[0] & 0xFF, sid = (o[0] >> 8) & 0xFF;
+    if (kind == WOP_PUT5) {
+      const int psid = (o[0] >> 16) & 0xFF;
+      if (!exists(node(l, slot_of(l, psid), o[2]))) my_err = CEP_E_ILLEGAL_STATE;
+    } else if (kind == WOP_BRANCH) {                        // branch (:132-142)
+      int slot = slot_of(l, sid), e = o[1], pv = o[3];
+      for (;;) {
+        int32_t* nd = node(l, slot, e);
+        if (!exists(nd)) { my_err = CEP_E_NPE; break; }
+        atomicAdd(nd, 1);
+        const int p = first_compatible(l, nd, pv, nullptr);
+        if (p < 0 || l.heap[p + 1] < 0) break;
+        pv = l.heap[p]; slot = l.heap[p + 1]; e = l.heap[p + 2];
+      }
+    }
+  }
+  const uint64_t em = g.ballot(my_err != 0);
+  if (em) return g.bcast(my_err, __builtin_ctzll(em));
+  // (2) the current record's nodes: the last 3-arg put of a node overwrites, later 5-arg puts append
+  int before = 0, total = 0;
+  before = g.excl_scan(l.log_n, total);
+  for (int s = g.gl; s < ns; s += GL) { w.lastp3[s] = -1; w.scnt[s] = 0; }
+  wave_sync();
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if ((o[0] & 0xFF) == WOP_PUT3) atomicMax(&w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)], before + k);
+  }
+  wave_sync();
+  auto survives = [&](const int32_t* o, int gi) {
+    const int kind = o[0] & 0xFF;
+    if (kind == WOP_BRANCH || kind == WOP_AGG) return false;
+    const int lp = w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)];
+    return kind == WOP_PUT3 ? gi == lp : gi > lp;
+  };
+  int npred = 0;
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if (survives(o, before + k)) { atomicAdd(&w.scnt[slot_of(l, (o[0] >> 8) & 0xFF)], 1); npred++; }
+  }
+  int all = 0;
+  g.excl_scan(npred, all);
+  wave_sync();
+  if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(PW) * all, g)) return CEP_OK;   // w.overflow
+  if (g.gl == 0) {
+    int top = w.heap_top;
+    for (int s = 0; s < ns; s++)
+      if (w.scnt[s]) { w.sblk[s] = top; top += PW * w.scnt[s]; }
+    w.heap_top = top;
+  }
+  wave_sync();
+  l.heap = w.heap;
+  l.heapcap = w.heapcap;
+  for (int s = 0; s < ns; s++) {                             // uniform loop over the record's slots
+    const int cnt = w.scnt[s];
+    if (!cnt) continue;
+    int mine = 0;
+    for (int k = 0; k < l.log_n; k++) {
+      const int32_t* o = l.log + k * WL;
+      if (survives(o, before + k) && slot_of(l, (o[0] >> 8) & 0xFF) == s) mine++;
+    }
+    int tot = 0;
+    const int ex = g.excl_scan(mine, tot);
+    int j = 0;
+    for (int k = 0; k < l.log_n; k++) {
+      const int32_t* o = l.log + k * WL;
+      if (!survives(o, before + k) || slot_of(l, (o[0] >> 8) & 0xFF) != s) continue;
+      const int idx = ex + j++;
+      const int p = w.sblk[s] + PW * idx;
+      const int ver = o[3];
+      const bool p3 = (o[0] & 0xFF) == WOP_PUT3;
+      l.heap[p] = ver;                                       // MatchedEvent.addPredecessor
+      l.heap[p + 1] = p3 ? -1 : slot_of(l, (o[0] >> 16) & 0xFF);
+      l.heap[p + 2] = p3 ? 0 : o[2];
+      l.heap[p + 3] = idx + 1 < cnt ? p + PW : -1;
+      l.heap[p + 4] = l.heap[ver];
+      l.heap[p + 5] = l.heap[ver + 1];
+    }
+    if (g.gl == 0) {
+      int32_t* nd = node(l, s, r);
+      const int last = w.sblk[s] + PW * (cnt - 1);
+      if (w.lastp3[s] >= 0 || !exists(nd)) {                 // overwritten by a 3-arg put, or created: refs 1
+        nd[0] = 1; nd[1] = w.sblk[s]; nd[2] = last; nd[3] = NF_EXISTS;
+      } else {                                               // made by an earlier round: appended to
+        if (nd[1] < 0) nd[1] = w.sblk[s];
+        else l.heap[nd[2] + 3] = w.sblk[s];
+        nd[2] = last;
+      }
+    }
+  }
+  return CEP_OK;
+}
+
+// matchConstruction (NFA.java:151-158) of the record's final runs, 64 walks at a time in final-run
+// order.  A walk (SharedVersionedBufferStoreImpl.remove -> peek :176-201) persists a change only at
+// a node whose refs are <= 1 (the decrement of a copy is written back only at 0, Q4); nodes with
+// refs >= 2 stay so for the whole construction and are read-only.  Walks step to strictly earlier
+// events, so the walks are advanced event by event from the latest one (the frontier): at a
+// read-only node each lane picks its predecessor in parallel; the walks standing at a changing node
+// are stepped by lane 0 in final-run order -- every walk that will ever reach that node is there,
+// since none is left above the frontier.  The result is the sequential construction's.
+template <int GL>
+__device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int flen) {
+  const auto& P = KCEP_PROG(l);
+  const int lane = g.gl;
+  const int64_t pos = l.A->base + l.g;
+  const int maxp = l.nev + 1;                                  // one node per event at most
+  for (int base = 0; base < flen; base += GL) {
+    const int nact = flen - base < GL ? flen - base : GL;
+    const bool act = lane < nact;
+    if (!wave_heap_reserve(l, w, int64_t(w.heap_top) + int64_t(GL) * 2 * maxp, g)) return false;
+    l.heap = w.heap;
+    l.heapcap = w.heapcap;
+    int32_t* paths = w.heap + w.heap_top;                      // scratch above the heap top
+    int32_t* path = paths + lane * 2 * maxp;
+    int slot = 0, e = -1, pv = 0, cnt = 0, my_err = 0;
+    bool done = !act;
+    if (act) {
+      const int4 y = reinterpret_cast<const int4*>(w.fq)[base + lane];
+      slot = slot_of(l, y.x & 0xFF); e = y.z; pv = y.y;
+      if (e < 0) my_err = CEP_E_NPE;
+    }
+    for (;;) {
+      const bool live = !done && !my_err;
+      const int fr = g.max_all(live ? e : -1);
+      if (fr < 0) break;
+      const bool at = live && e == fr;
+      bool mut = false;
+      if (at) {
+        int32_t* nd = node(l, slot, e);
+        if (!exists(nd)) my_err = CEP_E_NPE;
+        else mut = nd[0] <= 1;
+        if (!my_err && !mut) {                                 // read-only node: a parallel step
+          path[2 * cnt] = slot; path[2 * cnt + 1] = e; cnt++;
+          const int p = first_compatible(l, nd, pv, nullptr);
+          if (p < 0 || l.heap[p + 1] < 0) done = true;
+          else { pv = l.heap[p]; slot = l.heap[p + 1]; e = l.heap[p + 2]; }
+        }
+      }
+      const uint64_t mm = g.ballot(at && !my_err && mut);
+      if (mm) {                                                // changing nodes: lane 0, in walk order
+        w.ms_slot[lane] = slot; w.ms_e[lane] = e; w.ms_pv[lane] = pv; w.ms_cnt[lane] = cnt; w.ms_done[lane] = done;
+        w.ms_err[lane] = my_err;
+        wave_sync();
+        if (lane == 0) {
+          for (uint64_t m = mm; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            const int sj = w.ms_slot[j], ej = w.ms_e[j], c = w.ms_cnt[j];
+            int32_t* nd = node(l, sj, ej);
+            if (!exists(nd)) { w.ms_err[j] = CEP_E_NPE; continue; }
+            int32_t* pj = paths + j * 2 * maxp;
+            pj[2 * c] = sj; pj[2 * c + 1] = ej;
+            w.ms_cnt[j] = c + 1;
+            const bool single = nd[1] < 0 || l.heap[nd[1] + 3] < 0;
+            int pp = -1;
+            const int p = first_compatible(l, nd, w.ms_pv[j], &pp);
+            if (p >= 0) {                                      // refs_left == 0: removePredecessor + put
+              nd[0] = 0;
+              const int nx = l.heap[p + 3];
+              if (pp < 0) nd[1] = nx; else l.heap[pp + 3] = nx;
+              if (nd[2] == p) nd[2] = pp;
+              nd[3] |= NF_EXISTS;
+            } else if (single) {
+              nd[3] &= ~NF_EXISTS;                             // delete
+            }
+            if (p < 0 || l.heap[p + 1] < 0) w.ms_done[j] = 1;
+            else { w.ms_pv[j] = l.heap[p]; w.ms_slot[j] = l.heap[p + 1]; w.ms_e[j] = l.heap[p + 2]; }
+          }
+        }
+        wave_sync();
+        if ((mm >> lane) & 1) {
+          slot = w.ms_slot[lane]; e = w.ms_e[lane]; pv = w.ms_pv[lane]; cnt = w.ms_cnt[lane];
+          done = w.ms_done[lane]; my_err = w.ms_err[lane];
+        }
+      }
+    }
+    const uint64_t em = g.ballot(my_err != 0);
+    if (em) {                                                  // the reference throws at the first failing walk
+      const int code = g.bcast(my_err, __builtin_ctzll(em));
+      if (lane == 0) w.err = code;
+      wave_sync();
+      return true;
+    }
+    // the matches, in final-run order: [pos lo, pos hi, cnt, (name, pos lo, pos hi) x cnt]
+    int total = 0;
+    const int words = act ? 3 + 3 * cnt : 0;
+    const int off = g.excl_scan(words, total);
+    if (w.out_top + total > w.outcap) {
+      int32_t cap = w.outcap;
+      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, g, false);
+      if (!na) return false;
+      if (lane == 0) { w.out = na; w.outcap = cap; }
+      wave_sync();
+    }
+    if (act) {
+      int32_t* o = w.out + w.out_top + off;
+      o[0] = int32_t(uint32_t(uint64_t(pos)));
+      o[1] = int32_t(uint32_t(uint64_t(pos) >> 32));
+      o[2] = cnt;
+      for (int i = 0; i < cnt; i++) {
+        const int64_t q = ev_pos(l, path[2 * i + 1]);
+        o[3 + 3 * i] = P.slot_name[path[2 * i]];
+        o[4 + 3 * i] = int32_t(uint32_t(uint64_t(q)));
+        o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
+      }
+    }
+    wave_sync();
+    if (lane == 0) { w.out_top += total; w.nmatch += nact; }
+    wave_sync();
+  }
+  return true;
+}
+
+// Stateful patterns: the round's aggregate writes (WOP_AGG log entries; wave_agg bit 0) in queue
+// order.  Without a conflict (wave_round_conflict) no two lanes write one (sequence, state) -- a lane
+// writes its own run's sequence and sequences it created -- so every lane applies its own entries,
+// placeholders numbered as the run words are (rb).  The table first grows to the largest sequence.
+template <int GL>
+__device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int rb) {
+  const int ns = KCEP_PROG(l).nstates;
+  auto real = [&](int sq) { return sq < -1 ? rb + (-sq - 2) + 1 : sq; };
+  int need = -1;
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if ((o[0] & 0xFF) == WOP_AGG) { const int sq = real(o[1]); need = sq > need ? sq : need; }
+  }
+  need = g.max_all(need);
+  if (need < 0) return true;
+  if (need >= w.seqcap) {
+    int32_t capw = w.seqcap * ns * 3;
+    const int64_t used = int64_t(capw);
+    int32_t* na = wave_regrow(l, w, w.aggs, capw, used, (int64_t(need) + 1) * ns * 3, g);
+    if (!na) return false;
+    for (int64_t i = used + g.gl; i < capw; i += GL) na[i] = 0;       // the new rows: every state null
+    wave_sync();
+    if (g.gl == 0) { w.aggs = na; w.seqcap = capw / (ns * 3); }
+    wave_sync();
+  }
+  l.aggs = w.aggs;
+  l.seqcap = w.seqcap;
+  for (int k = 0; k < l.log_n; k++) {
+    const int32_t* o = l.log + k * WL;
+    if ((o[0] & 0xFF) != WOP_AGG) continue;
+    int32_t* e = l.aggs + (int64_t(real(o[1])) * ns + ((o[0] >> 8) & 0xFF)) * 3;
+    e[0] = (o[0] >> 16) & 0xFF; e[1] = o[2]; e[2] = o[3];
+  }
+  wave_sync();
+  return true;
+}
+
+// A round whose parallel evaluation may differ from the reference's queue-order one: two runs of the
+// round share a run sequence (AggregatesStore rows are per sequence, AggregatesStoreImpl.java:55-75)
+// and one of them wrote it -- the later run would have read the earlier one's fold (NFA.java:319-321,
+// 362-369) -- or, with SequenceMatchers, a run died before others read partial sequences (its
+// removePattern, NFA.java:142-143, changes the buffer they walk).
+// conf: 2 x GL words of LDS (each lane's run sequence, whether it wrote it)
+template <int GL>
+__device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf, const Grp<GL>& g, bool act, int seq,
+                                                    uint64_t dmask) {
+  if ((l.A->wave_agg & 2) && dmask) return true;
+  if (!(l.A->wave_agg & 1)) return false;
+  const int lane = g.gl;
+  conf[lane] = act ? seq : INT32_MIN;
+  conf[GL + lane] = act && l.ov_own;
+  wave_sync();
+  bool c = false;
+  for (int j = 0; j < lane && act; j++) c = c || (conf[j] == seq && (conf[GL + j] || l.ov_own));
+  wave_sync();
+  return g.ballot(c) != 0;
+}
+
+// profiling kernels (KCEP_PHASES): lane 0's clocks per phase of the record loop -- record setup,
+// evaluation rounds, buffer commit, run numbering + queue placement, matchConstruction
+#ifdef KCEP_PHASES
+#define KWP_MARK(t) const uint64_t t = clock64()
+#define KWP_ADD(i, t) l.ph[i] += clock64() - t
+#else
+#define KWP_MARK(t)
+#define KWP_ADD(i, t)
 #endif
-  return wave_key<AGG, WAVE>(A, seg, gp, w.g, s_arena, arena_words, s_priv);
+
+// AGG: the pattern reads or writes aggregates / reads partial sequences (DevProgram, abi.cpp
+// wave_stateful): the round machinery for them (conflict checks, the sequential re-evaluation,
+// applying the logged aggregate writes) is compiled in only then.
+// One key (segment `seg`) on the GL lanes of group gp (w, s_arena, s_priv: the group's LDS).
+// Returns false when a grouped key (GL < 64) outgrew its group (more than GROUP_RUNS live runs):
+// nothing of it was committed and it is re-run on a whole wave (nfa_wave_heavy).
+template <bool AGG, int GL>
+__device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL>& gp, WaveShared<GL>& w,
+                                         int32_t* s_arena, int arena_words, int32_t*& s_priv) {
+  const int lane = gp.gl;
+  Lane l;
+  int ok = 1;
+  if (lane == 0) {
+    ok = key_begin(l, A, seg, s_arena, arena_words) ? 1 : 0;
+    if (ok) {
+      lane_to_ws(w, l);
+      w.pool_words = l.pool_words;
+      w.arena = s_arena;
+      w.arena_cap = arena_words;
+      w.arena_used = l.arena_used >= 0 ? (l.arena_used + 3) & ~3 : arena_words;
+    }
+  }
+  ok = gp.bcast(ok);
+  if (!ok) return true;
+  wave_sync();
+  if (lane != 0) {
+    l.A = &A; l.P = A.P;
+    l.seg0 = A.seg_start[seg];
+    l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
+    l.wave = 0; l.cap_hit = 0;
+  }
+  l.wpool = &w.pool_words;
+  // every lane: the key's fixed shape (lane 0's key_begin set it)
+  l.C = gp.bcast(l.C);
+  l.nev = gp.bcast(l.nev);
+  l.evw = gp.bcast(l.evw);
+  l.cev = reinterpret_cast<const int32_t*>(gp.bcast(reinterpret_cast<uintptr_t>(l.cev)));
+  l.tq = reinterpret_cast<int32_t*>(gp.bcast(reinterpret_cast<uintptr_t>(l.tq)));
+  l.tq_cap = gp.bcast(l.tq_cap);
+  l.runs_delta = gp.bcast(l.runs_delta);
+  l.pool_words = 0;
+  l.rec_out_top = 0; l.rec_nmatch = 0;
+  l.slm = 0; l.sle = 0; l.flen = 0; l.tlen = 0;
+  ws_to_lane(l, w);
+  // private run lists and operation logs: written by every evaluation and read back by the commit
+  // and the queue placement.  A slice of LDS per lane (WAVE_PRIV words: 2 runs + 2 log entries, growing
+  // into the pool on demand).  Next to the full 2048-word arena it cost occupancy (C4 9.39 vs 8.34 ms,
+  // profiles/r03_ab_s5.jsonl); with the arena halved it is the faster build (7.78 vs 8.43 ms, r04)
+  const int q0 = 2;
+#if WAVE_PRIV > 0
+  constexpr int priv_stride = WAVE_PRIV, log0 = (WAVE_PRIV - 4 * q0) / WL;
+  static_assert(WAVE_PRIV % 4 == 0 && log0 >= 1, "WAVE_PRIV: room for the run list and one log entry");
+#else
+  constexpr int priv_stride = 4 * (q0 + q0 * WL / 4 + 4), log0 = q0;
+  if (lane == 0) {
+    s_priv = pool_alloc(l, int64_t(GL) * priv_stride);
+    if (!s_priv) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
+  }
+#endif
+  wave_sync();
+  const auto& P = KCEP_PROG(l);
+  const int ns = P.nslots;
+  Frame fr[MAXD];
+  int64_t err_rec = -1;
+  const bool proc = A.mode == CEP_MODE_PROCESSOR;
+#ifdef KCEP_PHASES
+  for (int i = 0; i < 11; i++) l.ph[i] = 0;
+#endif
+  int32_t live_max = w.qlen;
+  int64_t evals = 0;
+  const uint64_t t0 = A.profile ? wall_clock64() : 0;
+  if (!w.overflow) {
+    int32_t* pv = s_priv + int64_t(lane) * priv_stride;
+    l.tq = pv;
+    l.tq_cap = q0;
+    l.log = pv + 4 * q0;
+    l.log_cap = log0;
+  }
+  l.wtop = &w.heap_top;
+  for (int i = 0; i < l.L && !w.err && !w.overflow; i++) {
+    if (GL < WAVE && w.qlen > GROUP_RUNS) return false;          // too many runs for the group: a whole wave
+    const int r = l.C + i;
+    const int64_t g = l.seg0 + i;
+    l.r = r;
+    l.g = g;
+    KWP_MARK(t_rec);
+    ws_to_lane(l, w);
+    for (int x = lane; x < ns * NW; x += GL) {                   // the record's buffer nodes: none yet
+      const int k = x & (NW - 1);
+      l.nodes[(int64_t(r) * ns) * NW + x] = (k == 1 || k == 2) ? -1 : 0;
+    }
+    if (proc) {
+      if (!record_admitted(l, g)) { wave_sync(); continue; }
+      for (int k = lane; k < w.qlen; k += GL) l.qa[4 * k] &= ~(1 << 17);   // isIgnored not serialised (Q3)
+    }
+    wave_sync();
+    eval_event_only(l);
+    const int n = w.qlen;
+    evals += n;
+    if (lane == 0) { l.rec_out_top = w.out_top; l.rec_nmatch = w.nmatch; }
+    int qn = 0, flen = 0;
+    KWP_ADD(0, t_rec);
+    for (int base = 0; base < n && !w.err && !w.overflow; base += GL) {
+      const int my = base + lane;
+      const bool act = my < n;
+      Run run{0, 0, 0, 0};
+      if (act) {
+        const int4 x = reinterpret_cast<const int4*>(l.qa)[my];
+        run = Run{x.x, x.y, x.z, x.w};
+      }
+      const int top0 = w.heap_top;
+      const int nact = n - base < GL ? n - base : GL;
+      bool good = true, seqd = false;
+      int jj = 0;                                              // sequential mode: the lane evaluating
+      uint64_t emask = 0, dmask = 0;
+      bool err_lane = false;
+      KWP_MARK(t_ev);
+      for (;;) {
+        // one evaluation pass: every lane its run with logged side effects (parallel), or -- for a
+        // stateful round that conflicts (wave_round_conflict) -- lane jj alone with the lane kernel's
+        // immediate ones, on the key's shared state, lanes in queue order (one call site of evaluate)
+        const bool me = seqd ? lane == jj : act;
+        if (seqd) {
+          wave_sync();
+          if (me) ws_to_lane(l, w);
+        } else {
+          l.heap = w.heap; l.heapcap = w.heapcap;
+        }
+        if (me || !seqd) { l.tlen = 0; l.log_n = 0; l.nph = 0; l.err = 0; l.overflow = 0; l.wgrow = 0; l.ov_own = 0; }
+        l.wave = seqd ? 0 : 1;
+        good = true;
+        if (me) good = evaluate(l, run, fr);
+        l.wave = 0;
+        if (seqd) {
+          if (me) {
+            if (good && l.tlen == 0) buf_peek(l, r_sid(run), run.ev, run.ver, true, nullptr, 0);   // removePattern
+            const int e = l.err, o = l.overflow;
+            lane_to_ws(w, l);
+            if (e) w.err = e;
+            if (o) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
+          }
+          wave_sync();
+          if (w.err || w.overflow || ++jj >= nact) break;
+          continue;
+        }
+        const bool grow = gp.ballot(l.wgrow) != 0;
+        const bool pool_out = gp.ballot(l.overflow && !l.wgrow) != 0;
+        if (pool_out) {                                        // a private list could not grow
+          if (lane == 0) w.overflow = 1;
+          const uint64_t ch = gp.ballot(l.cap_hit);
+          if (lane == 0 && ch) w.cap_hit = 1;
+          break;
+        }
+        if (grow) {
+          wave_sync();
+          if (lane == 0) w.heap_top = top0;
+          wave_sync();
+          if (!wave_heap_reserve(l, w, int64_t(w.heapcap) * 2, gp)) break;
+          continue;
+        }
+        err_lane = act && !good && l.err;
+        const bool dead = act && good && l.tlen == 0;
+        emask = gp.ballot(err_lane);
+        dmask = gp.ballot(dead);
+        // a conflict is checked before the errors: a run may throw on a state an earlier run of the
+        // round would have folded first
+        if (AGG && A.wave_agg && wave_round_conflict(l, w.conf, gp, act, run.seq, dmask)) {
+          seqd = true;
+          l.tlen = 0; l.log_n = 0; l.nph = 0;                  // the parallel pass is discarded
+          continue;
+        }
+        break;
+      }
+      wave_sync();
+      KWP_ADD(1, t_ev);
+      if (w.overflow) break;
+      // commit in queue order
+      KWP_MARK(t_cm);
+      if (seqd) {                                              // (committed as evaluated)
+        ws_to_lane(l, w);
+        if (w.err) { KWP_ADD(2, t_cm); break; }
+      } else if (!emask && !dmask) {
+        const int e = wave_commit_parallel(l, w, gp, r);
+        if (lane == 0 && e) w.err = e;
+        wave_sync();
+      } else {
+        w.logp[lane] = l.log;
+        w.logn[lane] = l.log_n;
+        w.errc[lane] = err_lane ? l.err : 0;
+        wave_sync();
+        if (lane == 0) {                                       // the reference's order, sequentially
+          ws_to_lane(l, w);
+          l.err = 0; l.overflow = 0;
+          for (int j = 0; j < nact && !l.err && !l.overflow; j++) {
+            const int32_t* lg = w.logp[j];
+            for (int k = 0; k < w.logn[j] && !l.err && !l.overflow; k++) {
+              const int32_t* o = lg + k * WL;
+              const int kind = o[0] & 0xFF, sid = (o[0] >> 8) & 0xFF, psid = (o[0] >> 16) & 0xFF;
+              if (kind == WOP_PUT5) buf_put5(l, sid, o[1], psid, o[2], o[3]);
+              else if (kind == WOP_PUT3) buf_put3(l, sid, o[1], o[3]);
+              else if (kind == WOP_BRANCH) buf_branch(l, sid, o[1], o[3]);
+            }
+            if (l.err || l.overflow) break;
+            if ((emask >> j) & 1) { l.err = w.errc[j]; break; }
+            if ((dmask >> j) & 1) {                            // removePattern (:160-163)
+              const int4 x = reinterpret_cast<const int4*>(l.qa)[base + j];
+              buf_peek(l, x.x & 0xFF, x.z, x.y, true, nullptr, 0);
+            }
+          }
+          lane_to_ws(w, l);
+        }
+        wave_sync();
+        ws_to_lane(l, w);
+      }
+      KWP_ADD(2, t_cm);
+      if (w.err || w.overflow) break;
+      // NFA.runs: the round's placeholders in queue order
+      KWP_MARK(t_pl);
+      int nrun = 0;
+      const int rb = w.runs + gp.excl_scan(l.nph, nrun);
+      if (AGG && (A.wave_agg & 1) && !seqd && !wave_apply_aggs(l, w, gp, rb)) {   // the round's folds and copies
+        if (lane == 0) w.overflow = 1;
+        break;
+      }
+      int nf = 0, nq = 0;
+      for (int t = 0; t < l.tlen; t++) {
+        int4* y = reinterpret_cast<int4*>(l.tq) + t;
+        if (y->w < -1) y->w = rb + (-y->w - 2) + 1;
+        if (is_fwd_final(l, y->x & 0xFF, (y->x >> 8) & 0xFF)) nf++; else nq++;
+      }
+      int tf = 0, tq = 0;
+      const int ef = gp.excl_scan(nf, tf), eq = gp.excl_scan(nq, tq);
+      wave_sync();
+      if (lane == 0) w.runs += nrun;
+      // room in the next queue and the final list
+      if (qn + tq > w.qb_cap) {
+        int32_t capw = w.qb_cap * 4;
+        int32_t* na = wave_regrow(l, w, w.qb, capw, int64_t(qn) * 4, int64_t(qn + tq) * 4, gp);
+        if (!na) break;
+        if (lane == 0) { w.qb = na; w.qb_cap = capw / 4; }
+      }
+      if (flen + tf > w.fq_cap) {
+        int32_t capw = w.fq_cap * 4;
+        int32_t* na = wave_regrow(l, w, w.fq, capw, int64_t(flen) * 4, int64_t(flen + tf) * 4, gp);
+        if (!na) break;
+        if (lane == 0) { w.fq = na; w.fq_cap = capw / 4; }
+      }
+      wave_sync();
+      int a = qn + eq, b = flen + ef;
+      for (int t = 0; t < l.tlen; t++) {
+        const int4 y = reinterpret_cast<const int4*>(l.tq)[t];
+        if (is_fwd_final(l, y.x & 0xFF, (y.x >> 8) & 0xFF)) reinterpret_cast<int4*>(w.fq)[b++] = y;
+        else reinterpret_cast<int4*>(w.qb)[a++] = y;
+      }
+      qn += tq;
+      flen += tf;
+      wave_sync();
+      KWP_ADD(3, t_pl);
+    }
+    if (w.err) { err_rec = A.base + g; break; }
+    if (w.overflow) break;
+    // swap the queues; matchConstruction (:151-158); the high-water mark on lane 0
+    if (lane == 0) {
+      int32_t* t = w.qa; w.qa = w.qb; w.qb = t;
+      const int32_t c = w.qa_cap; w.qa_cap = w.qb_cap; w.qb_cap = c;
+      w.qlen = qn;
+    }
+    wave_sync();
+    KWP_MARK(t_mc);
+    if (flen && !wave_emit_matches(l, w, gp, flen)) {
+      if (lane == 0) w.overflow = 1;
+    }
+    wave_sync();
+    KWP_ADD(4, t_mc);
+    if (lane == 0 && !w.err && !w.overflow) {
+      ws_to_lane(l, w);
+      if (proc && !record_hwm(l, g)) l.overflow = 1;
+      lane_to_ws(w, l);
+    }
+    wave_sync();
+    if (w.err) { err_rec = A.base + g; break; }
+    live_max = w.qlen > live_max ? w.qlen : live_max;
+  }
+  wave_sync();
+  if (lane == 0) {
+    ws_to_lane(l, w);
+    l.pool_words = int64_t(w.pool_words);
+    l.wpool = nullptr;
+    l.wave = 0;
+    key_end(l, A, seg, err_rec, live_max, evals, t0);
+  }
+  return true;
 }
 
 // The key segments of a batch, GL lanes per key: workgroup b takes segments b * (64 / GL) ... (one
@@ -153,29 +756,25 @@ template <bool AGG, int GL>
 __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   constexpr int NG = WAVE / GL;
   constexpr int ARENA = (GL == WAVE ? WAVE_ARENA : GROUP_ARENA) & ~3;   // LDS words of each key's hot workspace
-  __shared__ WaveSharedU<GL> ws[NG];
-  // (+4 words: the LDS mode's arena and private slices never start at LDS offset 0, which an LDS pointer
-  // test would take for null)
-  __shared__ __attribute__((aligned(16))) int32_t s_arena[NG * ARENA + 8];
+  __shared__ WaveShared<GL> ws[NG];
+  __shared__ __attribute__((aligned(16))) int32_t s_arena[NG * ARENA + 4];
   __shared__ int32_t* s_priv[NG];
   const Grp<GL> gp{int(threadIdx.x) & (GL - 1), int(threadIdx.x) & ~(GL - 1)};
   const int grp = int(threadIdx.x) / GL;
   const int seg = int(blockIdx.x) * NG + grp;
   if (seg >= A.nseg) return;
 #if WAVE_PRIV > 0
-  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV + 4];
-  if (gp.gl == 0) s_priv[grp] = s_priv_lds + 4 + gp.base * WAVE_PRIV;
+  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
+  if (gp.gl == 0) s_priv[grp] = s_priv_lds + gp.base * WAVE_PRIV;
 #endif
-  int r;
-  if constexpr (GL == WAVE) r = wave_key_any<AGG>(A, seg, gp, ws[grp], s_arena + 4, ARENA, s_priv[grp]);
-  else r = wave_key<AGG, GL>(A, seg, gp, ws[grp].g, s_arena + grp * ARENA, ARENA, s_priv[grp]);
-  if (r == 0 && gp.gl == 0) A.heavy[atomicAdd(A.heavy_n, 1)] = seg;
+  if (!wave_key<AGG, GL>(A, seg, gp, ws[grp], s_arena + grp * ARENA, ARENA, s_priv[grp]) && gp.gl == 0)
+    A.heavy[atomicAdd(A.heavy_n, 1)] = seg;
 }
 
 // The heavy list of a grouped launch, one key per workgroup-wave (persistent over the list).
 template <bool AGG>
 __device__ __forceinline__ void nfa_wave_heavy(const NfaArgs& A) {
-  __shared__ WaveSharedU<WAVE> w;
+  __shared__ WaveShared<WAVE> w;
   __shared__ __attribute__((aligned(16))) int32_t s_arena[WAVE_ARENA];
   __shared__ int32_t* s_priv;
 #if WAVE_PRIV > 0
@@ -185,7 +784,7 @@ __device__ __forceinline__ void nfa_wave_heavy(const NfaArgs& A) {
   const Grp<WAVE> gp{int(threadIdx.x), 0};
   const int nh = *A.heavy_n;
   for (int i = blockIdx.x; i < nh; i += gridDim.x) {
-    wave_key<AGG, WAVE>(A, A.heavy[i], gp, w.g, s_arena, WAVE_ARENA, s_priv);   // (generic: keys that grew)
+    wave_key<AGG, WAVE>(A, A.heavy[i], gp, w, s_arena, WAVE_ARENA, s_priv);
     wave_sync();
   }
 }
