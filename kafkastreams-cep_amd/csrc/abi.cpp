@@ -305,10 +305,10 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
     total += (arrs[i].bytes + 255) & ~size_t(255);
   }
   if (!total) return CEP_OK;
-  // zero copy (the stencil path's one streaming pass, small batches): the kernel reads the pinned ring
-  // over the link itself, no copy into HBM first (KCEP_ZERO_COPY=0 turns it off for A/B).  Pinned
-  // caller memory takes it too: one host memcpy beats waiting for a DMA before the call may return
-  // (r04 flush probe, 64 k records: 55.8 us per flush pageable through the ring, 67-69 us pinned by DMA)
+  // zero copy (the stencil path's one streaming pass, batches up to kZeroCopyMax): the kernel reads the
+  // pinned ring over the link itself, no copy into HBM first (KCEP_ZERO_COPY=0 turns it off for A/B).
+  // Pinned caller memory takes it too: one host memcpy beats waiting for a DMA before the call may
+  // return (r04 flush probe, 64 k records: 55.8 us per flush through the ring, 67-69 us pinned by DMA)
   static const bool zc_env = [] { const char* e = getenv("KCEP_ZERO_COPY"); return !(e && e[0] == '0'); }();
   if (zero_copy && zc_env && total <= kZeroCopyMax) {
     const int j = s->ring_next;
@@ -366,7 +366,7 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
       if (s->ring[j]) HIPCHECK(hipHostFree(s->ring[j]));
       s->ring[j] = nullptr;
       s->ring_cap[j] = 0;
-      HIPCHECK(hipHostMalloc(&s->ring[j], want, hipHostMallocDefault));
+      HIPCHECK(hipHostMalloc(&s->ring[j], want, hipHostMallocMapped));   // (the slot may serve a zero-copy batch later)
       s->ring_cap[j] = want;
     }
     uint8_t* h = static_cast<uint8_t*>(s->ring[j]);
@@ -1962,6 +1962,8 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
   memcpy(b.data(), in + 28, size_t(w) * 4);
   const int nhwm = b[CB_NHWM], qlen = b[CB_QLEN], nev = b[CB_NEV], nnode = b[CB_NNODE], npred = b[CB_NPRED];
   const int nver = b[CB_NVER], nseq = b[CB_NSEQ], ncols = b[CB_NCOLS], nst = b[CB_NSTATES];
+  if (nhwm < 0 || qlen < 0 || nev < 0 || nnode < 0 || npred < 0 || nver < 0 || nseq < 0 || ncols < 0 || nst < 0)
+    return fail(CEP_E_ARG, "bad state blob");
   const int evw = 8 + 2 * ncols;
   const int64_t total = int64_t(CB_HDR) + 3 * nhwm + 4 * qlen + int64_t(evw) * nev + 4 * nnode + 4 * npred + nver +
                         int64_t(3) * nst * nseq;
@@ -2022,13 +2024,16 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
     i32(x[1]);
     i64(x[2]);
     int cnt = 0;
-    for (int pi = x[3]; pi >= 0 && cnt <= npred; pi = pr[4 * pi + 3]) cnt++;
-    if (cnt > npred) return fail(CEP_E_ARG, "bad predecessor list in state blob");
+    bool bad = false;
+    for (int pi = x[3]; pi >= 0; pi = pr[4 * pi + 3])   // a link out of the list, or a cycle: malformed
+      if (pi >= npred || ++cnt > npred) { bad = true; break; }
+    if (bad) return fail(CEP_E_ARG, "bad predecessor list in state blob");
     i32(cnt);
     for (int pi = x[3]; pi >= 0; pi = pr[4 * pi + 3]) {
       const int32_t* y = pr + 4 * pi;
       if (!version(y[0])) return fail(CEP_E_ARG, "bad version in state blob");
       const bool has = y[1] >= 0;
+      if (y[1] >= P.dev.nslots) return fail(CEP_E_ARG, "bad predecessor in state blob");
       i32(has ? 1 : 0);
       str(has ? P.names[size_t(slot[size_t(y[1])].first)] : std::string());
       i32(has ? slot[size_t(y[1])].second : 0);
