@@ -144,3 +144,45 @@ def test_runs_eligibility():
     runs = {f["name"] for f in scenarios() if N.CompiledPattern(bytes.fromhex(f["ir"])).info.runs_ok}
     assert {"nfa_stateful_condition", "nfa_one_or_more", "nfa_times3", "nfa_strict3"} <= runs
     assert not runs & {"nfa_sequence_condition", "nfa_zero_or_more", "nfa_any_any", "stock_demo"}
+
+
+def _kcst(words, key=0):
+    """A single-key KCST blob (cep_state_evict's format) around the key's state words."""
+    import struct
+    w = list(words)
+    return struct.pack("<IIqi", 0x5453434B, 1, 0, 1) + struct.pack("<ii", key, len(w)) + struct.pack("<%di" % len(w), *w)
+
+
+def test_state_to_reference_host_only():
+    """cep_state_to_reference (host-only): a minimal carried state -- one run on the begin stage with
+    version [1], one high-water mark -- becomes the KCRF form (runs counter, hwm, queue with its Dewey
+    digits), and malformed blobs are refused with CEP_E_ARG instead of read out of bounds."""
+    import struct
+    cp = N.CompiledPattern(synth.c4_pattern().to_ir(Schema([("value", "i32")])))
+    begin = [i for i, st in enumerate(cp.stages()) if st[1] == 0][0]      # StateType BEGIN
+    CB_HDR = 12
+    # header: words, runs lo/hi, nhwm, qlen, nev, nnode, npred, nver, nseq, ncols, nstates
+    hdr = [0, 5, 0, 1, 1, 0, 0, 0, 2, 0, 1, 0]
+    hwm = [0, 7, 0]                                   # topic 0, offset 7
+    queue = [begin | (0xFF << 8), 0, -1, 1]          # begin stage, version at 0, no event, seq 1
+    vers = [1, 1]                                     # [len 1, digit 1]
+    words = hdr + hwm + queue + vers
+    words[0] = len(words)
+    out = cp.state_to_reference(_kcst(words, key=3))
+    magic, ver, key, ncols, runs = struct.unpack_from("<IIiiq", out, 0)
+    assert (magic, ver, key, ncols, runs) == (0x4652434B, 1, 3, 1, 5)
+    nh, = struct.unpack_from("<i", out, 24)
+    assert nh == 1 and struct.unpack_from("<iq", out, 28) == (0, 7)
+    assert struct.unpack_from("<i", out, 40) == (0,)             # no events
+    qlen, sid, eps, flags, seq, last, ts, nd, d0 = struct.unpack_from("<iiiiqiqii", out, 44)
+    assert (qlen, sid, eps, flags, seq, last, ts, nd, d0) == (1, begin, -1, 0, 1, -1, -1, 1, 1)
+    bad = list(words)
+    bad[3] = -1                                       # negative hwm count
+    with pytest.raises(N.CepError):
+        cp.state_to_reference(_kcst(bad))
+    bad = list(words)
+    bad[CB_HDR + 3 + 1] = 40                          # the run's version outside the version section
+    with pytest.raises(N.CepError):
+        cp.state_to_reference(_kcst(bad))
+    with pytest.raises(N.CepError):
+        cp.state_to_reference(_kcst(words)[:-4])      # truncated
