@@ -169,6 +169,7 @@ __global__ __launch_bounds__(256) void runs_order(const unsigned long long* __re
 // stores); an entry finds its match by a binary search over the workgroup's entry offsets in LDS.
 __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
                                                    const int64_t* __restrict__ pos, const uint32_t* __restrict__ segs,
+                                                   int64_t nseg_rec,
                                                    const unsigned long long* __restrict__ sorted, int64_t nm,
                                                    const int64_t* __restrict__ ent_off, int64_t ne, int64_t base,
                                                    int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
@@ -191,9 +192,9 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
     match_key[m] = key[j];
     if (ent_off_out != ent_off) ent_off_out[m] = at;
     // the segments as two 16-B vectors, the second only when the first holds no terminator
-    const uint4* sv = reinterpret_cast<const uint4*>(segs + j * RUNS_MAX_SEGS);
-    const uint4 a = sv[0];
-    const uint4 b = a.w == ~0u ? make_uint4(~0u, ~0u, ~0u, ~0u) : sv[1];
+    const uint4* sv = reinterpret_cast<const uint4*>(segs);
+    const uint4 a = sv[j];
+    const uint4 b = a.w == ~0u ? make_uint4(~0u, ~0u, ~0u, ~0u) : sv[nseg_rec + j];
     s_seg[tid][0] = a.x; s_seg[tid][1] = a.y; s_seg[tid][2] = a.z; s_seg[tid][3] = a.w;
     s_seg[tid][4] = b.x; s_seg[tid][5] = b.y; s_seg[tid][6] = b.z; s_seg[tid][7] = b.w;
   }
@@ -438,7 +439,7 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
                               int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st) {
   if (nm <= 0) return hipSuccess;
-  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, sorted, nm,
+  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, R.n, sorted, nm,
                      ent_off, ne, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
   return hipGetLastError();
 }
