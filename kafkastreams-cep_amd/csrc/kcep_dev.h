@@ -181,8 +181,7 @@ struct RunsArgs {
   unsigned long long* err_n;
   int64_t err_cap;
   // runs_sim: the stages a run consumed, as up to RUNS_MAX_SEGS segments per start record j:
-  // segment i of start record j at segs[4 * j + i] (i < 4) and segs[4 * (n + j) + i - 4] (i >= 4):
-  // stage << 24 | offset of the segment's first record from j,
+  // segs[j * RUNS_MAX_SEGS + i] = stage << 24 | offset of the segment's first record from j,
   // terminated by ~0u when shorter (a run's consumed stages never increase, runs.hip); null: off
   uint32_t* segs;
   unsigned long long* seg_over;   // set when a run needs more segments or an offset >= 2^24

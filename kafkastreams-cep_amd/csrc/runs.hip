@@ -84,7 +84,16 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t per = (nw + 1023) / 1024, w0 = int64_t(threadIdx.x) * per, w1 = w0 + per < nw ? w0 + per : nw;
   int64_t c = 0, l = 0;
-  for (int64_t w = w0; w < w1; w++) { c += stat[w]; l += stat[W + w]; }
+  for (int64_t w = w0; w < w1; w += 8) {           // 8 loads of each array in flight, then the sums
+    int64_t cc[8], ll[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      cc[q] = w + q < w1 ? stat[w + q] : 0;
+      ll[q] = w + q < w1 ? stat[W + w + q] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) { c += cc[q]; l += ll[q]; }
+  }
   int64_t ic = c, il = l;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -169,7 +178,6 @@ __global__ __launch_bounds__(256) void runs_order(const unsigned long long* __re
 // stores); an entry finds its match by a binary search over the workgroup's entry offsets in LDS.
 __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
                                                    const int64_t* __restrict__ pos, const uint32_t* __restrict__ segs,
-                                                   int64_t nseg_rec,
                                                    const unsigned long long* __restrict__ sorted, int64_t nm,
                                                    const int64_t* __restrict__ ent_off, int64_t ne, int64_t base,
                                                    int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
@@ -192,9 +200,9 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
     match_key[m] = key[j];
     if (ent_off_out != ent_off) ent_off_out[m] = at;
     // the segments as two 16-B vectors, the second only when the first holds no terminator
-    const uint4* sv = reinterpret_cast<const uint4*>(segs);
-    const uint4 a = sv[j];
-    const uint4 b = a.w == ~0u ? make_uint4(~0u, ~0u, ~0u, ~0u) : sv[nseg_rec + j];
+    const uint4* sv = reinterpret_cast<const uint4*>(segs + j * RUNS_MAX_SEGS);
+    const uint4 a = sv[0];
+    const uint4 b = a.w == ~0u ? make_uint4(~0u, ~0u, ~0u, ~0u) : sv[1];
     s_seg[tid][0] = a.x; s_seg[tid][1] = a.y; s_seg[tid][2] = a.z; s_seg[tid][3] = a.w;
     s_seg[tid][4] = b.x; s_seg[tid][5] = b.y; s_seg[tid][6] = b.z; s_seg[tid][7] = b.w;
   }
@@ -439,7 +447,7 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
                               int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st) {
   if (nm <= 0) return hipSuccess;
-  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, R.n, sorted, nm,
+  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, sorted, nm,
                      ent_off, ne, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
   return hipGetLastError();
 }
