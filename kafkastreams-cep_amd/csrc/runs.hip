@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -400,7 +401,8 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
   if (n <= 0) return hipSuccess;
   const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
   if (chunk > RUNS_CHUNK || chunk < 64) return hipErrorInvalidValue;
-  if (nw <= (int64_t(1) << 16)) {
+  static const bool one_block = [] { const char* e = getenv("KCEP_RUNS_CHUNKSCAN"); return !(e && e[0] == '0'); }();
+  if (one_block && nw <= (int64_t(1) << 16)) {
     hipLaunchKernelGGL(runs_chunk_scan, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
   } else {
     hipError_t e = exclusive_scan(stat, nw, pre, tot_cnt, scan_tmp, st);
