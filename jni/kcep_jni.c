@@ -1,5 +1,7 @@
 /*
- * kcep_jni.c -- JNI shims between java/GpuCEPProcessor.java and libkcep.so (include/kcep.h).
+ * kcep_jni.c -- JNI shims between libkcep.so (include/kcep.h) and the Java side:
+ *   java/com/github/fhuss/kafka/streams/cep/processor/GpuCEPProcessor.java (cep* natives) and
+ *   java/com/github/fhuss/kafka/streams/cep/pattern/PatternIR.java (irb* natives, the IR builder).
  *
  * NOT BUILT in this repository: the image has no JDK, hence no jni.h.  A
  * maintainer builds it with

@@ -20,7 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "jni_stub", "libkcep_jni_test.so")
 PFX = "Java_com_github_fhuss_kafka_streams_cep_processor_GpuCEPProcessor_"
 
-# every native method of java/GpuCEPProcessor.java
+# every native method of java/com/github/fhuss/kafka/streams/cep/processor/GpuCEPProcessor.java
 NATIVES = ["cepCompile", "cepStageNames", "cepSessionOpen", "cepSessionPath", "cepPushBatch", "cepCollect",
            "cepBatchErrors", "cepStreamPosition", "cepStateExport", "cepStateImport", "cepStateEvict",
            "cepStateImportKeys", "cepStatePositions", "cepSetMaxKeyWords", "cepSessionClose", "cepPatternFree",

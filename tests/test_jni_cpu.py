@@ -1,5 +1,5 @@
 """The JNI shim (jni/kcep_jni.c) without a GPU: compiled unchanged against tests/jni_stub/jni.h, it
-exports one symbol per ``native`` method of java/GpuCEPProcessor.java, and its host-only calls
+exports one symbol per ``native`` method of java/com/github/fhuss/kafka/streams/cep/processor/GpuCEPProcessor.java, and its host-only calls
 (pattern compile, stage names, blob positions) work through a mock JNIEnv with every pinned array
 released."""
 import os

@@ -1,5 +1,5 @@
 """The Java drop-in's boundary on the GPU: jni/kcep_jni.c (compiled unchanged against
-tests/jni_stub/jni.h) driven call for call as java/GpuCEPProcessor.java drives it
+tests/jni_stub/jni.h) driven call for call as java/com/github/fhuss/kafka/streams/cep/processor/GpuCEPProcessor.java drives it
 (tests/jni_twin.py), record by record through ``process()`` with flushes every ``batch_size``
 records, against the oracle over the same arrival-order stream in processor mode.
 
