@@ -347,6 +347,7 @@ std::shared_ptr<const JitModule> build(const std::string& src, const char* const
       why = std::string("kernel not found: ") + kernels[i];
       return nullptr;
     }
+  if (src.find("#define GROUP_LANES 32\n") != std::string::npos) m->group_lanes = 32;
   c.mods[{dev, src}] = m;
   return m;
 }
@@ -392,6 +393,10 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // ... of each key of the grouped wave kernel, and its lanes per key / live-run limit (tuning only)
   if (const char* genv = getenv("KCEP_GROUP_ARENA"))
     o += "#define GROUP_ARENA " + std::to_string(std::min(4096, std::max(4, atoi(genv)))) + "\n";
+  if (const char* genv = getenv("KCEP_GROUP_LANES")) {        // lanes per key of the grouped kernel: 16 or 32
+    const int gl = atoi(genv) >= 32 ? 32 : 16;
+    o += "#define GROUP_LANES " + std::to_string(gl) + "\n";
+  }
   if (const char* genv = getenv("KCEP_GROUP_RUNS"))
     o += "#define GROUP_RUNS " + std::to_string(std::max(1, atoi(genv))) + "\n";
   // LDS words per lane of the wave kernel's private run lists / logs (KCEP_WAVE_PRIV, tuning only; 0: pool)

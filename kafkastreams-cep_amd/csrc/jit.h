@@ -19,6 +19,7 @@ struct JitModule {
   hipFunction_t nfa_wave = nullptr;     // nfa_wave.h nfa_wave_body, one key per wave (general path)
   hipFunction_t nfa_wave16 = nullptr;   // nfa_wave.h nfa_wave_body, four keys per wave
   hipFunction_t nfa_heavy = nullptr;    // nfa_wave.h nfa_wave_heavy: the grouped launch's outgrown keys
+  int group_lanes = 16;                 // lanes per key of nfa_wave16 (the source's GROUP_LANES)
   ~JitModule();
 };
 

@@ -190,7 +190,7 @@ hipError_t nfa_wave_launch(const NfaArgs& A, bool grouped, hipStream_t st, const
   if (A.nseg <= 0) return hipSuccess;
   NfaArgs a = A;
   void* args[] = {&a};
-  constexpr int NG = 64 / GROUP_LANES;
+  const int NG = 64 / (j ? j->group_lanes : GROUP_LANES);
   if (!grouped) {
     if (j) return hipModuleLaunchKernel(j->nfa_wave, unsigned(A.nseg), 1, 1, 64, 1, 1, 0, st, args, nullptr);
     if (A.wave_agg) hipLaunchKernelGGL((nfa_wave_kernel<true, 64>), dim3(unsigned(A.nseg)), dim3(64), 0, st, A);
