@@ -1061,8 +1061,9 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
     if (s->prog.ensure(sizeof(StencilProgram)) || s->status.ensure(sizeof(int64_t) * size_t(2 * nt + 2)) ||
         s->counter.ensure(sizeof(int64_t) * size_t(nt / 1024 + 4)) || s->total.ensure(64) || s->sum.ensure(64) ||
         s->out.ensure(sizeof(int32_t) * size_t(k) * size_t(out_cap)) ||
-        // (+ one super-tile of ints: a last, partial super-tile's aux bytes lie past its tiles' ints)
-        s->slots.ensure(sizeof(int32_t) * (size_t(k) * size_t(nt) + 4) * 4096))
+        // (+ one super-tile of ints: a last, partial super-tile's aux bytes lie past its tiles' ints;
+        // + the plain kernel's dense region, ST_DENSE ints per super-tile)
+        s->slots.ensure(sizeof(int32_t) * ((size_t(k) * size_t(nt) + 4) * 4096 + size_t(nt) * ST_DENSE)))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
     s->out_cap = out_cap;
     if (hipMemcpy(s->prog.p, &P.stencil, sizeof(StencilProgram), hipMemcpyHostToDevice) ||

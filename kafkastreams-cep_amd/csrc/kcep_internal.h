@@ -166,6 +166,15 @@ struct DeliverArgs {
   unsigned* ticket = nullptr;     // device: workgroups done (the last one stamps hdr[2] = stamp; reset to 0)
   int64_t stamp = 0;              // this delivery's number: cep_collect spins until hdr[2] holds it
 };
+// The plain stencil kernel without carry stores a super-tile's first ST_DENSE matches (one int each)
+// in a dense region at the head of the slot buffer (super-tile t at t * ST_DENSE) and the rest in
+// the super-tile's own region after it (nsuper * ST_DENSE + t * sub * 4096 + m): the dense runs sit
+// a few KB apart instead of 196 KB, C2 kernel -7.5 us (profiles/r04_ab_stencil_stores.txt).
+#ifndef KCEP_ST_DENSE
+#define KCEP_ST_DENSE 512                  // (<= 512: the session allocates 512 per tile; A/B builds only)
+#endif
+constexpr int ST_DENSE = KCEP_ST_DENSE;
+
 struct StencilLaunch {
   const int32_t* key;
   const void* val;
@@ -173,7 +182,7 @@ struct StencilLaunch {
   int64_t n;
   const StencilProgram* prog_dev;
   int k, coltype, use_topic, chain;
-  int32_t* slots;                 // per-tile match slots, ST_TILE * k ints each
+  int32_t* slots;                 // per-tile match slots, ST_TILE * k ints each (+ ST_DENSE per tile, see below)
   int64_t* tile_count;            // matches per tile
   int64_t* tile_pre;              // their exclusive prefix
   int64_t* scan_tmp;

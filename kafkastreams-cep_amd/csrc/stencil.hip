@@ -20,8 +20,15 @@ hipError_t stencil_count_k8(const StencilLaunch& L, hipStream_t st);
 // stages are consecutive records); the keyed kernel: its completing record, with an aux byte per
 // match after the super-tile's sub x 4096 ints (stencil_row) -- written out as k-int rows.
 struct SlotFormat {
-  int k, plain, chain, carry;
-  __device__ __forceinline__ int32_t entry(const int32_t* src, const uint8_t* aux, int64_t m, int s) const {
+  int k, plain, chain, carry, dense;
+  int64_t nsuper;
+  int sub;
+  // match m of super-tile t, stage s
+  __device__ __forceinline__ int32_t entry(const int32_t* slots, int64_t t, int64_t m, int s) const {
+    if (dense)                                   // the plain kernel without carry (kcep_internal.h ST_DENSE)
+      return (m < ST_DENSE ? slots[t * ST_DENSE + m] : slots[nsuper * ST_DENSE + t * int64_t(sub) * ST_TILE + m]) + s;
+    const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
+    const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
     const int32_t v = src[m];
     if (plain) {                                 // first record; carry boundary: -(1 + completing record)
       if (!carry || v >= 0) return v + s;
@@ -38,11 +45,9 @@ __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict_
   const int k = F.k;
   const int64_t words = cnt[t] * k, dst = pre[t] * k;
   if (pre[t] + cnt[t] > out_cap) return;
-  const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
-  const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
   for (int64_t w = threadIdx.x; w < words; w += blockDim.x) {
     const int64_t m = w / k;
-    out[dst + w] = F.entry(src, aux, m, int(w - m * k));
+    out[dst + w] = F.entry(slots, t, m, int(w - m * k));
   }
 }
 
@@ -133,12 +138,10 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
   for (int64_t t = wid; t < nt; t += 16) {                 // one wave per super-tile
     const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
     if (pre + m > out_cap) continue;
-    const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
-    const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
     int32_t* dst = out + pre * k;
     for (int64_t w = lane; w < m * k; w += 64) {
       const int64_t q = w / k;
-      dst[w] = F.entry(src, aux, q, int(w - q * k));
+      dst[w] = F.entry(slots, t, q, int(w - q * k));
     }
   }
 }
@@ -200,15 +203,13 @@ __global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __r
   }
   const int64_t m = cnt[t];
   if (pre + m <= out_cap) {
-    const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
-    const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
     for (int64_t q = threadIdx.x; q < m; q += 256) {
       const int64_t i = pre + q;
       int32_t row[STENCIL_MAX_K], last = 0;
 #pragma unroll
       for (int s = 0; s < STENCIL_MAX_K; s++)
         if (s < k) {
-          row[s] = F.entry(src, aux, q, s);
+          row[s] = F.entry(slots, t, q, s);
           out[i * k + s] = row[s];
           last = row[s];
         }
@@ -271,7 +272,8 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e == hipSuccess && ev1) e = hipEventRecord(ev1, st);
   if (e != hipSuccess) return e;
   // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
-  const SlotFormat F{L.k, L.plain && !L.chain && L.k <= 7, L.chain, L.carry.hdr != nullptr};
+  const bool plain = L.plain && !L.chain && L.k <= 7;
+  const SlotFormat F{L.k, plain, L.chain, L.carry.hdr != nullptr, plain && !L.carry.hdr && ST_PLAIN_STAGE, nsuper, sub};
   if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr) {   // a small carry flush: scan, rows and delivery at once
     hipLaunchKernelGGL(stencil_finish_deliver, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, nsuper,
                        L.k, L.out, L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey,

@@ -804,6 +804,16 @@ __device__ __forceinline__ void load_tile(Chunk<VT, TOPIC>& c, const int32_t* __
 // (and of every record whose neighbour lies in another lane), the only keys a visit reads.  A
 // boundary match is stored as -(1 + completing record) with its halo record count in the slot's
 // aux byte (stencil_gather writes the -(1 + d) halo entries); an interior one as its first record.
+#ifndef ST_PLAIN_STAGE
+#define ST_PLAIN_STAGE 1                          // the super-tile's matches staged in LDS, one store run (A/B knob)
+#endif
+#ifndef ST_PLAIN_NTSTORE
+#define ST_PLAIN_NTSTORE 0                        // the staged run stored non-temporally (A/B knob)
+#endif
+#ifndef ST_PLAIN_PROBE
+#define ST_PLAIN_PROBE 0                          // timing probes (A/B builds only): 1 no match stores, 2 per-wave runs,
+                                                  // 3 no match stores with barrier (B) kept
+#endif
 #ifndef ST_CARRY_WAVES
 #define ST_CARRY_WAVES 4                          // waves per SIMD the carry variant's registers are cut for
 #endif
@@ -821,6 +831,8 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
   __shared__ uint8_t s_tab[64];
   __shared__ uint8_t s_lut[256];
   __shared__ uint8_t s_nan[4];
+  constexpr bool STAGE = !CARRY && ST_PLAIN_STAGE;
+  __shared__ int32_t s_out[STAGE ? ST_TILE : 1];   // staged matches of the super-tile (see the tile loop's end)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -857,6 +869,10 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
   int32_t* slot = out + tile0 * int64_t(ST_TILE) * K;
   uint8_t* const aux = reinterpret_cast<uint8_t*>(slot + SUB * ST_TILE);   // carry: per match, after the ints
   int64_t sum = 0;
+  int nbuf = 0;                                   // STAGE: the first nbuf matches are staged in s_out (uniform)
+  // STAGE: the slot layout of kcep_internal.h ST_DENSE (the first matches in the dense region)
+  int32_t* const dense = out + int64_t(blockIdx.x) * ST_DENSE;
+  int32_t* const over = out + int64_t(gridDim.x) * ST_DENSE + tile0 * ST_TILE;
   for (int j = 0; j < ntl; j++) {                 // uniform
     const int64_t base = (tile0 + j) * ST_TILE;
     int32_t nk = INT32_MIN;                       // carry: the key after the tile (thread 255)
@@ -1026,6 +1042,22 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
       before += int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) << b;
       wtot += __popcll(m) << b;
     }
+#if ST_PLAIN_PROBE == 1 || ST_PLAIN_PROBE == 2
+    if constexpr (!CARRY) {                       // timing probes only (wrong output order / no output)
+      if (halo_lane) h_mask = s_mask[ST_TILE + tid];
+      if (ST_PLAIN_PROBE == 2) {
+        int32_t* ws = out + tile0 * int64_t(ST_TILE) * K + j * ST_TILE + wid * 1024 + before;
+        const int32_t b32 = int32_t(base) - (K - 1);
+        while (hit) {
+          const int i = __ffs(hit) - 1;
+          hit &= hit - 1;
+          *ws++ = b32 + tid * ST_EPT + i;
+        }
+      }
+      sum += wtot;
+      continue;
+    }
+#endif
     if (lane == 0) s_wsum[j & 1][wid] = wtot;
     if (halo_lane) h_mask = s_mask[ST_TILE + tid];   // the next tile's halo: this tile's last records
     if constexpr (CARRY)
@@ -1040,6 +1072,36 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
     }
     tot = __builtin_amdgcn_readfirstlane(tot);
     const int32_t b32 = int32_t(base) - (K - 1);  // record index < 2^31 (checked by the launcher)
+    if constexpr (STAGE) {
+      // the super-tile's matches are staged in LDS and stored once, as one run into the dense region
+      // (kcep_internal.h ST_DENSE): C2 kernel 139 -> 131 us; storing each tile's run into the
+      // super-tile's own region (196 KB apart) cost 16 us over no stores at all, with or without the
+      // LDS staging (profiles/r04_ab_stencil_stores.txt)
+      // A tile whose matches no longer fit (over a quarter of the super-tile's records matching)
+      // stores them straight to their place, and so do the later ones (sum only grows).
+      const int p0 = int(sum) + o;
+      if (ST_PLAIN_PROBE == 3) {                  // timing probe: barrier (B) kept, no stores
+        sum += tot;
+        continue;
+      }
+      if (sum + tot <= ST_TILE) {                 // uniform
+        for (int q = 0; hit; q++) {
+          const int i = __ffs(hit) - 1;
+          hit &= hit - 1;
+          s_out[p0 + q] = b32 + tid * ST_EPT + i;
+        }
+        nbuf = int(sum) + tot;
+      } else {
+        for (int q = 0; hit; q++) {
+          const int i = __ffs(hit) - 1;
+          hit &= hit - 1;
+          const int p = p0 + q;
+          (p < ST_DENSE ? dense : over)[p] = b32 + tid * ST_EPT + i;
+        }
+      }
+      sum += tot;
+      continue;
+    }
     // each thread stores its own matches at their place in the tile's run of the slot (no LDS
     // compaction and no third barrier: L2 merges the run's lines; 147.7-150.2 vs 150.8-152.1 us,
     // profiles/r03_ab_stencil_direct_store.jsonl).  ONE int per match -- its first record: the
@@ -1061,6 +1123,22 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
     slot += tot;
     sum += tot;
   }
+  if constexpr (STAGE) {
+    __syncthreads();                              // the last tile's staged matches
+#if ST_PLAIN_NTSTORE
+    for (int i = tid; i < nbuf; i += ST_THREADS) __builtin_nontemporal_store(s_out[i], &(i < ST_DENSE ? dense : over)[i]);
+#else
+    for (int i = tid; i < nbuf; i += ST_THREADS) (i < ST_DENSE ? dense : over)[i] = s_out[i];
+#endif
+  }
+#if ST_PLAIN_PROBE == 1 || ST_PLAIN_PROBE == 2
+  if constexpr (!CARRY) {
+    if (lane == 0) s_wsum[0][wid] = int(sum);
+    __syncthreads();
+    if (tid == 0) tile_count[blockIdx.x] = s_wsum[0][0] + s_wsum[0][1] + s_wsum[0][2] + s_wsum[0][3];
+    return;
+  }
+#endif
   if (tid == 0) tile_count[blockIdx.x] = sum;
   if constexpr (CARRY)
     if (twice) atomicOr(C.flags, 2ull);           // a key in two segments of the batch

@@ -73,6 +73,35 @@ def test_always_true_overlapping_matches():
     assert got == want and len(got) == n - 2 * len(np.unique(key))
 
 
+def test_match_dense_super_tiles():
+    """The plain kernel's slot layout at four tiles per workgroup (>= 8192 tiles): a super-tile's first
+    ST_DENSE (512) matches in the dense region, the rest in its own region, a tile whose matches no
+    longer fit the LDS staging (over 4096) stored straight to both (csrc/stencil_kernel.h STAGE).
+    Per super-tile: tile 0 no match (distinct keys), tile 1 400 matches, tiles 2-3 ~3.8 k each."""
+    import os
+    import torch
+    n = 8192 * 4096 + 1000
+    r = np.arange(n) % 16384
+    t, o = r // 4096, r % 4096
+    new = (t == 0) | ((t == 1) & ((o == 0) | (o >= 402))) | ((t >= 2) & (o % 37 == 0))
+    key = (np.cumsum(new) - 1).astype(np.int32)
+    val = np.zeros(n, np.int32)
+    ir = (QueryBuilder().select("a").where(True).then().select("b").where(True).then()
+          .select("c").where(True).build().to_ir(I32))
+    s = N.Session(N.CompiledPattern(ir), n)
+    assert s.path == N.PATH_STENCIL
+    dk, dv = torch.from_numpy(key).cuda(), torch.from_numpy(val).cuda()
+    s.push(n, dk.data_ptr(), [dv.data_ptr()], mem=N.MEM_DEVICE, stream=torch.cuda.current_stream().cuda_stream)
+    got = s.collect()
+    b = O.BatchArrays(key, [val], [1])
+    want = O.baseline_csr(O.OraclePattern(ir), b, O.MODE_PROCESSOR, min(16, os.cpu_count() or 1))
+    assert len(want["match_record"]) > 10_000_000
+    for f in ("match_record", "match_key", "ent_off", "ent_name", "ent_record"):
+        assert got[f].shape == want[f].shape, f
+        bad = np.flatnonzero(got[f] != want[f])
+        assert len(bad) == 0, (f, bad[:5], got[f][bad[:5]], want[f][bad[:5]])
+
+
 @pytest.mark.parametrize("t", ["i64", "f64"])
 def test_wide_columns(t):
     rng = np.random.default_rng(7)
