@@ -808,7 +808,7 @@ __device__ __forceinline__ void load_tile(Chunk<VT, TOPIC>& c, const int32_t* __
 #define ST_PLAIN_STAGE 1                          // the super-tile's matches staged in LDS, one store run (A/B knob)
 #endif
 #ifndef ST_PLAIN_NTSTORE
-#define ST_PLAIN_NTSTORE 0                        // the staged run stored non-temporally (A/B knob)
+#define ST_PLAIN_NTSTORE 1                        // the staged run stored non-temporally (A/B knob)
 #endif
 #ifndef ST_PLAIN_PROBE
 #define ST_PLAIN_PROBE 0                          // timing probes (A/B builds only): 1 no match stores, 2 per-wave runs,
