@@ -155,6 +155,24 @@ def test_device_resident_batch_and_checksum():
     assert (nm, cs) == (want_n, want_cs)
 
 
+def test_many_super_tiles_multi_workgroup_scan():
+    """Over 8192 super-tiles (140 M records) the tile counts are scanned by the multi-workgroup
+    exclusive_scan instead of tile_scan (csrc/stencil.hip stencil_launch)."""
+    import torch
+    n, K = 140_000_000, 1_000_000
+    key, val, order = synth.c2_stream_torch(n, K, "cuda")
+    cp = N.CompiledPattern(c2_ir())
+    s = N.Session(cp, n)
+    s.push(n, key.data_ptr(), [val.data_ptr()], mem=N.MEM_DEVICE,
+           stream=torch.cuda.current_stream().cuda_stream)
+    nm, cs = s.checksum()
+    hk, hv, ho = key.cpu().numpy(), val.cpu().numpy(), order.cpu().numpy()
+    del key, val, order, s
+    b = O.BatchArrays(hk, [hv], [1], offset=ho, ts=ho)
+    want_n, want_cs = O.baseline(O.OraclePattern(c2_ir()), b, O.MODE_PROCESSOR, 16)
+    assert (nm, cs) == (want_n, want_cs) and nm > 1_000_000
+
+
 def test_irregular_batches_route_to_general_path():
     """Null records and unflagged offsets break the stencil's contiguity assumption:
     the session hands those batches to the general NFA kernel, with the same result."""
