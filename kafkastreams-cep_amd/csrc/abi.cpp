@@ -1063,7 +1063,8 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
         s->out.ensure(sizeof(int32_t) * size_t(k) * size_t(out_cap)) ||
         // (+ one super-tile of ints: a last, partial super-tile's aux bytes lie past its tiles' ints;
         // + the plain kernel's dense region, ST_DENSE ints per super-tile)
-        s->slots.ensure(sizeof(int32_t) * ((size_t(k) * size_t(nt) + 4) * 4096 + size_t(nt) * ST_DENSE)))
+        s->slots.ensure(sizeof(int32_t) * ((size_t(k) * size_t(nt) + 4) * 4096 +
+                                           size_t(nt) * std::max<size_t>(ST_DENSE, ST_DENSE_KEYED * 5 / 4))))
       return cleanup(fail(CEP_E_HIP, "device allocation failed"));
     s->out_cap = out_cap;
     if (hipMemcpy(s->prog.p, &P.stencil, sizeof(StencilProgram), hipMemcpyHostToDevice) ||

@@ -174,6 +174,13 @@ struct DeliverArgs {
 #define KCEP_ST_DENSE 512                  // (<= 512: the session allocates 512 per tile; A/B builds only)
 #endif
 constexpr int ST_DENSE = KCEP_ST_DENSE;
+// The keyed kernel without carry (C5's chain) the same way, with its aux bytes: a super-tile's first
+// ST_DENSE_KEYED matches at t * ST_DENSE_KEYED ints and, after nsuper of those, their aux bytes at
+// t * ST_DENSE_KEYED; the rest in the super-tile's own region (ints, then aux bytes) after both.
+constexpr int ST_DENSE_KEYED = 1024;
+#ifndef ST_KEYED_DENSE
+#define ST_KEYED_DENSE 0                   // A/B knob (builds only; off: kernel -16 us, step +5 us on C5)
+#endif
 
 struct StencilLaunch {
   const int32_t* key;

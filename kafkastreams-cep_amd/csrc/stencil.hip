@@ -20,14 +20,20 @@ hipError_t stencil_count_k8(const StencilLaunch& L, hipStream_t st);
 // stages are consecutive records); the keyed kernel: its completing record, with an aux byte per
 // match after the super-tile's sub x 4096 ints (stencil_row) -- written out as k-int rows.
 struct SlotFormat {
-  int k, plain, chain, carry, dense;
+  int k, plain, chain, carry, dense, kdense;
   int64_t nsuper;
   int sub;
-  // match m of super-tile t, stage s
-  __device__ __forceinline__ int32_t entry(const int32_t* slots, int64_t t, int64_t m, int s) const {
+  // match m of super-tile t (c matches), stage s
+  __device__ __forceinline__ int32_t entry(const int32_t* slots, int64_t t, int64_t c, int64_t m, int s) const {
     if (dense)                                   // the plain kernel without carry (kcep_internal.h ST_DENSE)
       return (m < ST_DENSE ? slots[t * ST_DENSE + m] : slots[nsuper * ST_DENSE + t * int64_t(sub) * ST_TILE + m]) + s;
-    const int32_t* src = slots + t * int64_t(sub) * ST_TILE * k;
+    if (kdense && c <= ST_DENSE_KEYED) {         // the keyed kernel without carry (kcep_internal.h)
+      const int64_t i = t * ST_DENSE_KEYED + m;
+      return stencil_row(slots[i], reinterpret_cast<const uint8_t*>(slots + nsuper * ST_DENSE_KEYED)[i], s, k, chain,
+                         carry);
+    }
+    const int32_t* src = slots + (kdense ? nsuper * (ST_DENSE_KEYED + ST_DENSE_KEYED / 4) : 0) +
+                         t * int64_t(sub) * ST_TILE * k;
     const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
     const int32_t v = src[m];
     if (plain) {                                 // first record; carry boundary: -(1 + completing record)
@@ -47,7 +53,7 @@ __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict_
   if (pre[t] + cnt[t] > out_cap) return;
   for (int64_t w = threadIdx.x; w < words; w += blockDim.x) {
     const int64_t m = w / k;
-    out[dst + w] = F.entry(slots, t, m, int(w - m * k));
+    out[dst + w] = F.entry(slots, t, cnt[t], m, int(w - m * k));
   }
 }
 
@@ -64,7 +70,7 @@ __global__ __launch_bounds__(256) void stencil_gather_rows(const int32_t* __rest
   for (int64_t q = threadIdx.x; q < m; q += blockDim.x) {
     int32_t row[STENCIL_MAX_K];
 #pragma unroll
-    for (int s = 0; s < STENCIL_MAX_K; s++) row[s] = s < k ? F.entry(slots, t, q, s) : 0;
+    for (int s = 0; s < STENCIL_MAX_K; s++) row[s] = s < k ? F.entry(slots, t, m, q, s) : 0;
     int32_t* d = out + (p + q) * k;
     if (k == 4) {
       *reinterpret_cast<int4*>(d) = make_int4(row[0], row[1], row[2], row[3]);
@@ -166,7 +172,7 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
     int32_t* dst = out + pre * k;
     for (int64_t w = lane; w < m * k; w += 64) {
       const int64_t q = w / k;
-      dst[w] = F.entry(slots, t, q, int(w - q * k));
+      dst[w] = F.entry(slots, t, m, q, int(w - q * k));
     }
   }
 }
@@ -234,7 +240,7 @@ __global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __r
 #pragma unroll
       for (int s = 0; s < STENCIL_MAX_K; s++)
         if (s < k) {
-          row[s] = F.entry(slots, t, q, s);
+          row[s] = F.entry(slots, t, m, q, s);
           out[i * k + s] = row[s];
           last = row[s];
         }
@@ -299,7 +305,8 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   if (e != hipSuccess) return e;
   // the kernel that ran (stencil_kernel.h launch_kts) and its slot format
   const bool plain = L.plain && !L.chain && L.k <= 7;
-  const SlotFormat F{L.k, plain, L.chain, L.carry.hdr != nullptr, plain && !L.carry.hdr && ST_PLAIN_STAGE, nsuper, sub};
+  const SlotFormat F{L.k, plain, L.chain, L.carry.hdr != nullptr, plain && !L.carry.hdr && ST_PLAIN_STAGE,
+                     !plain && !L.carry.hdr && ST_KEYED_DENSE, nsuper, sub};
   if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr) {   // a small carry flush: scan, rows and delivery at once
     hipLaunchKernelGGL(stencil_finish_deliver, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, nsuper,
                        L.k, L.out, L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey,

@@ -657,8 +657,22 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
   // record) plus one aux byte (chain: start distance | consumed stages << 2 | halo records << 6;
   // carry: the stages taken from the halo) after the super-tile's SUB x 4096 ints; stencil_gather
   // writes the K-int rows (stencil_row)
-  int32_t* const slot = out + tile0 * int64_t(ST_TILE) * K;   // super-tile s_super's slot
-  uint8_t* const aux = reinterpret_cast<uint8_t*>(slot + SUB * ST_TILE);
+  // without carry, a super-tile of at most ST_DENSE_KEYED matches writes them to the dense regions
+  // (kcep_internal.h; uniform per workgroup), a larger one to its own region after them
+  constexpr bool KD = !CARRY && ST_KEYED_DENSE;
+  const int64_t nsup = gridDim.x;
+  int64_t stot = 0;
+#pragma unroll
+  for (int j = 0; j < SUB; j++) stot += total[j];
+  const bool dense = KD && stot <= ST_DENSE_KEYED;
+  int32_t* const own = out + (KD ? nsup * (ST_DENSE_KEYED + ST_DENSE_KEYED / 4) : 0) + tile0 * int64_t(ST_TILE) * K;
+  int32_t* const slot = dense ? out + int64_t(s_super) * ST_DENSE_KEYED : own;
+  uint8_t* const aux = dense ? reinterpret_cast<uint8_t*>(out + nsup * ST_DENSE_KEYED) + int64_t(s_super) * ST_DENSE_KEYED
+                             : reinterpret_cast<uint8_t*>(own + SUB * ST_TILE);
+  auto store_match = [&](int64_t m, int32_t v, uint8_t a) {
+    slot[m] = v;
+    if constexpr (K > 1) aux[m] = a;             // (k = 1: the own region has no room after the ints; never read)
+  };
   int64_t mbase = 0;                               // matches of the super-tile's earlier tiles
   if constexpr (CHAIN && CARRY) {                  // halo runs can exceed a tile's match space: fail the batch
     int64_t sum = 0;
@@ -696,8 +710,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         // one match: completing record rj, started d records before, consumed-stage mask cm; ho: the
         // segment's records before rj when the run started in the halo (3: it did not)
         auto put = [&](int32_t rj, uint32_t d, uint32_t cm, int ho) {
-          slot[mbase + o] = rj;
-          aux[mbase + o] = uint8_t(d | (cm << 2) | (uint32_t(ho) << 6));
+          store_match(mbase + o, rj, uint8_t(d | (cm << 2) | (uint32_t(ho) << 6)));
           o++;
         };
         while (any) {                                // record order; per record oldest start first
@@ -740,9 +753,9 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
         while (h) {
           const int i = __ffs(h) - 1;
           h &= h - 1;
-          slot[mbase + o] = int32_t(base + tid * ST_EPT + i);   // record index < 2^31 (checked by the launcher)
-          if constexpr (K > 1)                         // carry: the stages taken from the halo
-            aux[mbase + o] = CARRY ? uint8_t((bneed[j] >> (4 * i)) & 0xF) : uint8_t(0);
+          // record index < 2^31 (checked by the launcher); aux: carry: the stages taken from the halo
+          store_match(mbase + o, int32_t(base + tid * ST_EPT + i),
+                      CARRY && K > 1 ? uint8_t((bneed[j] >> (4 * i)) & 0xF) : uint8_t(0));
           o++;
         }
       }
