@@ -39,7 +39,8 @@ hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k,
                                   int32_t* dkey, int64_t* dpos, hipStream_t st);
 
 hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf);
-hipError_t nfa_wave_launch(const NfaArgs& A, bool grouped, hipStream_t st, const JitModule* j);
+hipError_t nfa_wave_launch(const NfaArgs& A, int64_t grid, hipStream_t st, const JitModule* j);
+int64_t nfa_wave_grid(int64_t nseg, bool agg, const JitModule* j);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
 hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
@@ -207,8 +208,7 @@ struct cep_session {
   bool jitg_tried = false;
   int64_t live_hwm = 0;                    // general path: most live runs any key held in the last batch
   bool wave = false;                       // general path: one key per wave (nfa_wave.h) for this pattern
-  bool grouped = false;                    // ... or four light keys per wave, outgrown keys on whole waves
-  DBuf heavy;                              // the grouped launch's outgrown segments
+  DBuf wscratch;                           // the wave kernel's recycled per-workgroup workspace regions
   bool g_any_err = false;                  // general path: some key of the last batch raised
   DBuf r_prof;                             // CEP_SESSION_PROFILE: per key segment {live max, evaluations, cycles}
   std::string jit_why;
@@ -815,16 +815,12 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   cap.out_mult = std::max<int32_t>(1, int32_t(cap.out_mult * scale));
   const size_t sb = size_t(nseg) * 8;
   if (s->r_matches.ensure(sb) || s->r_words.ensure(sb) || s->r_out.ensure(sb) || s->r_err.ensure(sb) ||
-      s->heavy.ensure(size_t(nseg) * 4 + 4) ||
       s->r_errrec.ensure(sb) || s->r_carry.ensure(sb) || s->ents.ensure(sb) || s->moff.ensure(sb) || s->eoff.ensure(sb))
     return fail(CEP_E_HIP, "allocation failed");
   // first-allocation words of every key (NfaCaps) plus the events carried into the batch
   const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base;
   const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 3 * D.nstates;
   int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
-  // the grouped wave kernel re-runs a key that outgrew its group from scratch on a whole wave, and the
-  // bump pool cannot give back what the first attempt took: count such keys twice
-  if (s->wave && s->grouped) est *= 2;
   s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
   A.cap = cap;
   A.carry = s->carry ? 1 : 0;
@@ -849,6 +845,19 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     if (s->r_prof.ensure(sb * NFA_PROFILE_W)) return fail(CEP_E_HIP, "allocation failed");
     A.profile = s->r_prof.as<int64_t>();
   }
+  // the wave kernel's persistent grid and its workgroups' scratch regions (nfa_wave.h): 16 K words
+  // each by default (KCEP_WAVE_SCRATCH words, 0: none -- every workspace from the pool)
+  int64_t wgrid = 0;
+  if (s->wave) {
+    const char* scr_env = getenv("KCEP_WAVE_SCRATCH");
+    const int64_t scr_words = scr_env ? std::max<int64_t>(0, atoll(scr_env)) & ~int64_t(3) : int64_t(1) << 14;
+    wgrid = nfa_wave_grid(nseg, A.wave_agg != 0, s->jitg.get());
+    A.scratch_words = scr_words;
+    if (scr_words > 0) {
+      if (s->wscratch.ensure(size_t(wgrid * scr_words) * 4)) return fail(CEP_E_HIP, "allocation failed");
+      A.scratch = s->wscratch.as<int32_t>();
+    }
+  }
   bool timed = false;
   bool pool_at_limit = false;                      // the pool cannot grow further: overflowing keys are handed back
   int64_t tots[2] = {0, 0};                        // matches, entries of the batch
@@ -864,12 +873,11 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.cpool_cap = s->carry ? s->cpool_words : 0;
     A.last_attempt = attempt >= kMaxRetry || pool_at_limit ? 1 : 0;   // then an overflowing key is handed back per key
     A.max_key_words = s->opts.max_key_words;
-    unsigned long long init[6] = {0, (unsigned long long)s->cpool_used, 0, 0, 0, 0};   // [5]: heavy count
+    unsigned long long init[6] = {0, (unsigned long long)s->cpool_used, 0, 0, 0, 0};   // [5]: next segment
     HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
-    A.heavy = s->heavy.as<int32_t>();
-    A.heavy_n = reinterpret_cast<int32_t*>(ctl + 5);
-    if (s->wave) HIPCHECK(nfa_wave_launch(A, s->grouped, st, s->jitg.get()));
+    A.seg_next = reinterpret_cast<int32_t*>(ctl + 5);
+    if (s->wave) HIPCHECK(nfa_wave_launch(A, wgrid, st, s->jitg.get()));
     else HIPCHECK(nfa_launch(A, st, s->jitg ? s->jitg->nfa : nullptr));
     if (!timed) HIPCHECK(hipEventRecord(s->ev1, st));
     timed = true;
@@ -1114,11 +1122,6 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   else if (opts->flags & CEP_SESSION_WAVE_NFA) wave = true;
   else if (env_wave) wave = env_wave[0] == '1';
   s->wave = P.general_ok && wave && wave_ok(P.dev);
-  // KCEP_NFA_GROUPED=1: four keys per wave, keys past GROUP_RUNS live runs re-run on whole waves
-  // (C4: 8.8 vs 8.5-8.9 ms -- the grouped kernel takes the light keys in 5.5 ms, the outgrown keys
-  // then need 2.7 ms more on whole waves, profiles/r03_ab_c4_grouped.jsonl); default: one key per wave
-  const char* env_grp = getenv("KCEP_NFA_GROUPED");
-  s->grouped = env_grp && env_grp[0] == '1';
   const char* env_jit = getenv("KCEP_JIT");
   s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
   if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels
@@ -1132,7 +1135,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 
 void cep_session_close(cep_session* s) {
   if (!s) return;
-  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->heavy, &s->dstage, &s->dl_ticket,
+  for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->wscratch, &s->dstage, &s->dl_ticket,
                   &s->h_topic, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
                   &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,

@@ -347,7 +347,6 @@ std::shared_ptr<const JitModule> build(const std::string& src, const char* const
       why = std::string("kernel not found: ") + kernels[i];
       return nullptr;
     }
-  if (src.find("#define GROUP_LANES 32\n") != std::string::npos) m->group_lanes = 32;
   c.mods[{dev, src}] = m;
   return m;
 }
@@ -390,34 +389,13 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // LDS arena words of the wave kernel's key workspace (KCEP_WAVE_ARENA, tuning only)
   const char* aenv = getenv("KCEP_WAVE_ARENA");
   if (aenv) o += "#define WAVE_ARENA " + std::to_string(std::min(8192, std::max(4, atoi(aenv)))) + "\n";
-  // ... of each key of the grouped wave kernel, and its lanes per key / live-run limit (tuning only)
-  if (const char* genv = getenv("KCEP_GROUP_ARENA"))
-    o += "#define GROUP_ARENA " + std::to_string(std::min(4096, std::max(4, atoi(genv)))) + "\n";
-  if (const char* genv = getenv("KCEP_GROUP_LANES")) {        // lanes per key of the grouped kernel: 16 or 32
-    const int gl = atoi(genv) >= 32 ? 32 : 16;
-    o += "#define GROUP_LANES " + std::to_string(gl) + "\n";
-  }
-  if (const char* genv = getenv("KCEP_GROUP_RUNS"))
-    o += "#define GROUP_RUNS " + std::to_string(std::max(1, atoi(genv))) + "\n";
-  // LDS words per lane of the wave kernel's private run lists / logs (KCEP_WAVE_PRIV, tuning only; 0: pool)
-  const char* penv = getenv("KCEP_WAVE_PRIV");
-  if (penv) {
-    const int pw = atoi(penv);
-    o += "#define WAVE_PRIV " + std::to_string(pw <= 0 ? 0 : std::min(64, std::max(12, (pw + 3) & ~3))) + "\n";
-  }
   const std::string agg = wave_stateful(P.dev) || P.has_seq ? "true" : "false";
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
        "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {
   kcep::nfa_kernel_body(A);
 }
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()" + std::to_string(wave_occ) + R"())) void kcep_nfa_wave(kcep::NfaArgs A) {
-  kcep::nfa_wave_body<)" + agg + R"(, 64>(A);
-}
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()" + std::to_string(wave_occ) + R"())) void kcep_nfa_wave16(kcep::NfaArgs A) {
-  kcep::nfa_wave_body<)" + agg + R"(, GROUP_LANES>(A);
-}
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()" + std::to_string(wave_occ) + R"())) void kcep_nfa_heavy(kcep::NfaArgs A) {
-  kcep::nfa_wave_heavy<)" + agg + R"(>(A);
+  kcep::nfa_wave_body<)" + agg + R"(>(A);
 }
 )";
   return o;
@@ -426,10 +404,9 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()
 std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why, bool phases) {
   const std::string src = jit_source_general(P, why, phases);
   if (src.empty()) return nullptr;
-  static const char* const names[] = {"kcep_nfa_kernel", "kcep_nfa_wave", "kcep_nfa_wave16", "kcep_nfa_heavy"};
-  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa, &JitModule::nfa_wave, &JitModule::nfa_wave16,
-                                                      &JitModule::nfa_heavy};
-  return build(src, names, slots, 4, why);
+  static const char* const names[] = {"kcep_nfa_kernel", "kcep_nfa_wave"};
+  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa, &JitModule::nfa_wave};
+  return build(src, names, slots, 2, why);
 }
 
 bool jit_check_general(const Program& P, std::string& why) {

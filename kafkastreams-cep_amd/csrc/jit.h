@@ -17,9 +17,6 @@ struct JitModule {
   hipFunction_t runs_write = nullptr;   // runs_dev.h runs_write_body<JitTab>
   hipFunction_t nfa = nullptr;          // nfa_dev.h nfa_kernel_body (general path)
   hipFunction_t nfa_wave = nullptr;     // nfa_wave.h nfa_wave_body, one key per wave (general path)
-  hipFunction_t nfa_wave16 = nullptr;   // nfa_wave.h nfa_wave_body, four keys per wave
-  hipFunction_t nfa_heavy = nullptr;    // nfa_wave.h nfa_wave_heavy: the grouped launch's outgrown keys
-  int group_lanes = 16;                 // lanes per key of nfa_wave16 (the source's GROUP_LANES)
   ~JitModule();
 };
 

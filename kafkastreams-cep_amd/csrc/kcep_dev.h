@@ -66,8 +66,11 @@ constexpr int RUNS_MAX_STATES = 8; // aggregate registers of one deterministic r
 // per key segment: live-run max, run evaluations, wall clock (100 MHz), then (profiling kernels; -1
 // otherwise) shader clocks in evaluate / predicates / buffer put+branch / removePattern /
 // matchConstruction / first_compatible / add_pred / version copies, and counts of first_compatible
-// calls / pred entries examined / digit-by-digit checks
-constexpr int NFA_PROFILE_W = 16;   // + reserved (0) / workspace words taken from the pool
+// calls / pred entries examined / digit-by-digit checks, reserved (0), the key's workspace words (wave
+// scratch + pool), then (profiling kernels) those words per allocation kind -- first workspace, match
+// output, heap, run queues, private lists, aggregates, other (nfa_dev.h AK_*) -- and the batch pool's
+// share of them (the rest came from the wave's recycled scratch region)
+constexpr int NFA_PROFILE_W = 24;
 
 struct DevStage {
   int32_t name, type, slot, nedges, nfolds;
@@ -152,8 +155,9 @@ struct NfaArgs {
   int32_t wave_agg;               // wave kernel: bit 0 the pattern folds / reads / copies aggregates (rounds
                                   // check for runs sharing a sequence), bit 1 it has SequenceMatchers
   int32_t last_attempt;           // 1: no pool regrowth follows -- an overflowing key reports CEP_E_RUN_CAPACITY
-  int32_t* heavy;                 // grouped wave kernel: segments that outgrew their group (nfa_wave.h) ...
-  int32_t* heavy_n;               // ... and their count (zeroed before the launch)
+  int32_t* seg_next;              // wave kernel: the next key segment a persistent wave takes (zeroed before)
+  int32_t* scratch;               // wave kernel: one recycled workspace region per workgroup (nfa_wave.h) ...
+  int64_t scratch_words;          // ... of this many words (0: none)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY
   unsigned long long* err_any;    // set when any key reports an exception (the host reads res_err only then)
 };

@@ -53,15 +53,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nf
 }
 
 // one key per wave, one queued run per lane (nfa_wave.h); AGG: patterns with aggregates or
-// SequenceMatchers.  GL = 64: every key on a whole wave; GL = GROUP_LANES: four keys per wave, the
-// keys that outgrow their group re-run on a whole wave by nfa_wave_heavy_kernel
-template <bool AGG, int GL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_kernel(NfaArgs A) {
-  nfa_wave_body<AGG, GL>(A);
-}
+// SequenceMatchers.  A persistent grid (nfa_wave_grid)
 template <bool AGG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_heavy_kernel(NfaArgs A) {
-  nfa_wave_heavy<AGG>(A);
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_kernel(NfaArgs A) {
+  nfa_wave_body<AGG>(A);
 }
 
 // ---- segments, scans, output compaction, carry commit ----
@@ -183,33 +178,31 @@ hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf) {
   return hipGetLastError();
 }
 
-// The wave kernels over A.nseg key segments: grouped (four keys per wave, then the outgrown keys on
-// whole waves; A.heavy_n zeroed by the caller) or one key per wave.  j: the pattern's compiled
-// kernels (null: the built-in interpreting ones).
-hipError_t nfa_wave_launch(const NfaArgs& A, bool grouped, hipStream_t st, const JitModule* j) {
-  if (A.nseg <= 0) return hipSuccess;
+// The workgroups (one wave each) the wave kernel's persistent grid should have: as many as the chip
+// holds at once (occupancy x compute units), at most one per segment.
+int64_t nfa_wave_grid(int64_t nseg, bool agg, const JitModule* j) {
+  int per_cu = 0, cus = 0, dev = 0;
+  hipError_t e = j ? hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, j->nfa_wave, 64, 0)
+                   : agg ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nfa_wave_kernel<true>, 64, 0)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, nfa_wave_kernel<false>, 64, 0);
+  if (e != hipSuccess || per_cu <= 0) per_cu = 12;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  const int64_t g = int64_t(per_cu) * cus;
+  return nseg < g ? nseg : g;
+}
+
+// The wave kernel over A.nseg key segments on `grid` persistent workgroups (A.seg_next zeroed by the
+// caller; A.scratch holds grid x A.scratch_words words).  j: the pattern's compiled kernel (null: the
+// built-in interpreting one).
+hipError_t nfa_wave_launch(const NfaArgs& A, int64_t grid, hipStream_t st, const JitModule* j) {
+  if (A.nseg <= 0 || grid <= 0) return hipSuccess;
   NfaArgs a = A;
   void* args[] = {&a};
-  const int NG = 64 / (j ? j->group_lanes : GROUP_LANES);
-  if (!grouped) {
-    if (j) return hipModuleLaunchKernel(j->nfa_wave, unsigned(A.nseg), 1, 1, 64, 1, 1, 0, st, args, nullptr);
-    if (A.wave_agg) hipLaunchKernelGGL((nfa_wave_kernel<true, 64>), dim3(unsigned(A.nseg)), dim3(64), 0, st, A);
-    else hipLaunchKernelGGL((nfa_wave_kernel<false, 64>), dim3(unsigned(A.nseg)), dim3(64), 0, st, A);
-    return hipGetLastError();
-  }
-  const unsigned grid = unsigned((A.nseg + NG - 1) / NG);
-  const unsigned hgrid = unsigned(A.nseg < 4096 ? A.nseg : 4096);   // persistent over the heavy list
-  if (j) {
-    hipError_t e = hipModuleLaunchKernel(j->nfa_wave16, grid, 1, 1, 64, 1, 1, 0, st, args, nullptr);
-    return e != hipSuccess ? e : hipModuleLaunchKernel(j->nfa_heavy, hgrid, 1, 1, 64, 1, 1, 0, st, args, nullptr);
-  }
-  if (A.wave_agg) {
-    hipLaunchKernelGGL((nfa_wave_kernel<true, GROUP_LANES>), dim3(grid), dim3(64), 0, st, A);
-    hipLaunchKernelGGL(nfa_wave_heavy_kernel<true>, dim3(hgrid), dim3(64), 0, st, A);
-  } else {
-    hipLaunchKernelGGL((nfa_wave_kernel<false, GROUP_LANES>), dim3(grid), dim3(64), 0, st, A);
-    hipLaunchKernelGGL(nfa_wave_heavy_kernel<false>, dim3(hgrid), dim3(64), 0, st, A);
-  }
+  if (j) return hipModuleLaunchKernel(j->nfa_wave, unsigned(grid), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+  if (A.wave_agg) hipLaunchKernelGGL(nfa_wave_kernel<true>, dim3(unsigned(grid)), dim3(64), 0, st, A);
+  else hipLaunchKernelGGL(nfa_wave_kernel<false>, dim3(unsigned(grid)), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 

@@ -49,6 +49,22 @@ __device__ __forceinline__ Run mk_run(int sid, int eps, int ver, int ev, int seq
 
 enum { ST_BEGIN_ = 0, ST_NORMAL_ = 1, ST_FINAL_ = 2 };
 
+// What a workspace allocation is for (profiling builds count the words per kind, cep_key_profile)
+enum : int { AK_WS = 0, AK_OUT, AK_HEAP, AK_QUEUE, AK_PRIV, AK_AGG, AK_OTHER, AK_N };
+
+// The wave kernel's allocator state of the key on the wave (LDS, nfa_wave.h): its words so far (the
+// per-key cap) and the wave's recycled scratch region.  A key's workspace dies with the key, so the
+// persistent wave hands the same region to every key it takes: the region's lines stay in the XCD's
+// L2 from one key to the next instead of a fresh stretch of the batch pool being dirtied (and
+// written back to HBM) per key.  Only what outlives the kernel -- the match output -- and what does
+// not fit the region come from the batch pool.
+struct KeyAlloc {
+  unsigned long long pool_words;   // every word the key took (scratch + pool): max_key_words
+  unsigned long long scr_top;      // scratch words handed out (may pass scr_cap: then the pool)
+  int32_t* scr;                    // the wave's region (nullptr: none)
+  int64_t scr_cap;
+};
+
 struct Lane {
   const NfaArgs* A;
   const DevProgram* P;
@@ -89,11 +105,12 @@ struct Lane {
   int32_t nph;                 // wave: run-counter increments of this lane's run (seq placeholders)
   int32_t wgrow;               // wave: the shared heap was too small (grow it and re-run the round)
   int32_t ov_own;              // wave: this evaluation wrote an aggregate of its run's own sequence
-  unsigned long long* wpool;   // wave: the key's pool words, in LDS (every lane allocates for the key)
+  KeyAlloc* wpool;             // wave: the key's allocator, in LDS (every lane allocates for the key)
 #ifdef KCEP_PHASES
   uint64_t ph[11];             // profiling kernels only: clocks in evaluate / predicates / buffer puts+branch /
                                // removePattern / matchConstruction / first_compatible / add_pred / versions,
                                // then counts: first_compatible calls / entries examined / digit-by-digit checks
+  uint64_t kw[AK_N + 1];       // profiling kernels only: words allocated per kind (AK_*), then those of the pool
 #endif
 };
 
@@ -120,25 +137,37 @@ __device__ __forceinline__ int32_t lds_add(int32_t* p, int32_t v) {
 __device__ __forceinline__ unsigned long long lds_add(unsigned long long* p, unsigned long long v) {
   return __hip_atomic_fetch_add((lds_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words) {
+// persist: the words must outlive the kernel (the match output): never from the wave's scratch
+__device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words, int kind, bool persist = false) {
   const int64_t w = (words + 3) & ~int64_t(3);
-  if (l.wpool) {                                   // wave mode: one counter for the key
-    const int64_t was = int64_t(lds_add(l.wpool, (unsigned long long)w));
+#ifdef KCEP_PHASES
+  l.kw[kind] += uint64_t(w);
+#endif
+  if (l.wpool) {                                   // wave mode: one allocator for the key
+    const int64_t was = int64_t(lds_add(&l.wpool->pool_words, (unsigned long long)w));
     if (l.A->max_key_words > 0 && was + w > l.A->max_key_words) { l.overflow = 1; l.cap_hit = 1; return nullptr; }
+    if (!persist && l.wpool->scr && w <= l.wpool->scr_cap) {
+      const int64_t at = int64_t(lds_add(&l.wpool->scr_top, (unsigned long long)w));
+      if (at <= l.wpool->scr_cap - w) { l.pool_words += w; return l.wpool->scr + at; }
+    }
   } else if (l.A->max_key_words > 0 && l.pool_words + w > l.A->max_key_words) {
     l.overflow = 1; l.cap_hit = 1; return nullptr;
   }
   const unsigned long long at = atomicAdd(l.A->pool_top, (unsigned long long)w);
   if (at + (unsigned long long)w > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
   l.pool_words += w;
+#ifdef KCEP_PHASES
+  l.kw[AK_N] += uint64_t(w);
+#endif
   return l.A->pool + at;
 }
 // re-allocate `*a` (cap words used up to `used`) at >= need words
-__device__ __forceinline__ bool regrow(Lane& l, int32_t*& a, int32_t& cap, int64_t used, int64_t need, int32_t fill = 0, bool zero = false) {
+__device__ __forceinline__ bool regrow(Lane& l, int32_t*& a, int32_t& cap, int64_t used, int64_t need, int kind,
+                                       int32_t fill = 0, bool zero = false) {
   int64_t nc = int64_t(cap) * 2;
   if (nc < need) nc = need;
   if (nc > (int64_t(1) << 30)) { l.overflow = 1; return false; }
-  int32_t* na = pool_alloc(l, nc);
+  int32_t* na = pool_alloc(l, nc, kind);
   if (!na) return false;
   for (int64_t i = 0; i < used; i++) na[i] = a[i];
   if (zero)
@@ -169,7 +198,7 @@ __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
     if (at + words > l.heapcap) { l.wgrow = 1; l.overflow = 1; return -1; }
     return at;
   }
-  if (l.heap_top + words > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + words))
+  if (l.heap_top + words > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + words, AK_HEAP))
     return -1;
   const int at = l.heap_top;
   l.heap_top += words;
@@ -265,7 +294,7 @@ enum : int32_t { WOP_PUT5 = 1, WOP_PUT3 = 2, WOP_BRANCH = 3, WOP_AGG = 4 };
 __device__ __forceinline__ void wlog(Lane& l, int kind, int sid, int psid, int ev, int pev, int ver) {
   if (l.log_n >= l.log_cap) {
     int32_t capw = l.log_cap * WL;
-    if (!regrow(l, l.log, capw, int64_t(l.log_n) * WL, int64_t(l.log_n + 1) * WL * 2)) return;
+    if (!regrow(l, l.log, capw, int64_t(l.log_n) * WL, int64_t(l.log_n + 1) * WL * 2, AK_PRIV)) return;
     l.log_cap = capw / WL;
   }
   int32_t* o = l.log + l.log_n * WL;
@@ -359,7 +388,7 @@ __device__ __forceinline__ int32_t* agg(Lane& l, int state, int seq) {
     int32_t cap = l.seqcap * ns * 3;
     int32_t* a = l.aggs;
     const int64_t need = (int64_t(seq) + 1) * ns * 3;
-    if (!regrow(l, a, cap, int64_t(l.seqcap) * ns * 3, need, 0, true)) return nullptr;
+    if (!regrow(l, a, cap, int64_t(l.seqcap) * ns * 3, need, AK_AGG, 0, true)) return nullptr;
     l.aggs = a;
     l.seqcap = cap / (ns * 3);
   }
@@ -453,7 +482,7 @@ __device__ __forceinline__ int32_t* seq_scratch(Lane& l) {
     const int at = heap_alloc(l, need);
     return at < 0 ? nullptr : l.heap + at;
   }
-  if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need))
+  if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need, AK_HEAP))
     return nullptr;
   return l.heap + l.heap_top;
 }
@@ -669,7 +698,7 @@ __device__ __forceinline__ int next_seq(Lane& l) {
 __device__ __forceinline__ bool push_run(Lane& l, int32_t*& q, int32_t& cap_runs, int32_t& len, const Run& x) {
   if (len >= cap_runs) {
     int32_t capw = cap_runs * 4;
-    if (!regrow(l, q, capw, int64_t(len) * 4, (int64_t(len) + 1) * 4)) return false;
+    if (!regrow(l, q, capw, int64_t(len) * 4, (int64_t(len) + 1) * 4, q == l.tq ? AK_PRIV : AK_QUEUE)) return false;
     cap_runs = capw / 4;
   }
   reinterpret_cast<int4*>(q)[len++] = make_int4(x.w0, x.ver, x.ev, x.seq);
@@ -850,11 +879,11 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
 __device__ __forceinline__ bool reserve_walk(Lane& l) {
   const int need_out = 3 + 3 * l.nev;
   if (l.out_top + need_out > l.outcap &&
-      !regrow(l, l.out, l.outcap, l.out_top, int64_t(l.out_top) + need_out))
+      !regrow(l, l.out, l.outcap, l.out_top, int64_t(l.out_top) + need_out, AK_OUT))
     return false;
   const int need_heap = 2 * l.nev + 2;
   if (l.heap_top + need_heap > l.heapcap &&
-      !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need_heap))
+      !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need_heap, AK_HEAP))
     return false;
   return true;
 }
@@ -957,7 +986,7 @@ __device__ __forceinline__ bool import_state(Lane& l, const int32_t* b) {
   const int32_t* ag = p;
   // heap: versions at [0, nver), predecessors after them
   const int PB = nver;
-  if (PB + PW * npred > l.heapcap && !regrow(l, l.heap, l.heapcap, 0, int64_t(PB) + PW * npred + 64)) return false;
+  if (PB + PW * npred > l.heapcap && !regrow(l, l.heap, l.heapcap, 0, int64_t(PB) + PW * npred + 64, AK_HEAP)) return false;
   for (int i = 0; i < nver; i++) l.heap[i] = vs[i];
   for (int i = 0; i < npred; i++) {
     int32_t* h = l.heap + PB + PW * i;
@@ -980,7 +1009,7 @@ __device__ __forceinline__ bool import_state(Lane& l, const int32_t* b) {
   }
   if (qlen > l.qa_cap) {
     int32_t capw = l.qa_cap * 4;
-    if (!regrow(l, l.qa, capw, 0, int64_t(qlen) * 4)) return false;
+    if (!regrow(l, l.qa, capw, 0, int64_t(qlen) * 4, AK_QUEUE)) return false;
     l.qa_cap = capw / 4;
   }
   for (int i = 0; i < 4 * qlen; i++) l.qa[i] = q[i];
@@ -1033,7 +1062,7 @@ __device__ __forceinline__ int64_t export_state(Lane& l) {
   {
     int32_t capw = l.tq_cap * 4;
     if (capw < l.nev) {
-      if (!regrow(l, l.tq, capw, 0, l.nev)) return -1;
+      if (!regrow(l, l.tq, capw, 0, l.nev, AK_OTHER)) return -1;
       l.tq_cap = capw / 4;
     }
     evmap = l.tq;
@@ -1050,7 +1079,7 @@ __device__ __forceinline__ int64_t export_state(Lane& l) {
   int32_t* seqmap = l.fq;                                           // qlen entries: new id of run i's seq
   if (l.fq_cap < l.qlen) {
     int32_t capw = l.fq_cap * 4;
-    if (!regrow(l, l.fq, capw, 0, int64_t(l.qlen) * 4)) return -1;
+    if (!regrow(l, l.fq, capw, 0, int64_t(l.qlen) * 4, AK_OTHER)) return -1;
     l.fq_cap = capw / 4;
     seqmap = l.fq;
   }
@@ -1153,18 +1182,22 @@ __device__ __forceinline__ int64_t export_state(Lane& l) {
 // false if the key has nothing to run (its result words are then final).
 // arena (wave kernel): LDS words for the key's hot workspace (hwm, nodes, queues, aggregates, heap);
 // used when they fit, the match output stays in the pool (the compaction reads it after the kernel).
-// Arrays that outgrow it are re-allocated in the pool like any other (generic pointers throughout).
+// Arrays that outgrow it are re-allocated like any other (generic pointers throughout): from the
+// wave's scratch region (ka, wave kernel) or the pool.
 __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, int32_t* arena = nullptr,
-                                         int64_t arena_words = 0) {
+                                         int64_t arena_words = 0, KeyAlloc* ka = nullptr) {
   l.A = &A;
   l.P = A.P;
   l.pool_words = 0;
+#ifdef KCEP_PHASES
+  for (int i = 0; i <= AK_N; i++) l.kw[i] = 0;
+#endif
   const auto& P = KCEP_PROG(l);
   l.seg0 = A.seg_start[seg];
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
   l.g = l.seg0;
   l.wave = 0; l.wtop = nullptr; l.log = nullptr; l.log_cap = 0; l.log_n = 0; l.nph = 0; l.wgrow = 0;
-  l.wpool = nullptr;
+  l.wpool = ka;
   l.cap_hit = 0;
   l.rec_out_top = 0;
   l.rec_nmatch = 0;
@@ -1197,12 +1230,12 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.heapcap = A.cap.heap_base + A.cap.heap_mult * l.nev;
   l.outcap = A.cap.out_base + A.cap.out_mult * l.L;
   const int64_t fixed = 3 * HWM_MAX + int64_t(NW) * ns * l.nev + 16 * int64_t(A.cap.q0) +
-                        int64_t(3) * nst * l.seqcap + l.heapcap + l.outcap;
-  const bool in_lds = arena && fixed - l.outcap <= arena_words;
-  l.arena_used = in_lds ? int32_t(fixed - l.outcap) : -1;
-  int32_t* p = in_lds ? arena : pool_alloc(l, fixed);
-  int32_t* out_at = in_lds && p ? pool_alloc(l, l.outcap) : nullptr;
-  if (!p || (in_lds && !out_at)) {
+                        int64_t(3) * nst * l.seqcap + l.heapcap;
+  const bool in_lds = arena && fixed <= arena_words;
+  l.arena_used = in_lds ? int32_t(fixed) : -1;
+  int32_t* p = in_lds ? arena : pool_alloc(l, fixed, AK_WS);
+  int32_t* out_at = p ? pool_alloc(l, l.outcap, AK_OUT, true) : nullptr;
+  if (!p || !out_at) {
     if (A.last_attempt || l.cap_hit) {                                 // handed back per key
       A.res_err[seg] = CEP_E_RUN_CAPACITY;
       A.res_err_rec[seg] = A.base + l.seg0;
@@ -1219,8 +1252,8 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.tq = p; p += 4 * A.cap.q0;
   l.fq = p; p += 4 * A.cap.q0;
   l.aggs = p; p += int64_t(3) * nst * l.seqcap;
-  l.heap = p; p += l.heapcap;
-  l.out = in_lds ? out_at : p;
+  l.heap = p;
+  l.out = out_at;
   l.heap_top = 0; l.out_top = 0;
   for (int64_t i = 0; i < int64_t(3) * nst * l.seqcap; i++) l.aggs[i] = 0;   // all states null
   if (blob) {
@@ -1291,8 +1324,13 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
 #else
     for (int i = 0; i < 11; i++) pr[3 + i] = -1;
 #endif
-    pr[14] = 0;                                                        // (no LDS workspace)
+    pr[14] = 0;                                                        // (reserved)
     pr[15] = l.pool_words;
+#ifdef KCEP_PHASES
+    for (int i = 0; i <= AK_N; i++) pr[16 + i] = int64_t(l.kw[i]);  // words per kind, then the pool's share
+#else
+    for (int i = 0; i <= AK_N; i++) pr[16 + i] = -1;
+#endif
   }
   if (l.overflow && (A.last_attempt || l.cap_hit)) {
     // over capacity: the key stops at this record and is handed back (CEP_E_RUN_CAPACITY); the

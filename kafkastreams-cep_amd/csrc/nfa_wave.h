@@ -22,9 +22,11 @@
 //   * matchConstruction after the last round: the final runs' buffer walks, 64 at a time, stepped
 //     event by event (wave_emit_matches).
 //
-// The key's workspace is the lane kernel's (nfa_dev.h): nodes, queues and heap in the pool, with
-// the heap allocated by an LDS atomic; a round that outgrows the heap is re-run after the wave has
-// doubled it.
+// The key's workspace is the lane kernel's (nfa_dev.h): nodes, queues and heap in the key's LDS arena
+// while they fit, then in the wave's recycled scratch region, then in the batch pool, with the heap
+// allocated by an LDS atomic; a round that outgrows the heap is re-run after the wave has doubled it.
+// The grid is persistent: each workgroup (one wave) takes key segments from a counter until none is
+// left, and hands its scratch region to every key it takes (nfa_dev.h KeyAlloc).
 #pragma once
 #include "nfa_dev.h"
 
@@ -40,21 +42,12 @@ constexpr int WAVE = 64;
 #endif
 #ifndef WAVE_PRIV
 #define WAVE_PRIV 16                       // LDS words per lane for its private run list + operation log
-#endif                                     // (KCEP_WAVE_PRIV A/B; 0 = in the pool)
-#ifndef GROUP_LANES
-#define GROUP_LANES 16                     // lanes per key of the grouped kernel (4 keys per wave)
-#endif
-#ifndef GROUP_ARENA
-#define GROUP_ARENA 1024                   // LDS words per key workspace of the grouped kernel (KCEP_GROUP_ARENA A/B)
-#endif
-#ifndef GROUP_RUNS
-#define GROUP_RUNS 32                      // a key of the grouped kernel with more live runs moves to a whole wave
 #endif
 
 // The lanes of one key: GL consecutive lanes of the wave (GL = 64: the whole wave, one key per
-// workgroup; GL = 16: four keys per wave).  Ballots, broadcasts and scans stay inside the group, so
-// the keys of one wave never exchange anything; their lanes merely share the instruction stream,
-// which is what a latency-bound key leaves idle.
+// workgroup).  Ballots, broadcasts and scans stay inside the group.  (A grouped build -- four keys per
+// wave, 16 lanes each, outgrown keys re-run on whole waves -- was measured slower in rounds 3 and 4,
+// DESIGN.md 4.4, and removed; the helpers keep the group width as a parameter.)
 template <int GL>
 struct Grp {
   int gl;                                  // lane within the group
@@ -83,9 +76,7 @@ struct Grp {
 };
 
 // A hand-off between lanes of the wave (the workgroup is one wave): a wavefront performs its
-// memory operations in program order, so only the compiler must not move them across it.  No
-// s_barrier, which the grouped kernel could not take anyway: its keys leave loops at different
-// times.
+// memory operations in program order, so only the compiler must not move them across it.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -97,7 +88,7 @@ struct WaveShared {
   int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm, *aggs;
   int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs, seqcap;
   int64_t nmatch;
-  unsigned long long pool_words;   // the key's pool words (every lane allocates for the key)
+  KeyAlloc ka;                     // the key's allocator: its words, the wave's scratch region
   int32_t err, overflow, cap_hit;
   int32_t* logp[GL];
   int32_t logn[GL], errc[GL];
@@ -131,7 +122,7 @@ __device__ __forceinline__ void lane_to_ws(W& w, const Lane& l) {
 // lds_ok: the array may move into the key's LDS arena (not the match output, read after the kernel)
 template <int GL>
 __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int32_t* a, int32_t& cap, int64_t used,
-                                                int64_t need, const Grp<GL>& g, bool lds_ok = true) {
+                                                int64_t need, const Grp<GL>& g, int kind, bool lds_ok = true) {
   int64_t nc = int64_t(cap) * 2;
   if (nc < need) nc = need;
   wave_sync();
@@ -140,7 +131,7 @@ __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int3
       w.grown = w.arena + w.arena_used;
       w.arena_used += int32_t((nc + 3) & ~int64_t(3));
     } else {
-      w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc);
+      w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc, kind, !lds_ok);
     }
     if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
   }
@@ -157,7 +148,7 @@ template <int GL>
 __device__ __forceinline__ bool wave_heap_reserve(Lane& l, WaveShared<GL>& w, int64_t need_top, const Grp<GL>& g) {
   if (need_top <= w.heapcap) return true;
   int32_t cap = w.heapcap;
-  int32_t* na = wave_regrow(l, w, w.heap, cap, w.heap_top, need_top, g);
+  int32_t* na = wave_regrow(l, w, w.heap, cap, w.heap_top, need_top, g, AK_HEAP);
   if (!na) return false;
   if (g.gl == 0) { w.heap = na; w.heapcap = cap; }
   wave_sync();
@@ -363,7 +354,7 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, co
     const int off = g.excl_scan(words, total);
     if (w.out_top + total > w.outcap) {
       int32_t cap = w.outcap;
-      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, g, false);
+      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, g, AK_OUT, false);
       if (!na) return false;
       if (lane == 0) { w.out = na; w.outcap = cap; }
       wave_sync();
@@ -405,7 +396,7 @@ __device__ __forceinline__ bool wave_apply_aggs(Lane& l, WaveShared<GL>& w, cons
   if (need >= w.seqcap) {
     int32_t capw = w.seqcap * ns * 3;
     const int64_t used = int64_t(capw);
-    int32_t* na = wave_regrow(l, w, w.aggs, capw, used, (int64_t(need) + 1) * ns * 3, g);
+    int32_t* na = wave_regrow(l, w, w.aggs, capw, used, (int64_t(need) + 1) * ns * 3, g, AK_AGG);
     if (!na) return false;
     for (int64_t i = used + g.gl; i < capw; i += GL) na[i] = 0;       // the new rows: every state null
     wave_sync();
@@ -458,35 +449,40 @@ __device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf
 // AGG: the pattern reads or writes aggregates / reads partial sequences (DevProgram, abi.cpp
 // wave_stateful): the round machinery for them (conflict checks, the sequential re-evaluation,
 // applying the logged aggregate writes) is compiled in only then.
-// One key (segment `seg`) on the GL lanes of group gp (w, s_arena, s_priv: the group's LDS).
-// Returns false when a grouped key (GL < 64) outgrew its group (more than GROUP_RUNS live runs):
-// nothing of it was committed and it is re-run on a whole wave (nfa_wave_heavy).
+// One key (segment `seg`) on the GL lanes of group gp (w, s_arena, s_priv: the group's LDS; scr: the
+// wave's scratch region of A.scratch_words words, or nullptr).
 template <bool AGG, int GL>
-__device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL>& gp, WaveShared<GL>& w,
-                                         int32_t* s_arena, int arena_words, int32_t*& s_priv) {
+__device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL>& gp, WaveShared<GL>& w,
+                                         int32_t* s_arena, int arena_words, int32_t* s_priv, int32_t* scr) {
   const int lane = gp.gl;
   Lane l;
   int ok = 1;
   if (lane == 0) {
-    ok = key_begin(l, A, seg, s_arena, arena_words) ? 1 : 0;
+    w.ka.pool_words = 0;
+    w.ka.scr_top = 0;
+    w.ka.scr = scr;
+    w.ka.scr_cap = scr ? A.scratch_words : 0;
+    ok = key_begin(l, A, seg, s_arena, arena_words, &w.ka) ? 1 : 0;
     if (ok) {
       lane_to_ws(w, l);
-      w.pool_words = l.pool_words;
       w.arena = s_arena;
       w.arena_cap = arena_words;
       w.arena_used = l.arena_used >= 0 ? (l.arena_used + 3) & ~3 : arena_words;
     }
   }
   ok = gp.bcast(ok);
-  if (!ok) return true;
+  if (!ok) return;
   wave_sync();
   if (lane != 0) {
     l.A = &A; l.P = A.P;
     l.seg0 = A.seg_start[seg];
     l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
     l.wave = 0; l.cap_hit = 0;
+#ifdef KCEP_PHASES
+    for (int i = 0; i <= AK_N; i++) l.kw[i] = 0;
+#endif
   }
-  l.wpool = &w.pool_words;
+  l.wpool = &w.ka;
   // every lane: the key's fixed shape (lane 0's key_begin set it)
   l.C = gp.bcast(l.C);
   l.nev = gp.bcast(l.nev);
@@ -501,19 +497,11 @@ __device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL
   ws_to_lane(l, w);
   // private run lists and operation logs: written by every evaluation and read back by the commit
   // and the queue placement.  A slice of LDS per lane (WAVE_PRIV words: 2 runs + 2 log entries, growing
-  // into the pool on demand).  Next to the full 2048-word arena it cost occupancy (C4 9.39 vs 8.34 ms,
-  // profiles/r03_ab_s5.jsonl); with the arena halved it is the faster build (7.78 vs 8.43 ms, r04)
+  // into the scratch region on demand).  Next to the full 2048-word arena it cost occupancy (C4 9.39 vs
+  // 8.34 ms, profiles/r03_ab_s5.jsonl); with the arena halved it is the faster build (7.78 vs 8.43 ms, r04)
   const int q0 = 2;
-#if WAVE_PRIV > 0
   constexpr int priv_stride = WAVE_PRIV, log0 = (WAVE_PRIV - 4 * q0) / WL;
   static_assert(WAVE_PRIV % 4 == 0 && log0 >= 1, "WAVE_PRIV: room for the run list and one log entry");
-#else
-  constexpr int priv_stride = 4 * (q0 + q0 * WL / 4 + 4), log0 = q0;
-  if (lane == 0) {
-    s_priv = pool_alloc(l, int64_t(GL) * priv_stride);
-    if (!s_priv) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
-  }
-#endif
   wave_sync();
   const auto& P = KCEP_PROG(l);
   const int ns = P.nslots;
@@ -535,7 +523,6 @@ __device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL
   }
   l.wtop = &w.heap_top;
   for (int i = 0; i < l.L && !w.err && !w.overflow; i++) {
-    if (GL < WAVE && w.qlen > GROUP_RUNS) return false;          // too many runs for the group: a whole wave
     const int r = l.C + i;
     const int64_t g = l.seg0 + i;
     l.r = r;
@@ -692,13 +679,13 @@ __device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL
       // room in the next queue and the final list
       if (qn + tq > w.qb_cap) {
         int32_t capw = w.qb_cap * 4;
-        int32_t* na = wave_regrow(l, w, w.qb, capw, int64_t(qn) * 4, int64_t(qn + tq) * 4, gp);
+        int32_t* na = wave_regrow(l, w, w.qb, capw, int64_t(qn) * 4, int64_t(qn + tq) * 4, gp, AK_QUEUE);
         if (!na) break;
         if (lane == 0) { w.qb = na; w.qb_cap = capw / 4; }
       }
       if (flen + tf > w.fq_cap) {
         int32_t capw = w.fq_cap * 4;
-        int32_t* na = wave_regrow(l, w, w.fq, capw, int64_t(flen) * 4, int64_t(flen + tf) * 4, gp);
+        int32_t* na = wave_regrow(l, w, w.fq, capw, int64_t(flen) * 4, int64_t(flen + tf) * 4, gp, AK_QUEUE);
         if (!na) break;
         if (lane == 0) { w.fq = na; w.fq_cap = capw / 4; }
       }
@@ -739,52 +726,37 @@ __device__ __forceinline__ bool wave_key(const NfaArgs& A, int seg, const Grp<GL
     live_max = w.qlen > live_max ? w.qlen : live_max;
   }
   wave_sync();
+#ifdef KCEP_PHASES
+  for (int i = 0; i <= AK_N; i++)                                // the key's allocations, summed over its lanes
+    for (int d = GL / 2; d > 0; d >>= 1) l.kw[i] += __shfl_xor(l.kw[i], d, GL);
+#endif
   if (lane == 0) {
     ws_to_lane(l, w);
-    l.pool_words = int64_t(w.pool_words);
+    l.pool_words = int64_t(w.ka.pool_words);
     l.wpool = nullptr;
     l.wave = 0;
     key_end(l, A, seg, err_rec, live_max, evals, t0);
   }
-  return true;
 }
 
-// The key segments of a batch, GL lanes per key: workgroup b takes segments b * (64 / GL) ... (one
-// per group).  GL < 64 (light keys): a key whose live runs outgrow its group is appended to the
-// heavy list (A.heavy / A.heavy_n) for nfa_wave_heavy.
-template <bool AGG, int GL>
-__device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
-  constexpr int NG = WAVE / GL;
-  constexpr int ARENA = (GL == WAVE ? WAVE_ARENA : GROUP_ARENA) & ~3;   // LDS words of each key's hot workspace
-  __shared__ WaveShared<GL> ws[NG];
-  __shared__ __attribute__((aligned(16))) int32_t s_arena[NG * ARENA + 4];
-  __shared__ int32_t* s_priv[NG];
-  const Grp<GL> gp{int(threadIdx.x) & (GL - 1), int(threadIdx.x) & ~(GL - 1)};
-  const int grp = int(threadIdx.x) / GL;
-  const int seg = int(blockIdx.x) * NG + grp;
-  if (seg >= A.nseg) return;
-#if WAVE_PRIV > 0
-  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
-  if (gp.gl == 0) s_priv[grp] = s_priv_lds + gp.base * WAVE_PRIV;
-#endif
-  if (!wave_key<AGG, GL>(A, seg, gp, ws[grp], s_arena + grp * ARENA, ARENA, s_priv[grp]) && gp.gl == 0)
-    A.heavy[atomicAdd(A.heavy_n, 1)] = seg;
-}
-
-// The heavy list of a grouped launch, one key per workgroup-wave (persistent over the list).
+// The key segments of a batch, one key per wave at a time.  The grid is persistent (the host sizes it
+// to the waves the chip holds at once, or the segment count if smaller): each workgroup takes the next
+// segment from A.seg_next until none is left, and every key it takes works in the workgroup's own
+// scratch region (recycled, so L2-resident, instead of a fresh stretch of the pool per key).
 template <bool AGG>
-__device__ __forceinline__ void nfa_wave_heavy(const NfaArgs& A) {
-  __shared__ WaveShared<WAVE> w;
-  __shared__ __attribute__((aligned(16))) int32_t s_arena[WAVE_ARENA];
-  __shared__ int32_t* s_priv;
-#if WAVE_PRIV > 0
-  __shared__ __attribute__((aligned(16))) int32_t s_priv_lds[WAVE * WAVE_PRIV];
-  s_priv = s_priv_lds;
-#endif
+__device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
+  constexpr int ARENA = WAVE_ARENA & ~3;   // LDS words of the key's hot workspace
+  __shared__ WaveShared<WAVE> ws;
+  __shared__ __attribute__((aligned(16))) int32_t s_arena[ARENA + 4];
+  __shared__ __attribute__((aligned(16))) int32_t s_priv[WAVE * WAVE_PRIV];
   const Grp<WAVE> gp{int(threadIdx.x), 0};
-  const int nh = *A.heavy_n;
-  for (int i = blockIdx.x; i < nh; i += gridDim.x) {
-    wave_key<AGG, WAVE>(A, A.heavy[i], gp, w, s_arena, WAVE_ARENA, s_priv);
+  int32_t* scr = A.scratch_words > 0 ? A.scratch + int64_t(blockIdx.x) * A.scratch_words : nullptr;
+  for (;;) {
+    int seg = 0;
+    if (gp.gl == 0) seg = atomicAdd(A.seg_next, 1);
+    seg = gp.bcast(seg);
+    if (seg >= A.nseg) break;                      // every wave of the grid reaches this
+    wave_key<AGG, WAVE>(A, seg, gp, ws, s_arena, ARENA, s_priv, scr);
     wave_sync();
   }
 }

@@ -322,12 +322,14 @@ class Session:
         return rec, code
 
     def key_profile(self):
-        """``profile=True`` sessions: int64 array [n_keys, 17] (cep_key_profile): key, live-run max, run
-        evaluations, wall clock (100 MHz), 8 phase clocks, 3 scan counters, 0, pool words."""
+        """``profile=True`` sessions: int64 array [n_keys, 25] (cep_key_profile): key, live-run max, run
+        evaluations, wall clock (100 MHz), 8 phase clocks, 3 scan counters, 0, workspace words, then the
+        words per allocation kind (first workspace, match output, heap, run queues, private lists,
+        aggregates, other) and the batch pool's share of them (kcep_dev.h NFA_PROFILE_W)."""
         import numpy as np
         n = C.c_int64()
         check(lib().cep_key_profile(self.h, None, 0, C.byref(n)))
-        out = np.zeros((n.value, 17), np.int64)
+        out = np.zeros((n.value, 25), np.int64)
         check(lib().cep_key_profile(self.h, out.ctypes.data, out.size, C.byref(n)))
         return out
 

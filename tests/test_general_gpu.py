@@ -270,13 +270,17 @@ def test_c4_heavy_keys(lane_nfa):
     assert s.live_run_hwm() > 128
 
 
-@pytest.mark.parametrize("grouped", ["0", "1"], ids=["whole_wave", "grouped"])
+@pytest.mark.parametrize("scratch", ["0", "64", None], ids=["pool_only", "scratch_64", "scratch_default"])
 @pytest.mark.parametrize("name,mk,vmax,gen", CASES, ids=[c[0] for c in CASES])
-def test_grouped_and_whole_wave_kernels(name, mk, vmax, gen, grouped, monkeypatch):
-    """The wave kernel with four keys per wave (16 lanes each) and with one key per wave: keys of
-    every size in one batch -- light ones stay in their group, keys past GROUP_RUNS live runs are
-    re-run from scratch on a whole wave (nfa_wave.h nfa_wave_heavy) -- against the oracle."""
-    monkeypatch.setenv("KCEP_NFA_GROUPED", grouped)
+def test_wave_scratch_regions(name, mk, vmax, gen, scratch, monkeypatch):
+    """The persistent wave kernel's workspace placement (nfa_wave.h, nfa_dev.h KeyAlloc): keys of every
+    size in one batch, each wave recycling its scratch region from key to key, with no region (every
+    array that leaves the LDS arena from the batch pool), a 64-word region (keys overflow into the
+    pool mid-key) and the default one -- against the oracle."""
+    if scratch is None:
+        monkeypatch.delenv("KCEP_WAVE_SCRATCH", raising=False)
+    else:
+        monkeypatch.setenv("KCEP_WAVE_SCRATCH", scratch)
     rng = np.random.default_rng(stable_seed(name, 977))
     if name in ("c4_any", "any_any"):       # skip-till-any: live runs multiply with every record (Q6)
         lens = np.concatenate([rng.integers(1, 6, 200), rng.integers(10, 15, 60)])

@@ -36,7 +36,7 @@ for i in o:
     print("  ", int(prof[i, 0]), int(live[i]), int(ev[i]), round(float(cyc[i]), 1))
 print("us per evaluation (top 100 keys):", float(cyc[o[:100]].sum() / max(1, ev[np.argsort(-cyc)[:100]].sum())))
 print("corr(evals, us)", float(np.corrcoef(ev, cyc)[0, 1]))
-ws = prof[:, 15] + prof[:, 16]
+ws = prof[:, 16]
 print("workspace words: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %d; heaviest key %d" %
       (ws.mean(), np.median(ws), np.percentile(ws, 90), np.percentile(ws, 99), ws.max(), ws[o[0]]))
 ph = prof[:, 4:15].astype(np.float64)
@@ -53,3 +53,11 @@ if (ph >= 0).all():
         print(nm, "scans", int(tot[8]), "entries/scan", round(float(tot[9] / max(1, tot[8])), 2),
               "digit checks/scan", round(float(tot[10] / max(1, tot[8])), 2),
               "clocks/scan", round(float(tot[5] / max(1, tot[8])), 1))
+kinds = ["first workspace", "match output", "heap", "run queues", "private lists", "aggregates", "other"]
+kw = prof[:, 17:25].astype(np.float64)
+if (kw >= 0).all():
+    tot = kw.sum(axis=0)
+    print("allocated words per kind over the batch (share):",
+          {k: f"{t:.3e} ({t / max(1.0, tot[:7].sum()):.3f})" for k, t in zip(kinds, tot[:7])})
+    print(f"  of which from the batch pool: {tot[7]:.3e} words ({tot[7] * 4 / 1e6:.1f} MB); "
+          f"from the waves' scratch regions: {tot[:7].sum() - tot[7]:.3e} words")
