@@ -91,6 +91,11 @@ typedef struct {
                               session keeps its state as of the batch start, and every other key of the
                               batch completes normally.  The host routes that key to the reference CPU path
                               (a key over capacity falls back per key). */
+  int64_t max_pool_bytes;  /* general path: device memory the session's NFA workspace pool may grow to when a
+                              batch overflows it (0 = a quarter of the device's HBM).  Past it the overflowing
+                              keys are handed back per key as above.  A pool grown for one batch is given back
+                              after that batch, so one heavy batch does not hold the device for the session's
+                              lifetime (several sessions share one GPU: one GpuCEPProcessor per stream task) */
 } cep_opts;
 
 /* Session flags */

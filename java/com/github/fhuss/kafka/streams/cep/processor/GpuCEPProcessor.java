@@ -20,8 +20,9 @@
  * the pool has grown toward free HBM) is NOT a task failure: the reference never runs out of capacity
  * (NFA.java:134-149 over unbounded stores).  Its state as of the batch start is evicted from the device,
  * rewritten in the reference's terms (cep_state_to_reference) and loaded into the three stores
- * (state.internal.ReferenceHandoff); the key then continues on the reference's own CEPProcessor -- this
- * batch's records replayed with their record context, every later record at once in process().
+ * (state.internal.ReferenceHandoff); the key then continues on the reference's own CEPProcessor, its
+ * records replayed with their own record context at each flush, in arrival order among the device's
+ * records, so the forwarded stream keeps the reference's per-record order across keys.
  *
  * Record context: matches are forwarded from flush(), so a downstream processor that reads
  * context().timestamp() / topic() / offset() sees the record or punctuation that triggered the flush,
@@ -184,10 +185,6 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     @Override
     public void process(K key, V value) {                               // CEPProcessor.process :134-150
         if (key == null || value == null) return;                        // :136-138
-        if (cpuKeys.contains(key)) {                                    // outgrew the device: the reference
-            reference.process(key, value);                              // (live record context, forwards now)
-            return;
-        }
         pending.add(new Event<>(key, value, context.timestamp(), context.topic(), context.partition(),
                                 context.offset()));
         if (pending.size() >= batchSize) flush();
@@ -207,7 +204,8 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     /** One match: arrival index of its completing record, device key id, traversal -- or, for a key on
      *  the reference, the Sequence its CEPProcessor forwarded. */
     private final class Match {
-        final int arrival, key;
+        int arrival;
+        final int key;
         final int[] names;
         final long[] records;
         final Sequence<K, V> sequence;
@@ -328,37 +326,84 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         }
     }
 
-    /** One cep_push_batch of the pending records, then forward in arrival order. */
+    /** One cep_push_batch of the pending records, the records of keys on the reference replayed on it,
+     *  then every match forwarded in arrival order of its completing record. */
     public void flush() {
         if (pending.isEmpty()) return;
-        List<Event<K, V>> recs = new ArrayList<>(pending);
+        final List<Event<K, V>> arrived = new ArrayList<>(pending);
         pending.clear();
-        int flags = 0;
-        if (path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN || path == CEP_PATH_RUNS) {
-            // the stencil / chain / runs paths carry each key's records (its last K-1, or those from
-            // its oldest open run on), not its NFA: the high-water-mark rule
-            // (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the batch
-            // is declared clean.  Every admitted record is processed and moves the mark (a record that
-            // throws fails the task anyway).
-            List<Event<K, V>> kept = new ArrayList<>(recs.size());
-            for (Event<K, V> e : recs) {
+        final boolean hostMark = path == CEP_PATH_STENCIL || path == CEP_PATH_CHAIN || path == CEP_PATH_RUNS;
+        List<Match> matches = new ArrayList<>();
+        List<long[]> errors = new ArrayList<>();                        // (arrival index, code)
+        cpuFailure = null;
+        cpuFailureAt = -1;
+        // the device's records (recs[j] arrived at at[j]); a key on the reference replays there
+        List<Event<K, V>> recs = new ArrayList<>(arrived.size());
+        List<Integer> at = new ArrayList<>(arrived.size());
+        boolean cpuFailed = false;
+        for (int i = 0; i < arrived.size(); i++) {
+            final Event<K, V> e = arrived.get(i);
+            if (cpuKeys.contains(e.key())) {                            // its CEPProcessor applies its own rules
+                if (!cpuFailed) cpuFailed = !replayOnReference(e, i, matches, errors);
+                continue;
+            }
+            if (hostMark) {
+                // the stencil / chain / runs paths carry each key's records (its last K-1, or those from
+                // its oldest open run on), not its NFA: the high-water-mark rule
+                // (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the batch
+                // is declared clean.  Every admitted record is processed and moves the mark (a record that
+                // throws fails the task anyway).
                 Map<Integer, Long> hw = highWater.computeIfAbsent(e.key(), k -> new HashMap<>());
                 int t = topicIds.computeIfAbsent(e.topic(), x -> topicIds.size());
                 Long mark = hw.get(t);
                 if (mark != null && e.offset() < mark) continue;
                 hw.put(t, e.offset() + 1);
-                kept.add(e);
             }
-            recs = kept;
-            flags = CEP_BATCH_OFFSETS_MONOTONE;
-            if (recs.isEmpty()) return;
+            recs.add(e);
+            at.add(i);
         }
+        if (!recs.isEmpty()) {
+            List<Match> dev = new ArrayList<>();
+            List<long[]> devErrors = new ArrayList<>();
+            handOffFailure = null;
+            handOffFailureAt = -1;
+            runDevice(recs, hostMark ? CEP_BATCH_OFFSETS_MONOTONE : 0, dev, devErrors);
+            for (Match m : dev) { m.arrival = at.get(m.arrival); matches.add(m); }   // into arrival order
+            for (long[] e : devErrors) errors.add(new long[] {at.get((int) e[0]), e[1]});
+            if (handOffFailure != null && (cpuFailure == null || at.get(handOffFailureAt) < cpuFailureAt)) {
+                cpuFailure = handOffFailure;
+                cpuFailureAt = at.get(handOffFailureAt);
+            }
+        }
+        // where the reference would have thrown: the first failing record in arrival order
+        long limit = Long.MAX_VALUE;
+        long code = 0;
+        for (long[] e : errors) if (e[0] < limit) { limit = e[0]; code = e[1]; }
+        // forward in arrival order of the completing record (stable within one record)
+        matches.sort((a, b) -> Integer.compare(a.arrival, b.arrival));
+        for (Match m : matches) {
+            if (m.arrival >= limit) break;
+            if (m.sequence != null) {                                   // a key on the reference
+                context.forward(arrived.get(m.arrival).key(), m.sequence);
+                continue;
+            }
+            Sequence.Builder<K, V> b = Sequence.newBuilder();
+            for (int i = 0; i < m.names.length; i++) b.add(names[m.names[i]], log.get(m.records[i]));
+            context.forward(arrived.get(m.arrival).key(), b.build(true));  // Sequence.java:210-223
+        }
+        if (limit != Long.MAX_VALUE) {
+            if (cpuFailure != null && cpuFailureAt == limit) throw cpuFailure;   // the reference's own exception
+            throw new IllegalStateException(queryName + ": reference exception " + code + " at record " + limit);
+        }
+        if (log.size() >= pruneAt) prune();
+    }
+
+    /** The device part of a flush over records recs (matches and errors index recs). */
+    private void runDevice(List<Event<K, V>> recs, int flags, List<Match> matches, List<long[]> errors) {
         final int n = recs.size();
         final int[] kid = keyIds(recs);
         int[] all = new int[n];
         for (int i = 0; i < n; i++) all[i] = i;
-        List<Match> matches = new ArrayList<>();
-        List<long[]> errors = new ArrayList<>();
         run(recs, kid, all, flags, matches, errors);
         // keys over the per-key workspace cap come back with their state as of the batch start: their
         // records are pushed again with the cap lifted, so that every record is processed (:134-150)
@@ -384,31 +429,29 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
                 handOff(recs, kid, whole, matches, errors);
             }
         }
-        // where the reference would have thrown: the first failing record in arrival order
-        long limit = Long.MAX_VALUE;
-        long code = 0;
-        for (long[] e : errors) if (e[0] < limit) { limit = e[0]; code = e[1]; }
-        // forward in arrival order of the completing record (stable within one record)
-        matches.sort((a, b) -> Integer.compare(a.arrival, b.arrival));
-        for (Match m : matches) {
-            if (m.arrival >= limit) break;
-            if (m.sequence != null) {                                   // a key on the reference
-                context.forward(recs.get(m.arrival).key(), m.sequence);
-                continue;
-            }
-            Sequence.Builder<K, V> b = Sequence.newBuilder();
-            for (int i = 0; i < m.names.length; i++) b.add(names[m.names[i]], log.get(m.records[i]));
-            context.forward(recs.get(m.arrival).key(), b.build(true));  // Sequence.java:210-223
-        }
-        if (limit != Long.MAX_VALUE) {
-            if (cpuFailure != null && cpuFailureAt == limit) throw cpuFailure;   // the reference's own exception
-            throw new IllegalStateException(queryName + ": reference exception " + code + " at record " + limit);
-        }
-        if (log.size() >= pruneAt) prune();
     }
 
-    private RuntimeException cpuFailure;
+    // the reference's own exception of this flush (arrival index), and the one a hand-off met (recs index)
+    private RuntimeException cpuFailure, handOffFailure;
     private long cpuFailureAt = -1;
+    private int handOffFailureAt = -1;
+
+    /** One record of a key on the reference CEPProcessor, with its own record context; its forwards are
+     *  captured as matches at arrival index i.  False if the reference threw (the task fails there). */
+    @SuppressWarnings("unchecked")
+    private boolean replayOnReference(Event<K, V> e, int i, List<Match> matches, List<long[]> errors) {
+        replay.begin(e, seq -> matches.add(new Match(i, (Sequence<K, V>) seq)));
+        try {
+            reference.process(e.key(), e.value());
+            return true;
+        } catch (RuntimeException ex) {                                 // the reference's exception, at this record
+            if (cpuFailure == null || i < cpuFailureAt) { cpuFailure = ex; cpuFailureAt = i; }
+            errors.add(new long[] {i, -1});
+            return false;
+        } finally {
+            replay.end();
+        }
+    }
 
     /** Keys that outgrew the whole device pool: their state (as of this batch's start) moves into the
      *  reference's stores and their records of this batch replay on the reference CEPProcessor. */
@@ -442,7 +485,7 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
                 try {
                     reference.process(e.key(), e.value());
                 } catch (RuntimeException ex) {                         // the reference's exception, at this record
-                    if (cpuFailure == null || i < cpuFailureAt) { cpuFailure = ex; cpuFailureAt = i; }
+                    if (handOffFailure == null || i < handOffFailureAt) { handOffFailure = ex; handOffFailureAt = i; }
                     errors.add(new long[] {i, -1});
                     break;
                 } finally {

@@ -13,9 +13,10 @@
  * Either way the returned stream carries KStream<K, Sequence<K, V>>, and the query's Ir matchers are
  * bound to the schema first (PatternIR.bind), so they also evaluate on the CPU route.
  *
- * Wiring: ComplexStreamsBuilder.stream(KStream) (cep/ComplexStreamsBuilder.java:100-102) returns
- *     new GpuCEPStreamImpl<>(stream, schema, GpuOptions.defaults())
- * instead of new CEPStreamImpl<>(stream); a stream built without a schema keeps every query on the CPU.
+ * Wiring: GpuComplexStreamsBuilder (java/com/github/fhuss/kafka/streams/cep/), the drop-in for the
+ * reference's ComplexStreamsBuilder (cep/ComplexStreamsBuilder.java:31-106), returns
+ *     new GpuCEPStreamImpl<>(stream, schema, options)
+ * from every stream(...) overload; a stream built without a schema keeps every query on the CPU.
  *
  * NOT BUILT in this repository (no JDK or Kafka jars in the image, SURVEY.md §8c).
  */

@@ -822,6 +822,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 3 * D.nstates;
   int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
   s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
+  const int64_t pool_base = s->pool_words;         // what the batch starts with (kept for the next batch)
   A.cap = cap;
   A.carry = s->carry ? 1 : 0;
   A.max_keys = int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX));
@@ -859,6 +860,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     }
   }
   bool timed = false;
+  bool grew = false;                               // the pool was regrown for this batch: given back after it
   bool pool_at_limit = false;                      // the pool cannot grow further: overflowing keys are handed back
   int64_t tots[2] = {0, 0};                        // matches, entries of the batch
   for (int attempt = 0;; attempt++) {
@@ -902,13 +904,15 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       return fail(CEP_E_RUN_CAPACITY, "the NFA workspace pool cannot grow");
     if (attempt >= kMaxRetry && fl[1]) return fail(CEP_E_RUN_CAPACITY, "the carried-state pool cannot grow");
     if (fl[0]) {                                   // workspace pool exhausted: twice the pool, same inputs,
-      s->pool.release();                           // but no more than the device's free HBM allows (keeping
-      size_t free_b = 0, total_b = 0;              // 1/16 of it): only then is a key handed back per key
-      HIPCHECK(hipMemGetInfo(&free_b, &total_b));
-      const int64_t room = int64_t(free_b / 4) - int64_t(free_b / 64);
+      s->pool.release();                           // within the session's budget (cep_opts.max_pool_bytes,
+      size_t free_b = 0, total_b = 0;              // default a quarter of the HBM) and the free HBM (keeping
+      HIPCHECK(hipMemGetInfo(&free_b, &total_b));  // 1/16 of it): past that a key is handed back per key
+      const int64_t budget = (s->opts.max_pool_bytes > 0 ? s->opts.max_pool_bytes : int64_t(total_b / 4)) / 4;
+      const int64_t room = std::min<int64_t>(int64_t(free_b / 4) - int64_t(free_b / 64), budget);
       const int64_t want = std::min<int64_t>(s->pool_words * 2, room);
       if (want <= s->pool_words) pool_at_limit = true;
       else s->pool_words = want;
+      grew = true;
     }
     if (fl[1]) {                                   // carry pool exhausted: compact into a larger one
       if ((rc = carry_gc(s, 2 * s->cpool_words, st))) return rc;
@@ -931,6 +935,11 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     s->base += n;
   }
   HIPCHECK(hipEventRecord(s->eb1, st));
+  if (grew) {                                      // one heavy batch does not keep the device's memory: the
+    HIPCHECK(hipStreamSynchronize(st));            // compaction has read the matches out of the pool
+    s->pool.release();
+    s->pool_words = pool_base;
+  }
   // the reference fails the task at its first exception: report the earliest failing record
   if (!s->g_any_err) {                             // no key raised: nothing to read back
     if (s->carry && s->cpool_used > s->cpool_words / 4 * 3) {
@@ -1969,9 +1978,9 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
   const int nver = b[CB_NVER], nseq = b[CB_NSEQ], ncols = b[CB_NCOLS], nst = b[CB_NSTATES];
   if (nhwm < 0 || qlen < 0 || nev < 0 || nnode < 0 || npred < 0 || nver < 0 || nseq < 0 || ncols < 0 || nst < 0)
     return fail(CEP_E_ARG, "bad state blob");
-  const int evw = 8 + 2 * ncols;
-  const int64_t total = int64_t(CB_HDR) + 3 * nhwm + 4 * qlen + int64_t(evw) * nev + 4 * nnode + 4 * npred + nver +
-                        int64_t(3) * nst * nseq;
+  const int64_t evw = 8 + 2 * int64_t(ncols);
+  const int64_t total = int64_t(CB_HDR) + 3 * int64_t(nhwm) + 4 * int64_t(qlen) + evw * nev + 4 * int64_t(nnode) +
+                        4 * int64_t(npred) + nver + int64_t(3) * nst * nseq;
   if (ncols != int(P.coltypes.size()) || nst != P.dev.nstates || total != w) return fail(CEP_E_ARG, "state blob does not match the pattern");
   // buffer-node slot -> (stage name, stage type), as lower_general numbers them (Matched.java:31-35)
   std::vector<std::pair<int, int>> slot(size_t(P.dev.nslots), {0, 0});
@@ -2012,6 +2021,7 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
     const int32_t w0 = q[4 * r];
     const int sid = w0 & 0xFF, eps = (w0 >> 8) & 0xFF;
     if (sid >= int(P.stages.size()) || (eps != 0xFF && eps >= int(P.stages.size()))) return fail(CEP_E_ARG, "bad run in state blob");
+    if (q[4 * r + 2] < -1 || q[4 * r + 2] >= nev) return fail(CEP_E_ARG, "bad run event in state blob");
     i32(sid);
     i32(eps == 0xFF ? -1 : eps);
     i32(((w0 >> 16) & 1) | (((w0 >> 17) & 1) << 1));
@@ -2024,6 +2034,7 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
   for (int i = 0; i < nnode; i++) {
     const int32_t* x = nd + 4 * i;
     if (x[0] < 0 || x[0] >= P.dev.nslots) return fail(CEP_E_ARG, "bad node in state blob");
+    if (x[1] < 0 || x[1] >= nev) return fail(CEP_E_ARG, "bad node event in state blob");
     str(P.names[size_t(slot[size_t(x[0])].first)]);
     i32(slot[size_t(x[0])].second);
     i32(x[1]);
@@ -2039,6 +2050,7 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
       if (!version(y[0])) return fail(CEP_E_ARG, "bad version in state blob");
       const bool has = y[1] >= 0;
       if (y[1] >= P.dev.nslots) return fail(CEP_E_ARG, "bad predecessor in state blob");
+      if (has && (y[2] < 0 || y[2] >= nev)) return fail(CEP_E_ARG, "bad predecessor event in state blob");
       i32(has ? 1 : 0);
       str(has ? P.names[size_t(slot[size_t(y[1])].first)] : std::string());
       i32(has ? slot[size_t(y[1])].second : 0);
@@ -2046,7 +2058,10 @@ int cep_state_to_reference(const cep_pattern* p, const void* blob, size_t len, v
     }
   }
   int32_t nagg = 0;
-  for (int64_t i = 0; i < int64_t(nst) * nseq; i++) nagg += ag[3 * i] != 0;
+  for (int64_t i = 0; i < int64_t(nst) * nseq; i++) {
+    if (ag[3 * i] < 0 || ag[3 * i] > 3) return fail(CEP_E_ARG, "bad aggregate type in state blob");   // 1 int, 2 long, 3 double
+    nagg += ag[3 * i] != 0;
+  }
   i32(nagg);
   for (int sq = 0; sq < nseq; sq++)
     for (int st = 0; st < nst; st++) {

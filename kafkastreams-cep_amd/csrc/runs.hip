@@ -44,7 +44,9 @@ __global__ __launch_bounds__(RT) void runs_write(WriteArgs W) { runs_write_body(
 
 // completed runs in start order, key (end << 31 | start): one workgroup per runs_sim chunk, placed at
 // the exclusive scan of the chunks' counts (pre), each thread's items contiguous so that a block scan
-// of the per-thread counts ranks them
+// of the per-thread counts ranks them.  256 threads x up to 4 items: the chunk is a power of two of at
+// most 1024 records (runs_compact_launch checks it)
+static_assert(RUNS_CHUNK <= 1024 && (RUNS_CHUNK & (RUNS_CHUNK - 1)) == 0, "runs_compact covers chunks of <= 4 x 256");
 __global__ __launch_bounds__(256) void runs_compact(const int32_t* __restrict__ end_of, int64_t n, int chunk,
                                                     const int64_t* __restrict__ pre, unsigned long long* __restrict__ out) {
   __shared__ int32_t s_w[4];
@@ -400,9 +402,8 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
                                hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
-  if (chunk > RUNS_CHUNK || chunk < 64) return hipErrorInvalidValue;
-  static const bool one_block = [] { const char* e = getenv("KCEP_RUNS_CHUNKSCAN"); return !(e && e[0] == '0'); }();
-  if (one_block && nw <= (int64_t(1) << 16)) {
+  if (chunk > RUNS_CHUNK || chunk < 64 || (chunk & (chunk - 1))) return hipErrorInvalidValue;
+  if (nw <= (int64_t(1) << 16)) {
     hipLaunchKernelGGL(runs_chunk_scan, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
   } else {
     hipError_t e = exclusive_scan(stat, nw, pre, tot_cnt, scan_tmp, st);

@@ -245,16 +245,18 @@ __global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __r
           last = row[s];
         }
       const int32_t kk = key[last];
-      const HaloHdr& h = C.hdr[kk];
-      const int old = halo_old(h, C.stamp);
-      const int64_t* hp = C.pos + (2 * int64_t(kk) + old) * C.km1;
+      // a key id outside [0, max_keys) (error flag bit 0, the host fails the batch): no halo lookup
+      const bool kok = kk >= 0 && kk < C.max_keys;
+      const HaloHdr* h = kok ? C.hdr + kk : nullptr;
+      const int old = kok ? halo_old(*h, C.stamp) : 0;
+      const int64_t* hp = kok ? C.pos + (2 * int64_t(kk) + old) * C.km1 : nullptr;
       const bool host = i < host_cap;
       int64_t* p = host ? hpos + i * k : dpos + i * k;
 #pragma unroll
       for (int s = 0; s < STENCIL_MAX_K; s++)
         if (s < k) {
           const int32_t r = row[s];
-          p[s] = r >= 0 ? C.base + r : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
+          p[s] = r >= 0 ? C.base + r : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
         }
       if (host) hkey[i] = kk;
       else dkey[i] = kk;
@@ -411,14 +413,15 @@ __global__ __launch_bounds__(256) void stencil_deliver(const int32_t* __restrict
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nm; i += int64_t(gridDim.x) * blockDim.x) {
     const int32_t last = out[i * k + k - 1];
     const int32_t kk = key[last];
-    const HaloHdr& h = C.hdr[kk];
-    const int old = halo_old(h, C.stamp);
-    const int64_t* hp = C.pos + (2 * int64_t(kk) + old) * C.km1;
+    const bool kok = kk >= 0 && kk < C.max_keys;   // else error flag bit 0: the host fails the batch
+    const HaloHdr* h = kok ? C.hdr + kk : nullptr;
+    const int old = kok ? halo_old(*h, C.stamp) : 0;
+    const int64_t* hp = kok ? C.pos + (2 * int64_t(kk) + old) * C.km1 : nullptr;
     const bool host = i < host_cap;
     int64_t* p = host ? hpos + i * k : dpos + i * k;
     for (int s = 0; s < k; s++) {
       const int32_t r = out[i * k + s];
-      p[s] = r >= 0 ? C.base + r : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
+      p[s] = r >= 0 ? C.base + r : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
     }
     if (host) hkey[i] = kk;
     else dkey[i] = kk;

@@ -49,7 +49,7 @@ class PatternInfo(C.Structure):
 class Opts(C.Structure):
     _fields_ = [("device", C.c_int32), ("mode", C.c_int32), ("force_path", C.c_int32), ("flags", C.c_int32),
                 ("max_events", C.c_int64), ("max_keys", C.c_int64), ("arena_scale", C.c_double),
-                ("max_key_words", C.c_int64)]
+                ("max_key_words", C.c_int64), ("max_pool_bytes", C.c_int64)]
 
 
 class Batch(C.Structure):
@@ -227,20 +227,22 @@ class Session:
     """One ``cep_session`` (one stream task's processor on one GPU)."""
 
     def __init__(self, pattern: CompiledPattern, max_events: int, mode=MODE_PROCESSOR, device=0, force_path=0,
-                 carry=False, max_keys=0, interpret=False, profile=False, max_key_words=0, lane_nfa=None):
+                 carry=False, max_keys=0, interpret=False, profile=False, max_key_words=0, lane_nfa=None,
+                 max_pool_bytes=0):
         """``carry=True``: every key's NFA state continues across batches (CEP_SESSION_CARRY);
         key ids must then be dense in [0, max_keys) and record positions are stream positions.
         ``interpret=True``: the built-in interpreting kernels instead of kernels compiled for the
         pattern (CEP_SESSION_INTERPRET); ``self.jit`` says which run.  ``max_key_words``: the
         general path's per-key workspace cap -- a key over it is handed back per key
-        (``batch_errors`` lists it with RunCapacity), every other key completes."""
+        (``batch_errors`` lists it with RunCapacity), every other key completes.  ``max_pool_bytes``:
+        how far the general path's workspace pool may grow for a batch (0: a quarter of the HBM)."""
         self.pattern = pattern
         self.h = C.c_void_p()
         # lane_nfa: None = the library's choice, True = one key per lane, False = one key per wave
         flags = ((SESSION_CARRY if carry else 0) | (SESSION_INTERPRET if interpret else 0) |
                  (SESSION_PROFILE if profile else 0) | (SESSION_LANE_NFA if lane_nfa else 0) |
                  (SESSION_WAVE_NFA if lane_nfa is False else 0))
-        o = Opts(device, mode, force_path, flags, max_events, max_keys, 0.0, max_key_words)
+        o = Opts(device, mode, force_path, flags, max_events, max_keys, 0.0, max_key_words, max_pool_bytes)
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)
         self.jit = bool(lib().cep_session_jit(self.h))

@@ -298,21 +298,38 @@ class JavaTwin:
     def flush(self):
         if not self.pending:
             return
-        recs, self.pending = self.pending, []
-        flags = 0
-        if self.path in (CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS):
-            kept = []
-            for r in recs:
+        arrived, self.pending = self.pending, []
+        host_mark = self.path in (CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS)
+        recs, at = [], []                                   # the device's records and their arrival indices
+        for i, r in enumerate(arrived):                     # (keys on the reference: the Java's hand-off only)
+            if host_mark:
                 hw = self.high_water.setdefault(r[0], {})
                 t = self._topic(r[2])
                 if t in hw and r[4] < hw[t]:
                     continue
                 hw[t] = r[4] + 1
-                kept.append(r)
-            recs = kept
-            flags = CEP_BATCH_OFFSETS_MONOTONE
-            if not recs:
-                return
+            recs.append(r)
+            at.append(i)
+        matches, errors = [], []
+        if recs:
+            m, e = self._run_device(recs, CEP_BATCH_OFFSETS_MONOTONE if host_mark else 0)
+            matches = [(at[a],) + tuple(x) for a, *x in m]
+            errors = [(at[a], c) for a, c in e]
+        limit = min(errors)[0] if errors else None
+        matches.sort(key=lambda m: m[0])
+        for a, _, en, er in matches:
+            if limit is not None and a >= limit:
+                break
+            groups = {}
+            for nm, pos in zip(en, er):                     # Sequence.Builder.add, then build(true)
+                groups.setdefault(self.names[nm], []).append(self.log[int(pos)][4])
+            self.forwarded.append((arrived[a][0], [(s, sorted(v)) for s, v in reversed(list(groups.items()))]))
+        if errors:
+            raise RuntimeError(f"reference exception {min(errors)[1]} at record {limit}")
+        if len(self.log) >= self.prune_at:
+            self._prune()
+
+    def _run_device(self, recs, flags):
         kid = self._key_ids(recs)
         allidx = list(range(len(recs)))
         matches, errors = self._run(recs, kid, allidx, flags)
@@ -330,19 +347,7 @@ class JavaTwin:
             assert not any(c == CEP_E_RUN_CAPACITY for _, c in e2), "a key outgrew the whole device pool"
             matches += m2
             errors += e2
-        limit = min(errors)[0] if errors else None
-        matches.sort(key=lambda m: m[0])
-        for a, _, en, er in matches:
-            if limit is not None and a >= limit:
-                break
-            groups = {}
-            for nm, pos in zip(en, er):                     # Sequence.Builder.add, then build(true)
-                groups.setdefault(self.names[nm], []).append(self.log[int(pos)][4])
-            self.forwarded.append((recs[a][0], [(s, sorted(v)) for s, v in reversed(list(groups.items()))]))
-        if errors:
-            raise RuntimeError(f"reference exception {min(errors)[1]} at record {limit}")
-        if len(self.log) >= self.prune_at:
-            self._prune()
+        return matches, errors
 
     def _prune(self):
         state = self.j.cepStateExport(self.session, 0, 2 ** 31 - 1)

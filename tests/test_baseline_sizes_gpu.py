@@ -47,12 +47,14 @@ def test_full_size_checksum(name):
     assert gm == om and gcs == ocs and gm > 0
 
 
-@pytest.mark.parametrize("name", ["c2", "c5"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
 def test_full_size_ordered_csr(name):
     """Element by element, not only the order-independent checksum: every match's emitting record, key
     and traversal (stage name, record), in the CSR's order -- key order of the grouped batch, per key
     the reference's emission order (CEPProcessor.java:148, SharedVersionedBufferStoreImpl.peek) -- at
-    the full C2 / C5 sizes, against the oracle's run of the same records."""
+    the full sizes of every config, against the oracle's run of the same records.  C3 exercises the runs
+    path's ordering (runs_order's windowed rank in LDS, runs.hip), C4 the wave kernel's queue-order
+    placement by prefix scans (nfa_wave.h) and its matchConstruction walks."""
     key, val, ts, pat, path = _cfg(name)
     n = key.numel()
     ir = pat.to_ir(I32)
@@ -66,7 +68,7 @@ def test_full_size_ordered_csr(name):
     del key, val, ts
     b = O.BatchArrays(hk, [hv], [1], offset=ht if name == "c2" else None, ts=ht)
     want = O.baseline_csr(O.OraclePattern(ir), b, O.MODE_PROCESSOR, min(THREADS, os.cpu_count() or 1))
-    assert len(want["match_record"]) > 1_000_000
+    assert len(want["match_record"]) > {"c2": 1_000_000, "c3": 1_000_000, "c4": 100_000, "c5": 1_000_000}[name]
     for f in ("match_record", "match_key", "ent_off", "ent_name", "ent_record"):
         assert got[f].shape == want[f].shape, f
         bad = np.flatnonzero(got[f] != want[f])

@@ -193,6 +193,35 @@ def test_key_id_out_of_range_is_rejected():
     assert e.value.code == 11
 
 
+@pytest.mark.parametrize("mk", [synth.c2_pattern, PL.c5_optional], ids=["stencil", "chain"])
+@pytest.mark.parametrize("mem", ["host", "device"])
+def test_delivered_batch_with_key_id_out_of_range(mk, mem):
+    """CEP_BATCH_DELIVER on a stencil / chain carry session: the delivery kernels run in the same
+    stream as the count kernel, before the host sees its error flags, so a match of a key id outside
+    [0, max_keys) must not make them read a halo header out of bounds.  The batch fails
+    with CEP_E_ARG and the session keeps working."""
+    ir = mk().to_ir(PL.I32)
+    s = N.Session(N.CompiledPattern(ir), 64, carry=True, max_keys=4)
+    assert s.path in (N.PATH_STENCIL, N.PATH_CHAIN)
+    vals = [0, 1, 2] if mk is synth.c2_pattern else [12, 5, 33]
+    key = np.array([1, 1, 1, 1 << 20, 1 << 20, 1 << 20], np.int32)
+    val = np.array(vals + vals, np.int32)
+    if mem == "device":
+        import torch
+        dk, dv = torch.from_numpy(key).cuda(), torch.from_numpy(val).cuda()
+        torch.cuda.synchronize()
+        push = lambda: s.push(len(key), dk.data_ptr(), [dv.data_ptr()], mem=N.MEM_DEVICE,
+                              flags=N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER)
+    else:
+        push = lambda: s.push(len(key), key, [val], flags=N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER)
+    with pytest.raises(N.CepError) as e:
+        push()
+        s.collect()
+    assert e.value.code == 11
+    s.push(3, key[:3], [val[:3]], flags=N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER)   # the session still works
+    assert len(s.collect()["match_record"]) == 1
+
+
 def test_interleaved_carry_batch_is_rejected():
     """A carry batch must hold each key in one contiguous segment (kcep.h batch contract): a key
     in two segments would load its carried state twice and lose one segment's update, so the

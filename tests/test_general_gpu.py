@@ -293,3 +293,41 @@ def test_wave_scratch_regions(name, mk, vmax, gen, scratch, monkeypatch):
     want, got, oerr, gerr = run_both(ir, O.MODE_PROCESSOR, key, [val], [1], lane_nfa=False)
     assert gerr == oerr
     assert got == want and len(want) > 0
+
+
+def test_pool_regrowth_is_bounded_and_given_back(monkeypatch):
+    """The general path's workspace pool: a batch that overflows it is re-run on a larger
+    pool, and the pool goes back to its usual size after the batch, so one heavy batch does not hold
+    the device for the session's lifetime; with a budget (cep_opts.max_pool_bytes) the pool stops
+    growing there and the keys still out of room are handed back per key (CEP_E_RUN_CAPACITY) while
+    every other key completes as the oracle's."""
+    import torch
+    from kcep import synth
+    monkeypatch.setenv("KCEP_WAVE_SCRATCH", "0")          # every workspace array from the pool
+    key, val, _ = synth.c4_stream_np(400, L=16)
+    ir = synth.c4_pattern().to_ir(PL.I32)
+    want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
+    s = N.Session(N.CompiledPattern(ir), 2 * len(key), force_path=N.PATH_GENERAL, lane_nfa=False)
+    s.push(len(key), key, [val])                           # ~2.1 M pool words: over the first estimate
+    assert product_matches(s, s.collect()) == want
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    heavy = np.concatenate([key, key + 400])               # twice the keys: the pool overflows
+    hval = np.concatenate([val, val])
+    s.push(len(heavy), heavy, [hval])
+    got = product_matches(s, s.collect())
+    torch.cuda.synchronize()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert len(got) == 2 * len(want)
+    assert free1 >= free0 - (64 << 20)                     # the regrown pool was given back
+    # a second session on the same device, with a pool budget the batch cannot fit in
+    s2 = N.Session(N.CompiledPattern(ir), len(heavy), force_path=N.PATH_GENERAL, lane_nfa=False,
+                   max_pool_bytes=12 << 20)              # ~4.1 M words needed, 3 M allowed
+    s2.push(len(heavy), heavy, [hval])
+    out = s2.collect()
+    rec, code = s2.batch_errors()
+    assert len(code) > 0 and set(int(c) for c in code) == {9}
+    failed = set(int(heavy[r]) for r in rec)
+    mine = [m for m in product_matches(s2, out) if m[1] not in failed]
+    wantk = [m for m in oracle_matches(ir, heavy, [hval], [1], O.MODE_PROCESSOR) if m[1] not in failed]
+    assert mine == wantk and len(mine) > 0

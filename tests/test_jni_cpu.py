@@ -76,6 +76,7 @@ def _twin_body(src, name):
     (r"private int\[\] keyIds\(", "_key_ids"),
     (r"private void spill\(", "_spill"),
     (r"public void flush\(\)", "flush"),
+    (r"private void runDevice\(", "_run_device"),
     (r"private void prune\(\)", "_prune"),
 ])
 def test_java_methods_call_the_natives_the_twin_calls(java_sig, twin):

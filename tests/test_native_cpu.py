@@ -186,3 +186,20 @@ def test_state_to_reference_host_only():
         cp.state_to_reference(_kcst(bad))
     with pytest.raises(N.CepError):
         cp.state_to_reference(_kcst(words)[:-4])      # truncated
+    bad = list(words)
+    bad[CB_HDR + 3 + 2] = 0                           # the run's last event: there are no events
+    with pytest.raises(N.CepError):
+        cp.state_to_reference(_kcst(bad))
+    # a pattern with aggregates: one run sequence, its two states (sum, count) as (type, lo, hi)
+    cs = N.CompiledPattern(synth.c3_pattern().to_ir(Schema([("value", "i32")])))
+    begin = [i for i, st in enumerate(cs.stages()) if st[1] == 0][0]
+    hdr = [0, 5, 0, 0, 1, 0, 0, 0, 2, 1, 1, 2]
+    aggs = [1, 10, 0, 1, 2, 0]                        # sum = 10 (int), count = 2 (int)
+    words = hdr + [begin | (0xFF << 8), 0, -1, 0] + [1, 1] + aggs
+    words[0] = len(words)
+    assert cs.state_to_reference(_kcst(words))
+    for t in (4, -1):                                 # a boxed type outside int / long / double
+        bad = list(words)
+        bad[-6] = t
+        with pytest.raises(N.CepError):
+            cs.state_to_reference(_kcst(bad))

@@ -247,3 +247,49 @@ def test_irb_matches_encode_for_a_hand_built_query():
     assert bytes(buf) == want
     pat = N.CompiledPattern(want)
     assert L.cep_pattern_check(pat.h, 1) == 0
+
+
+# ComplexStreamsBuilder's public surface (core/src/main/java/com/github/fhuss/kafka/streams/cep/
+# ComplexStreamsBuilder.java:31-106): constructors, the stream(...) overloads and build()
+REFERENCE_BUILDER = {
+    "ctors": [[], ["StreamsBuilder"]],
+    "stream": [["Collection<String>", "Consumed<K, V>"], ["String", "Consumed<K, V>"], ["String"], ["KStream<K, V>"]],
+}
+
+
+def _params(sig):
+    """Parameter types of a Java signature (commas inside <...> belong to the type)."""
+    parts, depth, cur = [], 0, ""
+    for ch in sig:
+        depth += {"<": 1, ">": -1}.get(ch, 0)
+        if ch == "," and depth == 0:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    parts.append(cur)
+    return [" ".join(p.replace("final ", "").split()[:-1]) for p in parts if p.strip()]
+
+
+def test_gpu_streams_builder_mirrors_the_reference_entry_point():
+    """GpuComplexStreamsBuilder is the drop-in for ComplexStreamsBuilder (no reference file
+    needs a hand edit): every reference constructor and stream(...) overload exists with the same
+    parameters, each stream(...) has a twin taking the value's IrSchema last, every route ends in
+    new GpuCEPStreamImpl<>(stream, schema, options), and GpuCEPStreamImpl has that constructor."""
+    src = open(os.path.join(JAVA, "GpuComplexStreamsBuilder.java")).read()
+    ctors = [_params(m) for m in re.findall(r"public GpuComplexStreamsBuilder\(([^)]*)\)", src)]
+    streams = [_params(m) for m in re.findall(r"public <K, V> CEPStream<K, V> stream\(([^)]*)\)", src)]
+    for c in REFERENCE_BUILDER["ctors"]:
+        assert c in ctors, c
+    for sig in REFERENCE_BUILDER["stream"]:
+        assert sig in streams, sig
+        assert sig + ["IrSchema<V>"] in streams, sig
+    assert "public Topology build()" in src
+    assert src.count("new GpuCEPStreamImpl<>(stream, schema, options)") == 1
+    assert "new CEPStreamImpl" not in src                 # the CPU route is GpuCEPStreamImpl's decision
+    impl = open(os.path.join(ROOT, "java", "org", "apache", "kafka", "streams", "kstream", "internals",
+                             "GpuCEPStreamImpl.java")).read()
+    assert re.search(r"public GpuCEPStreamImpl\(final KStream<K, V> stream, final IrSchema<V> schema, "
+                     r"final GpuOptions options\)", impl)
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "GpuComplexStreamsBuilder" in integ

@@ -341,11 +341,28 @@ def runs_div_pattern():
 def test_runs_path_keys_fail_where_the_reference_fails(seed, batch):
     """several keys of one batch throw on the runs path.  cep_batch_errors must list every
     failing key's first exception, so that the processor (which groups a batch by key) fails at the
-    first exception in ARRIVAL order and forwards exactly what the reference forwarded before it."""
+    first exception in ARRIVAL order and forwards exactly what the reference forwarded before it.
+    The failures are constructed, not hoped for: no value is 7 except at five chosen records of five
+    keys, all inside one batch, where the strict second stage divides by (v - 7); the first of them in
+    arrival order belongs to the largest of the five keys, so the key-grouped batch meets it last."""
     rng = np.random.default_rng(seed)
     n = 5000
     kid = rng.integers(0, 1000, n).astype(np.int32)
-    val = rng.integers(0, 200, n).astype(np.int32)
+    val = rng.integers(1, 200, n).astype(np.int32)
+    val[val == 7] = 8
+    lo = (n // 2 // batch) * batch                        # one batch: arrival positions [lo, lo + batch)
+    hi = min(n, lo + batch)
+    pos = []
+    for i in range((lo + hi) // 2, hi):                   # records whose key arrived before (run waiting):
+        if (kid[:i] == kid[i]).any() and all(kid[j] != kid[i] for j in pos) and \
+                (kid[i] > 900 if not pos else kid[i] < kid[pos[0]]):   # the first of a large key
+            pos.append(i)
+        if len(pos) == 5:
+            break
+    assert len(pos) == 5
+    keys = sorted(int(kid[i]) for i in pos)
+    for i in pos:
+        val[i] = 7
     sch = Schema([("value", "i32")])
     ir = runs_div_pattern().to_ir(sch)
     assert N.CompiledPattern(ir).info.runs_ok
@@ -353,6 +370,7 @@ def test_runs_path_keys_fail_where_the_reference_fails(seed, batch):
     r = O.OracleRun(p, O.MODE_PROCESSOR)
     with pytest.raises(O.OracleError) as oe:
         r.process(O.BatchArrays(kid, [val], [1]))
+    assert oe.value.record == pos[0] and kid[pos[0]] == keys[-1]
     recs = [(f"K{kid[i]}", int(val[i]), "t", 0, i, i) for i in range(n)]
     want = [(recs[m.record][0], seq_view(sequence_from_traversal(
         m.traversal, p.names, lambda i: Ev(recs[i][0], recs[i][1], i, "t", 0, i))))
@@ -365,8 +383,8 @@ def test_runs_path_keys_fail_where_the_reference_fails(seed, batch):
         for rr in recs:
             proc.process(*rr)
         proc.flush()
-    assert (ge.value.code, ge.value.record) == (oe.value.code, oe.value.record) == (5, oe.value.record)
-    assert len(proc.session.batch_errors()[0]) > 1        # several keys failed in the failing batch
+    assert (ge.value.code, ge.value.record) == (oe.value.code, oe.value.record) == (5, pos[0])
+    assert len(proc.session.batch_errors()[0]) == 5       # every failing key of the batch is listed
     assert got == want and len(want) > 0
 
 
