@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--nfa-kernel", choices=["auto", "wave", "lane"], default="auto",
                     help="general path: one key per wave (CEP_SESSION_WAVE_NFA) or per lane (CEP_SESSION_LANE_NFA); "
                          "auto: the library's choice")
+    ap.add_argument("--handoff-cap", type=int, default=16384,
+                    help="C4: per-key workspace cap (words) of the hand-off leg -- keys over it continue on the "
+                         "CPU (the oracle) from their exported state; 0 skips the leg")
     ap.add_argument("--gather-matches", action="store_true",
                     help="N > 1: after the timed steps, gather every rank's matches to rank 0 (12 B/match) and "
                          "time it")
@@ -243,6 +246,8 @@ def main():
                                                        else "nfa_kernel + compaction") + ")"
         achieved = kernel_bytes / (roof_ms * 1e-3) / 1e9
         value = tot_events * args.steps / t_max
+        build = N.lib().cep_version().decode().rsplit(" ", 1)[-1]
+        traffic, traffic_src = _pmc_traffic(args.config, n, build)
         line = {
             "metric": METRIC if args.config == "c2" else f"events/sec (whole node), {C['desc']}",
             "value": value,
@@ -263,11 +268,12 @@ def main():
                        "kernels": "compiled for the pattern (hiprtc)" if sess.jit else "built-in",
                        "forced_path": args.force_path, "nfa_kernel": args.nfa_kernel},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": _pmc_traffic(args.config, n),
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": roof_kernel, "kernel_ms": roof_ms, "algo_bytes_per_launch": kernel_bytes,
                          "algo_bytes_per_step": algo_bytes},
             "cpu_baseline": None,
             "checksum": f"{csum:016x}",
+            "build": build,
         }
         if shard_info is not None:
             line["config"]["shard"] = shard_info[1]
@@ -279,7 +285,12 @@ def main():
                                     "ms": avg_kernel_ms}
         if sess.path == N.PATH_GENERAL:
             line["config"]["live_run_hwm"] = sess.live_run_hwm()     # run-explosion high-water mark
-            line["config"]["keys_on_cpu"] = 0                        # no CPU fallback: every key runs on the GPU
+            # keys the resident (uncapped) run handed back: they outgrew even the whole device pool
+            erec, ecode = sess.batch_errors()
+            line["config"]["keys_over_device_pool"] = int(sum(1 for c in ecode if c == N.E_RUN_CAPACITY))
+        if world == 1 and args.config == "c4" and args.handoff_cap > 0 and not force:
+            line["handoff"] = _handoff_leg(ir, key, cols[0], ts, K, C["per_key"], args.handoff_cap, stream)
+            line["config"]["keys_on_cpu"] = line["handoff"]["keys_on_cpu"]
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN) and not args.no_host_input:
             line["pcie_inclusive"], host = _pcie_inclusive(sess, n, key, cols, stream, csum)
             # the processor's own batch sizes (CEPStream.query batch_size defaults to 1 << 16): host
@@ -396,18 +407,139 @@ def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, r
     return out
 
 
-def _pmc_traffic(cfg, n):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (if any),
-    FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM)."""
+def _kcrf_events(blob):
+    """(offset, first column) of every event a KCRF state holds (include/kcep.h, cep_state_to_reference)."""
+    import struct
+    ncols = struct.unpack_from("<i", blob, 12)[0]
+    at = 24
+    (nh,) = struct.unpack_from("<i", blob, at)
+    at += 4 + 12 * nh
+    (ne,) = struct.unpack_from("<i", blob, at)
+    at += 4
+    evs = []
+    for _ in range(ne):
+        _, _, _, off, _ = struct.unpack_from("<qiiqq", blob, at)
+        at += 32
+        (c0,) = struct.unpack_from("<q", blob, at)
+        at += 8 * ncols
+        evs.append((off, c0))
+    return evs
+
+
+def _handoff_leg(ir, key, val, ts, K, L, cap, stream, nb=4):
+    """BASELINE.md §3 C4's CPU-fallback count, measured: the workload through a CEP_SESSION_CARRY session
+    (the GpuCEPProcessor route) in `nb` batches -- batch b holds records [b*L/nb, (b+1)*L/nb) of every key
+    -- with the per-key workspace capped at `cap` words (cep_opts.max_key_words).  A key over the cap is
+    handed back (CEP_E_RUN_CAPACITY, its state as of the batch start); as GpuCEPProcessor.handOff does,
+    its state is evicted, rewritten in the reference's terms (cep_state_to_reference) and the key
+    continues on the CPU -- here the oracle, the C restatement of the reference NFA, resumed from that
+    form -- over the rest of its records.  Parity: every key's joined matches (device, then CPU) against
+    the oracle's uninterrupted run, in the reference's per-key emission order.  C4's ts column is each
+    record's index within its key, pushed as its offset too, so the CPU side maps back by offset."""
+    import numpy as np
+    import torch
+    from kcep import native as N
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    per = L // nb
+    pat = N.CompiledPattern(ir)
+    s = N.Session(pat, K * per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K, max_key_words=cap)
+    kk, vv, tt = key.view(K, L), val.view(K, L), ts.view(K, L)
+    keep = torch.ones(K, dtype=torch.bool, device=key.device)
+    hv = val.cpu().numpy().reshape(K, L)
+    pos2idx = np.zeros(K * L, np.int64)          # stream position -> index in the key-grouped stream
+    dev_out, cpu_m, handed = [], {}, {}
+    t_dev = t_cpu = 0.0
+    for b in range(nb):
+        rows = torch.nonzero(keep).flatten()
+        bk = kk[rows, b * per:(b + 1) * per].contiguous().view(-1)
+        bv = vv[rows, b * per:(b + 1) * per].contiguous().view(-1)
+        bt = tt[rows, b * per:(b + 1) * per].contiguous().view(-1)
+        rk = rows.cpu().numpy()
+        base = s.stream_position()
+        j = np.arange(len(rk) * per)
+        pos2idx[base:base + len(j)] = rk[j // per] * L + b * per + j % per
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.push(bk.numel(), bk.data_ptr(), [bv.data_ptr()], ts=bt.data_ptr(), offset=bt.data_ptr(), mem=N.MEM_DEVICE,
+               stream=stream.cuda_stream, flags=N.BATCH_OFFSETS_MONOTONE)
+        out = s.collect(raise_on_error=False)
+        erec, ecode = s.batch_errors()
+        t_dev += time.perf_counter() - t0
+        assert all(c == N.E_RUN_CAPACITY for c in ecode), "C4 raises no reference exception"
+        cap_keys = sorted({int(rk[(int(r) - base) // per]) for r in erec})
+        dev_out.append((out, set(cap_keys)))
+        if not cap_keys:
+            continue
+        blobs = s.state_evict(cap_keys)
+        keep[torch.tensor(cap_keys, device=key.device)] = False
+        t1 = time.perf_counter()
+        for k, blob in zip(cap_keys, blobs):                    # the reference continues the key
+            handed[k] = b
+            ref = pat.state_to_reference(blob) if blob else None
+            evs = _kcrf_events(ref) if ref else []
+            o_ = np.array([e[0] for e in evs] + list(range(b * per, L)), np.int64)
+            v_ = np.array([e[1] for e in evs] + [int(hv[k, i]) for i in range(b * per, L)], np.int32)
+            r = O.OracleRun(O.OraclePattern(ir), O.MODE_PROCESSOR)
+            bat = O.BatchArrays(np.full(len(o_), k, np.int32), [v_], [1], offset=o_, ts=o_)
+            if ref:
+                r.resume(bat, ref)
+            else:
+                r.process(bat)
+            cpu_m[k] = [(k * L + int(o_[m.record]), [(nm, k * L + int(o_[e])) for nm, e in m.traversal])
+                        for m in r.matches(with_groups=False)]
+        t_cpu += time.perf_counter() - t1
+    got = {}
+    for out, cap_keys in dev_out:                               # device matches, batch by batch
+        mk, mr, eo = out["match_key"], pos2idx[out["match_record"]], out["ent_off"]
+        en, er = out["ent_name"], pos2idx[out["ent_record"]]
+        for m in range(len(mk)):
+            k = int(mk[m])
+            if k not in cap_keys:
+                got.setdefault(k, []).append((int(mr[m]), list(zip(en[eo[m]:eo[m + 1]].tolist(),
+                                                                    er[eo[m]:eo[m + 1]].tolist()))))
+    for k, ms in cpu_m.items():                                 # then the CPU's, after the hand-off
+        got.setdefault(k, []).extend(ms)
+    hk = key.cpu().numpy()
+    want_csr = O.baseline_csr(O.OraclePattern(ir), O.BatchArrays(hk, [val.cpu().numpy()], [1],
+                                                                 ts=ts.cpu().numpy()), O.MODE_PROCESSOR,
+                              max(1, min(16, os.cpu_count() or 1)))
+    want = {}
+    wk, wr, wo, wn, we = (want_csr[f] for f in ("match_key", "match_record", "ent_off", "ent_name", "ent_record"))
+    for m in range(len(wk)):
+        want.setdefault(int(wk[m]), []).append((int(wr[m]), list(zip(wn[wo[m]:wo[m + 1]].tolist(),
+                                                                      we[wo[m]:wo[m + 1]].tolist()))))
+    parity = all(got.get(k, []) == want.get(k, []) for k in set(got) | set(want))
+    s.close()
+    diff = None
+    if not parity:                                              # the first key that differs, for the record
+        k = next(k for k in sorted(set(got) | set(want)) if got.get(k, []) != want.get(k, []))
+        diff = {"key": k, "handed_back_in_batch": handed.get(k), "device_or_cpu": got.get(k, [])[:4],
+                "reference": want.get(k, [])[:4], "n_got": len(got.get(k, [])), "n_want": len(want.get(k, []))}
+    return {"cap_words": cap, "batches": nb, "keys_on_cpu": len(handed),
+            "handed_back_per_batch": [sum(1 for v in handed.values() if v == b) for b in range(nb)],
+            "device_s": t_dev, "cpu_continuation_s": t_cpu,
+            "matches": int(sum(len(v) for v in got.values())), "parity": bool(parity), "first_difference": diff,
+            "how": "keys over the cap: cep_state_evict -> cep_state_to_reference -> oracle resume (GpuCEPProcessor.handOff)"}
+
+
+def _pmc_traffic(cfg, n, build):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (if any), FETCH_SIZE doubled per
+    the gfx950 correction (MI355X_MICROARCH.md §HBM), and where they come from: the summary file, the
+    library build (source hash, cep_version) and commit its counters were taken on, and whether that is
+    the build this run measures.  rocprofv3 --pmc cannot run inside this process (tools/gpu_prof.sh
+    collects it in separate passes of the same command)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json" if cfg == "c2" else f"pmc_traffic_{cfg}.json")
     try:
         with open(p) as f:
             d = json.load(f)
         if int(d.get("events")) != n:
-            return None
-        return float(d["hbm_bytes_per_launch"])
+            return None, None
+        return float(d["hbm_bytes_per_launch"]), {
+            "file": os.path.relpath(p, ROOT), "pmc": d.get("source"), "build": d.get("build"),
+            "commit": d.get("commit"), "same_build_as_this_run": d.get("build") == build}
     except Exception:
-        return None
+        return None, None
 
 
 def host_cpu():

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/kcep.h"
+#include "build_id.h"   // KCEP_BUILD_ID (Makefile: hash of the library sources)
 #include "kcep_internal.h"
 #include "jit.h"
 
@@ -133,12 +134,7 @@ uint64_t mix64(uint64_t x) {
 // evaluations read nothing but the record -- every edge predicate event-only, no folds, no states.
 // the wave kernel takes every pattern: rounds whose runs share a sequence that one of them folds into
 // (or that read a partial sequence after a run of the round died) are evaluated again sequentially
-// (nfa_wave.h).  KCEP_NFA_WAVE_AGG=0 keeps patterns with aggregates / SequenceMatchers on the lane kernel.
-bool wave_ok(const DevProgram& D) {
-  const char* v = getenv("KCEP_NFA_WAVE_AGG");
-  const bool agg_on = !(v && v[0] == '0');
-  return agg_on || !wave_stateful(D);
-}
+// (nfa_wave.h).
 
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
 constexpr NfaCaps kCaps{16, 64, 32, 32, 8, 16};
@@ -267,13 +263,13 @@ bool getenv_flag(const char* name) {
 StencilCarry carry_args(const cep_session* s) {
   return StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), s->pat->prog.stencil.k - 1, s->halo_stamp,
                       int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->halo_base,
-                      s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), 0};
+                      s->hflags.as<unsigned long long>() + (s->halo_stamp & 1)};
 }
 
 // Host-resident batch columns -> one packed device image (s->dstage), 256-B aligned per column.  The
 // caller's memory is borrowed only for the call (kcep.h cep_push_batch):
 //  - pageable memory (a JVM heap array, a numpy buffer) is copied into the session's pinned ring in
-//    chunks of kRingChunk bytes, each chunk moved by one async copy while the next one is filled; the
+//    chunks of 2 MB, each chunk moved by one async copy while the next one is filled; the
 //    call returns once the last chunk is in the ring;
 //  - memory that is itself pinned is copied from directly, and the call waits for that copy (the
 //    kernels are already enqueued behind it).
@@ -282,7 +278,6 @@ struct HostArr {
   size_t bytes;
   const void** dst;               // receives the device address (null src: left null)
 };
-constexpr size_t kRingChunk = size_t(8) << 20;
 // zero copy only pays for small batches: the kernel then reads the batch over the link itself, which
 // for an 8 MB batch (1 M records) cost 706 us per flush against ~280 us by DMA (r04 bench)
 constexpr size_t kZeroCopyMax = size_t(1) << 20;
@@ -306,11 +301,10 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
   }
   if (!total) return CEP_OK;
   // zero copy (the stencil path's one streaming pass, batches up to kZeroCopyMax): the kernel reads the
-  // pinned ring over the link itself, no copy into HBM first (KCEP_ZERO_COPY=0 turns it off for A/B).
+  // pinned ring over the link itself, no copy into HBM first.
   // Pinned caller memory takes it too: one host memcpy beats waiting for a DMA before the call may
   // return (r04 flush probe, 64 k records: 55.8 us per flush through the ring, 67-69 us pinned by DMA)
-  static const bool zc_env = [] { const char* e = getenv("KCEP_ZERO_COPY"); return !(e && e[0] == '0'); }();
-  if (zero_copy && zc_env && total <= kZeroCopyMax) {
+  if (zero_copy && total <= kZeroCopyMax) {
     const int j = s->ring_next;
     s->ring_next ^= 1;
     if (s->ring_ev[j]) HIPCHECK(hipEventSynchronize(s->ring_ev[j]));
@@ -350,11 +344,8 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
     return CEP_OK;
   }
   // pageable: through the pinned ring, in chunks so that the copy of one overlaps the filling of the next
-  // (2 MB chunks: the copy of chunk i overlaps the filling of chunk i + 1; a smaller batch is one chunk.
-  // KCEP_RING_SPLIT=k: k equal chunks instead, A/B)
-  static const size_t split = [] { const char* e = getenv("KCEP_RING_SPLIT"); return e ? size_t(atoi(e)) : size_t(0); }();
-  const size_t chunk = split ? std::min(kRingChunk, std::max<size_t>(size_t(64) << 10, ((total / split) + 4095) & ~size_t(4095)))
-                             : std::min(total, size_t(2) << 20);
+  // (2 MB chunks: the copy of chunk i overlaps the filling of chunk i + 1; a smaller batch is one chunk)
+  const size_t chunk = std::min(total, size_t(2) << 20);
   for (size_t c0 = 0; c0 < total; c0 += chunk) {
     const size_t c1 = std::min(total, c0 + chunk);
     const int j = s->ring_next;
@@ -419,10 +410,9 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     // the batch's error flags: one of two words by the stamp's parity; the other one, cleared by this
     // batch's scan kernel, serves the next batch (no memset launch per batch)
     L.clear_flag = s->hflags.as<unsigned long long>() + (s->halo_stamp & 1);
-    const char* dbg = getenv("KCEP_CARRY_DBG");   // A/B probes of the carry kernel's parts (tools/carry_probe.py)
     L.carry = StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), SP.k - 1, ++s->halo_stamp,
                            int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->base,
-                           s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), dbg ? atoi(dbg) : 0};
+                           s->hflags.as<unsigned long long>() + (s->halo_stamp & 1)};
     s->halo_base = s->base;
     s->base += b->n;
   }
@@ -837,11 +827,10 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.cpool_top = ctl + 1;
   A.flags = reinterpret_cast<int32_t*>(ctl + 2);
   A.err_any = ctl + 4;
-  // key segments per wave (KCEP_NFA_SPREAD: experiments; fewer keys per wave diverge less but leave
-  // the chip emptier -- tools/c4_profile.py)
+  // lane kernel: 64 key segments per wave (fewer diverge less but leave the chip emptier: C4 gained 5 %
+  // at 8 per wave, light keys lost 2x, profiles/r01_s5_nfa_spread_*.log)
   A.wave_agg = (wave_stateful(D) ? 1 : 0) | (P.has_seq ? 2 : 0);
-  const char* spread_env = getenv("KCEP_NFA_SPREAD");
-  A.spread = spread_env ? std::min(64, std::max(1, atoi(spread_env))) : 64;
+  A.spread = 64;
   if (s->opts.flags & CEP_SESSION_PROFILE) {
     if (s->r_prof.ensure(sb * NFA_PROFILE_W)) return fail(CEP_E_HIP, "allocation failed");
     A.profile = s->r_prof.as<int64_t>();
@@ -972,7 +961,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
 extern "C" {
 
 const char* cep_last_error(void) { return g_err.c_str(); }
-const char* cep_version(void) { return "kcep 0.1 (gfx950)"; }
+const char* cep_version(void) { return "kcep 0.1 (gfx950) build " KCEP_BUILD_ID; }
 
 int cep_compile(const uint8_t* ir, size_t len, cep_pattern** out) {
   if (!ir || !out) return fail(CEP_E_ARG, "null argument");
@@ -1121,16 +1110,14 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
   // with an IGNORE edge (skip-till-next / skip-till-any, the C4 run explosion) -- else one key per
   // lane: keys of strict patterns hold a few runs, and a wave round costs a light key more than a
   // lane's walk (C3 on the general path: 342 vs 107 ms, profiles/r03_ab_c3_general_wave_lane.log).
-  // CEP_SESSION_LANE_NFA / CEP_SESSION_WAVE_NFA or KCEP_NFA_WAVE=0/1 choose explicitly.
+  // CEP_SESSION_LANE_NFA / CEP_SESSION_WAVE_NFA choose explicitly.
   bool grows = false;
   for (const auto& st : P.stages)
     for (const auto& e : st.edges) grows = grows || e.op == E_IGNORE;
-  const char* env_wave = getenv("KCEP_NFA_WAVE");
   bool wave = grows;
   if (opts->flags & CEP_SESSION_LANE_NFA) wave = false;
   else if (opts->flags & CEP_SESSION_WAVE_NFA) wave = true;
-  else if (env_wave) wave = env_wave[0] == '1';
-  s->wave = P.general_ok && wave && wave_ok(P.dev);
+  s->wave = P.general_ok && wave;
   const char* env_jit = getenv("KCEP_JIT");
   s->jit_on = !(opts->flags & CEP_SESSION_INTERPRET) && !(env_jit && !strcmp(env_jit, "0"));
   if (s->jit_on && path == CEP_PATH_RUNS) s->jit = jit_runs(P, s->jit_why);   // on failure: built-in kernels

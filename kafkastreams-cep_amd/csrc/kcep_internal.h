@@ -145,8 +145,6 @@ struct StencilCarry {
   int64_t base;                      // stream position of batch record 0
   unsigned long long* flags;         // bit 0: key id out of range, bit 1: a key in two segments,
                                      // bit 2: chain carry batch beyond a tile's match space
-  int32_t dbg;                       // KCEP_CARRY_DBG (A/B probes only): bit 0 no claims, bit 1 no halo
-                                     // loads, bit 2 no halo writes, bit 3 no visits (plain carry kernel)
 };
 KCEP_HD inline int halo_old(const HaloHdr& h, int32_t stamp) {
   // the newer slot written before batch `stamp` (or an empty one)

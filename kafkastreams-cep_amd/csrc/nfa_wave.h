@@ -50,23 +50,36 @@ constexpr int WAVE = 64;
 // DESIGN.md 4.4, and removed; the helpers keep the group width as a parameter.)
 template <int GL>
 struct Grp {
+  static_assert(GL == 64, "the wave kernel runs one key per wave");
   int gl;                                  // lane within the group
   int base;                                // the group's first lane in the wave
-  __device__ __forceinline__ uint64_t ballot(bool x) const {
-    const uint64_t b = __ballot(x);
-    if constexpr (GL == 64) return b;
-    else return (b >> base) & ((1ull << GL) - 1);
-  }
+  __device__ __forceinline__ uint64_t ballot(bool x) const { return __ballot(x); }
+  // lane src's value in every lane (v_readlane: a scalar result, no LDS round trip; src is uniform)
   template <class T>
-  __device__ __forceinline__ T bcast(T v, int src = 0) const { return __shfl(v, src, GL); }
-  // exclusive prefix of v over the group's lanes, and the group total
+  __device__ __forceinline__ T bcast(T v, int src = 0) const {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "bcast: 4- or 8-byte values");
+    if constexpr (sizeof(T) == 4) {
+      return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+    } else {
+      const uint64_t u = __builtin_bit_cast(uint64_t, v);
+      const uint32_t lo = __builtin_amdgcn_readlane(int(uint32_t(u)), src);
+      const uint32_t hi = __builtin_amdgcn_readlane(int(uint32_t(u >> 32)), src);
+      return __builtin_bit_cast(T, uint64_t(lo) | (uint64_t(hi) << 32));
+    }
+  }
+  // exclusive prefix of v over the wave, and the total: DPP row shifts and row broadcasts (VALU
+  // lane moves, rocPRIM's warp_scan_dpp pattern) instead of six LDS-crossbar permutes.  Every lane of
+  // the wave must be active (the callers are wave-uniform points); a shifted-in lane outside the row
+  // reads 0 (update_dpp's old value)
   __device__ __forceinline__ int excl_scan(int v, int& total) const {
     int x = v;
-    for (int d = 1; d < GL; d <<= 1) {
-      const int y = __shfl_up(x, d, GL);
-      if (gl >= d) x += y;
-    }
-    total = __shfl(x, GL - 1, GL);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 into rows 2, 3
+    total = __builtin_amdgcn_readlane(x, 63);
     return x - v;
   }
   __device__ __forceinline__ int max_all(int v) const {

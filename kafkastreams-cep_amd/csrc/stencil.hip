@@ -57,31 +57,6 @@ __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict_
   }
 }
 
-// The same move with one thread per match writing its whole k-int row (one 16-B store for k = 4):
-// the slot int and aux byte are read once per match instead of once per output word.
-__global__ __launch_bounds__(256) void stencil_gather_rows(const int32_t* __restrict__ slots,
-                                                           const int64_t* __restrict__ cnt,
-                                                           const int64_t* __restrict__ pre, int32_t* __restrict__ out,
-                                                           int64_t out_cap, SlotFormat F) {
-  const int64_t t = blockIdx.x;
-  const int64_t m = cnt[t], p = pre[t];
-  if (p + m > out_cap) return;
-  const int k = F.k;
-  for (int64_t q = threadIdx.x; q < m; q += blockDim.x) {
-    int32_t row[STENCIL_MAX_K];
-#pragma unroll
-    for (int s = 0; s < STENCIL_MAX_K; s++) row[s] = s < k ? F.entry(slots, t, m, q, s) : 0;
-    int32_t* d = out + (p + q) * k;
-    if (k == 4) {
-      *reinterpret_cast<int4*>(d) = make_int4(row[0], row[1], row[2], row[3]);
-    } else {
-#pragma unroll
-      for (int s = 0; s < STENCIL_MAX_K; s++)
-        if (s < k) d[s] = row[s];
-    }
-  }
-}
-
 // ---- launcher ------------------------------------------------------------
 
 int64_t stencil_tiles(int64_t n) { return (n + ST_TILE - 1) / ST_TILE; }
@@ -328,15 +303,8 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
       if (e == hipSuccess && L.clear_flag) e = hipMemsetAsync(L.clear_flag, 0, 8, st);
       if (e != hipSuccess) return e;
     }
-    static const int gthreads = [] { const char* e = getenv("KCEP_GATHER_THREADS"); const int v = e ? atoi(e) : 0;
-                                     return v == 64 || v == 128 || v == 256 ? v : 128; }();   // A/B knob
-    static const bool rows = getenv("KCEP_GATHER_ROWS") && getenv("KCEP_GATHER_ROWS")[0] == '1';   // A/B knob
-    if (rows)
-      hipLaunchKernelGGL(stencil_gather_rows, dim3(unsigned(nsuper)), dim3(gthreads), 0, st, L.slots, L.tile_count,
-                         L.tile_pre, L.out, L.out_cap, F);
-    else
-      hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(gthreads), 0, st, L.slots, L.tile_count,
-                         L.tile_pre, L.out, L.out_cap, sub, F);
+    hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre,
+                       L.out, L.out_cap, sub, F);
   }
   if (D.hdr) {
     hipError_t e = hipGetLastError();

@@ -507,11 +507,8 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
           kb = ck[8 + 31 - __clz(todo)];
           oka = key_ok(C, ka);
           okb = kb != ka && key_ok(C, kb);
-          if (!(C.dbg & 2)) {
-            ra = halo_load(C, oka ? ka : 0);
-            rb = halo_load(C, okb ? kb : 0);
-          }
-          if (C.dbg & 1) starts = 0;
+          ra = halo_load(C, oka ? ka : 0);
+          rb = halo_load(C, okb ? kb : 0);
           while (starts) {                                 // claims, checked after the visits
             const int i = __ffs(starts) - 1;
             starts &= starts - 1;
@@ -597,7 +594,6 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
           for (int t = 1; t < K; t++)
             if (o == t - 1 && s_key[kpos(lb + 8 + i - t)] == kj) o = t;
           HaloHead H = kj == H0.key ? H0 : H1;
-          if (C.dbg & 2) H.key = kj;
           if (!halo_head(C, kj, H)) continue;
           if ((bnd >> i) & 1) {
             if constexpr (CHAIN) {                         // runs started in the halo may end here
@@ -619,7 +615,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
             const int sg = o + 1 < K - 1 ? o + 1 : K - 1;
             uint64_t wmk = 0;
             for (int t = 0; t < sg; t++) wmk |= uint64_t(s_mask[lb + 8 + i - (sg - 1) + t]) << (8 * t);
-            if (!(C.dbg & 4)) halo_write<K>(C, H, sg, wmk, g0 + i);
+            halo_write<K>(C, H, sg, wmk, g0 + i);
           }
         }
         if (twice) atomicOr(C.flags, 2ull);               // a key in two segments of the batch
@@ -994,7 +990,6 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
       }
       cand = (cand >> 8) & live;
       uint32_t todo = cand | ends | starts;
-      if (C.dbg & 8) todo = 0;                    // A/B probe only: no visits
       if (todo) {
         const int lb16 = 16 + ST_EPT * tid;       // s_bk index of own record 0
         // same-key records before own record i in the batch (capped at K-1)

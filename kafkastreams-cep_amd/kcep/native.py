@@ -21,6 +21,7 @@ ERRORS = {
     7: "ArrayIndexOutOfBoundsException", 8: "BadIR", 9: "RunCapacity", 10: "HipError", 11: "BadArgument",
     12: "Unsupported",
 }
+E_RUN_CAPACITY = 9         # a key over its device workspace, handed back per key (cep_batch_errors)
 MODE_NFA, MODE_PROCESSOR = 0, 1
 PATH_STENCIL, PATH_GENERAL, PATH_CHAIN, PATH_RUNS = 1, 2, 3, 4
 MEM_HOST, MEM_DEVICE = 0, 1

@@ -135,6 +135,7 @@ class GpuCEPProcessor:
         self._prune_at = max(int(prune_at), 2 * self.batch_size)   # _log size that triggers a prune
         self._prune_min = self._prune_at
         self.capacity_reruns = 0                  # keys re-run with the per-key workspace cap lifted
+        self._arrived = 0                         # non-null records flushed so far (error records are numbered so)
 
     # ---- Processor API (CEPProcessor.init/process/punctuate/close, :88-170) ----
     def init(self, forward: Callable[[Any, Sequence], None], session=None):
@@ -260,6 +261,9 @@ class GpuCEPProcessor:
         if not self._pending:
             return 0
         recs, self._pending = self._pending, []
+        base = self._arrived                              # non-null records handed to process() before this flush
+        self._arrived += len(recs)
+        arrival = list(range(len(recs)))                  # the processor-wide arrival index of recs[i] is base + this
         self._flags = 0
         if self.session.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS):
             # the stencil / chain / runs paths carry each key's records (its last K-1, or those
@@ -267,13 +271,14 @@ class GpuCEPProcessor:
             # (CEPProcessor.checkHighWaterMark :152-160) is applied here, in arrival order, and the
             # batch handed over has increasing offsets per key and topic.  Every admitted record is
             # processed and moves the mark (a record that throws fails the task anyway).
-            kept = []
-            for r in recs:
+            kept, arrival = [], []
+            for i, r in enumerate(recs):
                 hk = (r[0], r[2])
                 if r[4] < self._hwm.get(hk, -1):
                     continue
                 self._hwm[hk] = r[4] + 1
                 kept.append(r)
+                arrival.append(i)
             recs = kept
             self._flags = N.BATCH_OFFSETS_MONOTONE
             if not recs:
@@ -295,7 +300,8 @@ class GpuCEPProcessor:
                 self.session.set_max_key_words(self.max_key_words)
             self.capacity_reruns += len(cap)
             if any(c == 9 for _, c in e2):
-                self._failed = N.CepError(9, "a key outgrew the whole device pool", min(a for a, c in e2 if c == 9))
+                self._failed = N.CepError(9, "a key outgrew the whole device pool",
+                                          base + arrival[min(a for a, c in e2 if c == 9)])
                 raise self._failed
             matches += m2
             errors += e2
@@ -314,7 +320,9 @@ class GpuCEPProcessor:
         if not errors and len(self._log) >= self._prune_at:
             self._prune()
         if errors:
-            self._failed = N.CepError(err_code, N.ERRORS.get(err_code, "exception") + " in process()", limit)
+            # the failing record by its arrival index over the processor's life (non-null records)
+            self._failed = N.CepError(err_code, N.ERRORS.get(err_code, "exception") + " in process()",
+                                      base + arrival[limit])
             raise self._failed
         return sent
 

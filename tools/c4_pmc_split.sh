@@ -11,7 +11,7 @@ mkdir -p $D
 run() {  # name, scratch, counters...
   local nm=$1 sc=$2; shift 2
   if [ "$sc" = default ]; then unset KCEP_WAVE_SCRATCH; else export KCEP_WAVE_SCRATCH=$sc; fi
-  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $D -o ${nm}_$sc -- python3 bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-host-input --carry-batches 1 --processor-batch , > $D/${nm}_$sc.log 2>&1 || return 1
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $D -o ${nm}_$sc -- python3 bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-host-input --carry-batches 1 --processor-batch , --handoff-cap 0 > $D/${nm}_$sc.log 2>&1 || return 1
   echo "pass $nm scratch=$sc ok"
 }
 for sc in default 0; do

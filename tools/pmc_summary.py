@@ -44,7 +44,20 @@ def main():
     with open(os.path.join(prof, f"{prefix}_pmc.json"), "w") as f:
         json.dump({"tag": tag, "per_launch": rows}, f, indent=1)
     k = rows[kernel]
-    out = {"kernel": kernel, "events": events, "source": f"profiles/{prefix}_pmc.json",
+    # the library build the counters were taken on: the bench line of the kernel-trace pass
+    build = None
+    try:
+        with open(os.path.join(ROOT, "gpurun_out", f"prof_trace_{tag}.log")) as f:
+            for line in f:
+                if line.startswith("{"):
+                    build = json.loads(line).get("build", build)
+    except OSError:
+        pass
+    import subprocess
+    commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                            text=True).stdout.strip() or None
+    out = {"kernel": kernel, "events": events, "source": f"profiles/{prefix}_pmc.json", "build": build,
+           "commit": commit,
            "fetch_bytes_per_launch": k["fetch_bytes_corrected"], "write_bytes_per_launch": k["write_bytes"],
            "hbm_bytes_per_launch": k["fetch_bytes_corrected"] + k["write_bytes"]}
     with open(os.path.join(prof, "pmc_traffic.json" if cfg == "c2" else f"pmc_traffic_{cfg}.json"), "w") as f:
