@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -256,6 +257,36 @@ done:
   return true;
 }
 
+// int f(int i) returning v[i] computed from 64-bit immediates (bit fields of a fixed width, the word
+// picked by comparisons): the stage table's small fields without a memory access -- a lookup in the
+// constexpr DevProgram with a lane-divergent stage id is a vector load from the code object's constant
+// data, which sat on every evaluation's dependency chain (nfa_dev.h ST_* accessors)
+void gen_packed(std::string& o, const char* name, const std::vector<int>& v) {
+  int lo = 0, hi = 0;
+  for (int x : v) { lo = std::min(lo, x); hi = std::max(hi, x); }
+  int bits = 1;
+  while ((int64_t(1) << bits) <= int64_t(hi) - lo) bits++;
+  const int per = 64 / bits;
+  const int nw = std::max<int>(1, int((v.size() + per - 1) / per));
+  std::vector<uint64_t> w(size_t(nw), 0);
+  for (size_t i = 0; i < v.size(); i++)
+    w[i / per] |= uint64_t(int64_t(v[i]) - lo) << (bits * (i % per));
+  char buf[96];
+  o += "__device__ __forceinline__ int " + std::string(name) + "(int i) {\n  uint64_t w = ";
+  for (int k = nw - 1; k > 0; k--) {
+    snprintf(buf, sizeof buf, "i >= %d ? 0x%016llxull : ", k * per, (unsigned long long)w[size_t(k)]);
+    o += buf;
+  }
+  snprintf(buf, sizeof buf, "0x%016llxull;\n", (unsigned long long)w[0]);
+  o += buf;
+  o += "  int s = i;\n";
+  for (int k = nw - 1; k > 0; k--) o += "  if (i >= " + std::to_string(k * per) + ") s = i - " + std::to_string(k * per) + ";\n" +
+                                     (k > 1 ? "  else\n" : "");
+  snprintf(buf, sizeof buf, "  return int((w >> (s * %d)) & 0x%llxull) + (%d);\n}\n", bits,
+           (unsigned long long)((uint64_t(1) << bits) - 1), lo);
+  o += buf;
+}
+
 // the generated part shared by every kernel family: program table, predicates, JitTab
 bool gen_program(const Program& P, std::string& o, std::string& why, bool branchfree = false) {
   const DevProgram& d = P.dev;
@@ -269,6 +300,21 @@ bool gen_program(const Program& P, std::string& o, std::string& why, bool branch
   for (int i = 0; i < d.nsl; i++) entries.insert(d.sl_pc[i]);
   o += "namespace kcep {\n";
   o += "constexpr DevProgram kcep_prog = " + program_table(d) + ";\n";
+  {                                               // the stage table's hot fields as immediates
+    std::vector<int> ty, nm, sl, ne, nf, op, tg, pr, es, sn;
+    for (int s = 0; s < d.nstages; s++) {
+      const DevStage& t = d.st[s];
+      ty.push_back(t.type); nm.push_back(t.name); sl.push_back(t.slot); ne.push_back(t.nedges); nf.push_back(t.nfolds);
+      for (int e = 0; e < NFA_MAX_EDGES; e++) {
+        op.push_back(t.op[e]); tg.push_back(t.target[e]); pr.push_back(t.pred[e]); es.push_back(t.sl[e]);
+      }
+    }
+    for (int s = 0; s < std::max(1, d.nslots); s++) sn.push_back(d.slot_name[s]);
+    gen_packed(o, "jst_type", ty); gen_packed(o, "jst_name", nm); gen_packed(o, "jst_slot", sl);
+    gen_packed(o, "jst_nedges", ne); gen_packed(o, "jst_nfolds", nf); gen_packed(o, "jst_op", op);
+    gen_packed(o, "jst_target", tg); gen_packed(o, "jst_pred", pr); gen_packed(o, "jst_sl", es);
+    gen_packed(o, "jst_slot_name", sn);
+  }
   for (int pc : entries)
     if (!gen_entry(d, pc, o, why, branchfree)) return false;
   o += "template <class Env>\n__device__ __forceinline__ bool jit_eval(int pc, Env& env, int64_t& r) {\n  switch (pc) {\n";
@@ -385,7 +431,9 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   const int waves = wenv ? std::min(8, std::max(1, atoi(wenv))) : 2;
   // the same for the wave kernel (KCEP_NFA_WAVE_OCC)
   const char* oenv = getenv("KCEP_NFA_WAVE_OCC");
-  const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 3;   // measured best on C4 (2: 13.3, 3: 10.8, 4: 11.8 ms)
+  // r05: 4 (C4 step 5.85 vs 6.40 ms at 3, with the stage fields as immediates and the phase-local LDS
+  // arrays unioned: 128 VGPRs, ~9.9 KB of LDS per wave); r02: 2: 13.3, 3: 10.8, 4: 11.8 ms
+  const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 4;
   // LDS arena words of the wave kernel's key workspace (KCEP_WAVE_ARENA, tuning only)
   const char* aenv = getenv("KCEP_WAVE_ARENA");
   if (aenv) o += "#define WAVE_ARENA " + std::to_string(std::min(8192, std::max(4, atoi(aenv)))) + "\n";

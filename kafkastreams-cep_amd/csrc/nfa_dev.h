@@ -63,6 +63,10 @@ struct KeyAlloc {
   unsigned long long scr_top;      // scratch words handed out (may pass scr_cap: then the pool)
   int32_t* scr;                    // the wave's region (nullptr: none)
   int64_t scr_cap;
+#ifdef KCEP_PHASES
+  unsigned long long kw[AK_N + 1]; // profiling kernels only: words allocated per kind (AK_*), then the pool's share
+  uint64_t ph[11];                 // profiling kernels only: lane 0's clocks per record-loop phase (nfa_wave.h KWP_*)
+#endif
 };
 
 struct Lane {
@@ -106,16 +110,16 @@ struct Lane {
   int32_t wgrow;               // wave: the shared heap was too small (grow it and re-run the round)
   int32_t ov_own;              // wave: this evaluation wrote an aggregate of its run's own sequence
   KeyAlloc* wpool;             // wave: the key's allocator, in LDS (every lane allocates for the key)
-#ifdef KCEP_PHASES
-  uint64_t ph[11];             // profiling kernels only: clocks in evaluate / predicates / buffer puts+branch /
-                               // removePattern / matchConstruction / first_compatible / add_pred / versions,
-                               // then counts: first_compatible calls / entries examined / digit-by-digit checks
-  uint64_t kw[AK_N + 1];       // profiling kernels only: words allocated per kind (AK_*), then those of the pool
+#ifdef KCEP_PHASES_LANE
+  uint64_t ph[11];             // lane-engine profiling builds only: clocks in evaluate / predicates / buffer
+                               // puts+branch / removePattern / matchConstruction / first_compatible / add_pred /
+                               // versions, then counts: first_compatible calls / entries examined / digit checks
 #endif
 };
 
-// phase timers of the profiling kernels (jit.cpp builds them for CEP_SESSION_PROFILE sessions)
-#ifdef KCEP_PHASES
+// phase timers of the lane engine (KCEP_PHASES_LANE builds only: they share Lane.ph with the wave
+// kernel's record-loop timers, nfa_wave.h KWP_*, which the CEP_SESSION_PROFILE kernels keep)
+#ifdef KCEP_PHASES_LANE
 #define KPH_BEGIN(l, i) const uint64_t kph_t##i = clock64()
 #define KPH_END(l, i) const_cast<Lane&>(l).ph[i] += clock64() - kph_t##i
 #define KPH_COUNT(l, i, n) const_cast<Lane&>(l).ph[i] += (n)
@@ -140,10 +144,10 @@ __device__ __forceinline__ unsigned long long lds_add(unsigned long long* p, uns
 // persist: the words must outlive the kernel (the match output): never from the wave's scratch
 __device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words, int kind, bool persist = false) {
   const int64_t w = (words + 3) & ~int64_t(3);
+  if (l.wpool) {
 #ifdef KCEP_PHASES
-  l.kw[kind] += uint64_t(w);
-#endif
-  if (l.wpool) {                                   // wave mode: one allocator for the key
+    lds_add(&l.wpool->kw[kind], (unsigned long long)w);
+#endif                                   // wave mode: one allocator for the key
     const int64_t was = int64_t(lds_add(&l.wpool->pool_words, (unsigned long long)w));
     if (l.A->max_key_words > 0 && was + w > l.A->max_key_words) { l.overflow = 1; l.cap_hit = 1; return nullptr; }
     if (!persist && l.wpool->scr && w <= l.wpool->scr_cap) {
@@ -157,7 +161,7 @@ __device__ __forceinline__ int32_t* pool_alloc(Lane& l, int64_t words, int kind,
   if (at + (unsigned long long)w > (unsigned long long)l.A->pool_cap) { l.overflow = 1; return nullptr; }
   l.pool_words += w;
 #ifdef KCEP_PHASES
-  l.kw[AK_N] += uint64_t(w);
+  if (l.wpool) lds_add(&l.wpool->kw[AK_N], (unsigned long long)w);
 #endif
   return l.A->pool + at;
 }
@@ -179,16 +183,41 @@ __device__ __forceinline__ bool regrow(Lane& l, int32_t*& a, int32_t& cap, int64
 
 // ---- stage references (real stage or Stage.newEpsilonState(src, target), Stage.java:247-251) ----
 __device__ __forceinline__ const DevStage& stg(const Lane& l, int sid) { return KCEP_PROG(l).st[sid]; }
-__device__ __forceinline__ bool is_begin(const Lane& l, int sid) { return stg(l, sid).type == ST_BEGIN_; }
+// the stage table's small fields by a lane's own stage id: in the per-pattern kernels computed from
+// immediates (jit.cpp gen_packed), not loaded from the program table (a divergent constant-memory load
+// on every evaluation's dependency chain); the built-in kernels read the DevProgram
+#ifdef KCEP_JIT
+#define ST_TYPE(l, s) ::kcep::jst_type(s)
+#define ST_NAME(l, s) ::kcep::jst_name(s)
+#define ST_SLOT(l, s) ::kcep::jst_slot(s)
+#define ST_NEDGES(l, s) ::kcep::jst_nedges(s)
+#define ST_NFOLDS(l, s) ::kcep::jst_nfolds(s)
+#define ST_OP(l, s, e) ::kcep::jst_op((s) * NFA_MAX_EDGES + (e))
+#define ST_TARGET(l, s, e) ::kcep::jst_target((s) * NFA_MAX_EDGES + (e))
+#define ST_PRED(l, s, e) ::kcep::jst_pred((s) * NFA_MAX_EDGES + (e))
+#define ST_SL(l, s, e) ::kcep::jst_sl((s) * NFA_MAX_EDGES + (e))
+#define SLOT_NAME(l, x) ::kcep::jst_slot_name(x)
+#else
+#define ST_TYPE(l, s) stg(l, s).type
+#define ST_NAME(l, s) stg(l, s).name
+#define ST_SLOT(l, s) stg(l, s).slot
+#define ST_NEDGES(l, s) stg(l, s).nedges
+#define ST_NFOLDS(l, s) stg(l, s).nfolds
+#define ST_OP(l, s, e) stg(l, s).op[e]
+#define ST_TARGET(l, s, e) stg(l, s).target[e]
+#define ST_PRED(l, s, e) stg(l, s).pred[e]
+#define ST_SL(l, s, e) stg(l, s).sl[e]
+#define SLOT_NAME(l, x) (l).P->slot_name[x]
+#endif
+__device__ __forceinline__ bool is_begin(const Lane& l, int sid) { return ST_TYPE(l, sid) == ST_BEGIN_; }
 __device__ __forceinline__ bool is_forwarding(const Lane& l, int sid, int eps) {   // ComputationStage.java:134-137
   if (eps != EPS_NONE) return true;
-  const DevStage& s = stg(l, sid);
-  return s.nedges == 1 && s.op[0] == E_PROCEED;
+  return ST_NEDGES(l, sid) == 1 && ST_OP(l, sid, 0) == E_PROCEED;
 }
 __device__ __forceinline__ bool is_fwd_final(const Lane& l, int sid, int eps) {    // :143-147
   if (!is_forwarding(l, sid, eps)) return false;
-  const int tgt = eps != EPS_NONE ? eps : stg(l, sid).target[0];
-  return stg(l, tgt).type == ST_FINAL_;
+  const int tgt = eps != EPS_NONE ? eps : ST_TARGET(l, sid, 0);
+  return ST_TYPE(l, tgt) == ST_FINAL_;
 }
 
 // ---- heap: versions and predecessor pointers ----
@@ -268,7 +297,7 @@ __device__ __forceinline__ bool dw_compatible(const Lane& l, int a, int b, int l
 __device__ __forceinline__ int32_t* node(Lane& l, int slot, int ev) {
   return l.nodes + (int64_t(ev) * KCEP_PROG(l).nslots + slot) * NW;
 }
-__device__ __forceinline__ int slot_of(const Lane& l, int sid) { return stg(l, sid).slot; }
+__device__ __forceinline__ int slot_of(const Lane& l, int sid) { return ST_SLOT(l, sid); }
 __device__ __forceinline__ bool exists(const int32_t* nd) { return nd[3] & NF_EXISTS; }
 
 __device__ __forceinline__ bool add_pred_(Lane& l, int32_t* nd, int ver, int pslot, int pev) {   // MatchedEvent.addPredecessor
@@ -721,14 +750,14 @@ __device__ __forceinline__ bool frame_enter(Lane& l, Frame& f) {
   f.nbase = l.tlen;
   uint32_t has = 0;
   const bool eps = f.cur_eps != EPS_NONE;
-  const DevStage& s = stg(l, f.cur_sid);
-  const int ne = eps ? 1 : s.nedges;
+  const int sid = f.cur_sid;
+  const int ne = eps ? 1 : ST_NEDGES(l, sid);
   for (int e = 0; e < ne; e++) {
-    const int op = eps ? E_PROCEED : s.op[e];
-    const int pc = eps ? -1 : s.pred[e];
+    const int op = eps ? E_PROCEED : ST_OP(l, sid, e);
+    const int pc = eps ? -1 : ST_PRED(l, sid, e);
     bool ok = true;
     if (pc >= 0) {
-      const int sl = s.sl[e];
+      const int sl = ST_SL(l, sid, e);
       if (sl >= 0 && !((l.sle >> sl) & 1)) {
         ok = (l.slm >> sl) & 1;
       } else {
@@ -765,15 +794,14 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
     if (f.i < f.nm) {
       const int e = f.medge[f.i++];
       const bool eps = f.cur_eps != EPS_NONE;
-      const DevStage& s = stg(l, f.cur_sid);
-      const int op = eps ? E_PROCEED : s.op[e];
-      const int target = eps ? f.cur_eps : s.target[e];
+      const int op = eps ? E_PROCEED : ST_OP(l, f.cur_sid, e);
+      const int target = eps ? f.cur_eps : ST_TARGET(l, f.cur_sid, e);
       const int ver = f.cs.ver, seq = f.cs.seq;
       if (op == E_PROCEED || op == E_SKIP_PROCEED) {                 // :222-237
         if (d + 1 >= MAXD) { l.overflow = 1; return false; }
         Frame g;
         g.cs = f.cs;
-        if (stg(l, target).name != s.name && !r_br(f.cs) && !r_ig(f.cs)) {   // isForwardingToNextStage :343-349
+        if (ST_NAME(l, target) != ST_NAME(l, f.cur_sid) && !r_br(f.cs) && !r_ig(f.cs)) {   // isForwardingToNextStage :343-349
           const int nv = dw_add_stage(l, ver);
           if (nv < 0) return false;
           g.cs = mk_run(r_sid(f.cs), r_eps(f.cs), nv, f.cs.ev, f.cs.seq, false, false);   // setVersion
@@ -841,7 +869,7 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
         if (!push_t(l, f.cs)) return false;
       }
     }
-    if (f.consumed && f.cur_eps == EPS_NONE) {                       // evaluateAggregates :319-321, :362-369
+    if (f.consumed && f.cur_eps == EPS_NONE && ST_NFOLDS(l, f.cur_sid) > 0) {   // evaluateAggregates :319-321, :362-369
       const DevStage& s = stg(l, f.cur_sid);
       for (int k = 0; k < s.nfolds; k++) {
         int32_t ct;
@@ -902,7 +930,7 @@ __device__ __forceinline__ bool emit_match(Lane& l, const Run& y) {
   o[2] = cnt;
   for (int i = 0; i < cnt; i++) {
     const int64_t q = ev_pos(l, tmp[2 * i + 1]);
-    o[3 + 3 * i] = KCEP_PROG(l).slot_name[tmp[2 * i]];
+    o[3 + 3 * i] = SLOT_NAME(l, tmp[2 * i]);
     o[4 + 3 * i] = int32_t(uint32_t(uint64_t(q)));
     o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
   }
@@ -1189,9 +1217,6 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.A = &A;
   l.P = A.P;
   l.pool_words = 0;
-#ifdef KCEP_PHASES
-  for (int i = 0; i <= AK_N; i++) l.kw[i] = 0;
-#endif
   const auto& P = KCEP_PROG(l);
   l.seg0 = A.seg_start[seg];
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
@@ -1307,8 +1332,9 @@ __device__ __forceinline__ bool record_hwm(Lane& l, int64_t g) {
 
 // Per-key results: carried state (NFAStoreImpl.put :144-147), profile, the capacity hand-off,
 // match counts.
+// prof (profiling wave kernels): the key's allocator with its phase clocks and allocation counts
 __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int64_t err_rec, int32_t live_max,
-                                        int64_t evals, uint64_t t0) {
+                                        int64_t evals, uint64_t t0, const KeyAlloc* prof = nullptr) {
   if (A.carry && !l.err && !l.overflow) {
     const int64_t at = export_state(l);
     if (at >= 0) A.res_carry[seg] = at;
@@ -1319,15 +1345,17 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
     pr[0] = live_max;
     pr[1] = evals;
     pr[2] = int64_t(wall_clock64() - t0);
-#ifdef KCEP_PHASES
+#if defined(KCEP_PHASES_LANE)
     for (int i = 0; i < 11; i++) pr[3 + i] = int64_t(l.ph[i]);
+#elif defined(KCEP_PHASES)
+    for (int i = 0; i < 11; i++) pr[3 + i] = prof ? int64_t(prof->ph[i]) : -1;
 #else
     for (int i = 0; i < 11; i++) pr[3 + i] = -1;
 #endif
     pr[14] = 0;                                                        // (reserved)
     pr[15] = l.pool_words;
 #ifdef KCEP_PHASES
-    for (int i = 0; i <= AK_N; i++) pr[16 + i] = int64_t(l.kw[i]);  // words per kind, then the pool's share
+    for (int i = 0; i <= AK_N; i++) pr[16 + i] = prof ? int64_t(prof->kw[i]) : -1;   // words per kind, the pool's share
 #else
     for (int i = 0; i <= AK_N; i++) pr[16 + i] = -1;
 #endif
@@ -1365,7 +1393,7 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
   Frame fr[MAXD];
   int64_t err_rec = -1;
   const bool proc = A.mode == CEP_MODE_PROCESSOR;
-#ifdef KCEP_PHASES
+#ifdef KCEP_PHASES_LANE
   for (int i = 0; i < 11; i++) l.ph[i] = 0;
 #endif
   int32_t live_max = l.qlen;                                         // live-run high-water mark of the key

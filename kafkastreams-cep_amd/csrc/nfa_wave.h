@@ -103,14 +103,16 @@ struct WaveShared {
   int64_t nmatch;
   KeyAlloc ka;                     // the key's allocator: its words, the wave's scratch region
   int32_t err, overflow, cap_hit;
-  int32_t* logp[GL];
-  int32_t logn[GL], errc[GL];
-  int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS];
   int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
   int32_t *arena, arena_used, arena_cap;   // the key's LDS arena, its bump pointer (re-allocations go there first), size
-  // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
-  int32_t ms_slot[GL], ms_e[GL], ms_pv[GL], ms_cnt[GL], ms_done[GL], ms_err[GL];
-  int32_t conf[2 * GL];            // stateful rounds: each lane's run sequence, whether it wrote it
+  // scratch of one phase of a record at a time (the phases never overlap): ~2.3 KB less LDS per wave
+  union {
+    struct { int32_t* logp[GL]; int32_t logn[GL], errc[GL]; } sq;   // the sequential commit's operation logs
+    struct { int32_t lastp3[NFA_MAX_SLOTS], scnt[NFA_MAX_SLOTS], sblk[NFA_MAX_SLOTS]; } pc;   // parallel commit
+    // matchConstruction: the walks waiting at a node the walks change (wave_emit_matches)
+    struct { int32_t slot[GL], e[GL], pv[GL], cnt[GL], done[GL], err[GL]; } ms;
+    int32_t conf[2 * GL];          // stateful rounds: each lane's run sequence, whether it wrote it
+  } u;
 };
 
 template <class W>
@@ -200,23 +202,23 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, 
   // (2) the current record's nodes: the last 3-arg put of a node overwrites, later 5-arg puts append
   int before = 0, total = 0;
   before = g.excl_scan(l.log_n, total);
-  for (int s = g.gl; s < ns; s += GL) { w.lastp3[s] = -1; w.scnt[s] = 0; }
+  for (int s = g.gl; s < ns; s += GL) { w.u.pc.lastp3[s] = -1; w.u.pc.scnt[s] = 0; }
   wave_sync();
   for (int k = 0; k < l.log_n; k++) {
     const int32_t* o = l.log + k * WL;
-    if ((o[0] & 0xFF) == WOP_PUT3) atomicMax(&w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)], before + k);
+    if ((o[0] & 0xFF) == WOP_PUT3) atomicMax(&w.u.pc.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)], before + k);
   }
   wave_sync();
   auto survives = [&](const int32_t* o, int gi) {
     const int kind = o[0] & 0xFF;
     if (kind == WOP_BRANCH || kind == WOP_AGG) return false;
-    const int lp = w.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)];
+    const int lp = w.u.pc.lastp3[slot_of(l, (o[0] >> 8) & 0xFF)];
     return kind == WOP_PUT3 ? gi == lp : gi > lp;
   };
   int npred = 0;
   for (int k = 0; k < l.log_n; k++) {
     const int32_t* o = l.log + k * WL;
-    if (survives(o, before + k)) { atomicAdd(&w.scnt[slot_of(l, (o[0] >> 8) & 0xFF)], 1); npred++; }
+    if (survives(o, before + k)) { atomicAdd(&w.u.pc.scnt[slot_of(l, (o[0] >> 8) & 0xFF)], 1); npred++; }
   }
   int all = 0;
   g.excl_scan(npred, all);
@@ -225,14 +227,14 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, 
   if (g.gl == 0) {
     int top = w.heap_top;
     for (int s = 0; s < ns; s++)
-      if (w.scnt[s]) { w.sblk[s] = top; top += PW * w.scnt[s]; }
+      if (w.u.pc.scnt[s]) { w.u.pc.sblk[s] = top; top += PW * w.u.pc.scnt[s]; }
     w.heap_top = top;
   }
   wave_sync();
   l.heap = w.heap;
   l.heapcap = w.heapcap;
   for (int s = 0; s < ns; s++) {                             // uniform loop over the record's slots
-    const int cnt = w.scnt[s];
+    const int cnt = w.u.pc.scnt[s];
     if (!cnt) continue;
     int mine = 0;
     for (int k = 0; k < l.log_n; k++) {
@@ -246,7 +248,7 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, 
       const int32_t* o = l.log + k * WL;
       if (!survives(o, before + k) || slot_of(l, (o[0] >> 8) & 0xFF) != s) continue;
       const int idx = ex + j++;
-      const int p = w.sblk[s] + PW * idx;
+      const int p = w.u.pc.sblk[s] + PW * idx;
       const int ver = o[3];
       const bool p3 = (o[0] & 0xFF) == WOP_PUT3;
       l.heap[p] = ver;                                       // MatchedEvent.addPredecessor
@@ -258,12 +260,12 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, 
     }
     if (g.gl == 0) {
       int32_t* nd = node(l, s, r);
-      const int last = w.sblk[s] + PW * (cnt - 1);
-      if (w.lastp3[s] >= 0 || !exists(nd)) {                 // overwritten by a 3-arg put, or created: refs 1
-        nd[0] = 1; nd[1] = w.sblk[s]; nd[2] = last; nd[3] = NF_EXISTS;
+      const int last = w.u.pc.sblk[s] + PW * (cnt - 1);
+      if (w.u.pc.lastp3[s] >= 0 || !exists(nd)) {                 // overwritten by a 3-arg put, or created: refs 1
+        nd[0] = 1; nd[1] = w.u.pc.sblk[s]; nd[2] = last; nd[3] = NF_EXISTS;
       } else {                                               // made by an earlier round: appended to
-        if (nd[1] < 0) nd[1] = w.sblk[s];
-        else l.heap[nd[2] + 3] = w.sblk[s];
+        if (nd[1] < 0) nd[1] = w.u.pc.sblk[s];
+        else l.heap[nd[2] + 3] = w.u.pc.sblk[s];
         nd[2] = last;
       }
     }
@@ -281,7 +283,6 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, 
 // since none is left above the frontier.  The result is the sequential construction's.
 template <int GL>
 __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int flen) {
-  const auto& P = KCEP_PROG(l);
   const int lane = g.gl;
   const int64_t pos = l.A->base + l.g;
   const int maxp = l.nev + 1;                                  // one node per event at most
@@ -319,21 +320,21 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, co
       }
       const uint64_t mm = g.ballot(at && !my_err && mut);
       if (mm) {                                                // changing nodes: lane 0, in walk order
-        w.ms_slot[lane] = slot; w.ms_e[lane] = e; w.ms_pv[lane] = pv; w.ms_cnt[lane] = cnt; w.ms_done[lane] = done;
-        w.ms_err[lane] = my_err;
+        w.u.ms.slot[lane] = slot; w.u.ms.e[lane] = e; w.u.ms.pv[lane] = pv; w.u.ms.cnt[lane] = cnt; w.u.ms.done[lane] = done;
+        w.u.ms.err[lane] = my_err;
         wave_sync();
         if (lane == 0) {
           for (uint64_t m = mm; m; m &= m - 1) {
             const int j = __builtin_ctzll(m);
-            const int sj = w.ms_slot[j], ej = w.ms_e[j], c = w.ms_cnt[j];
+            const int sj = w.u.ms.slot[j], ej = w.u.ms.e[j], c = w.u.ms.cnt[j];
             int32_t* nd = node(l, sj, ej);
-            if (!exists(nd)) { w.ms_err[j] = CEP_E_NPE; continue; }
+            if (!exists(nd)) { w.u.ms.err[j] = CEP_E_NPE; continue; }
             int32_t* pj = paths + j * 2 * maxp;
             pj[2 * c] = sj; pj[2 * c + 1] = ej;
-            w.ms_cnt[j] = c + 1;
+            w.u.ms.cnt[j] = c + 1;
             const bool single = nd[1] < 0 || l.heap[nd[1] + 3] < 0;
             int pp = -1;
-            const int p = first_compatible(l, nd, w.ms_pv[j], &pp);
+            const int p = first_compatible(l, nd, w.u.ms.pv[j], &pp);
             if (p >= 0) {                                      // refs_left == 0: removePredecessor + put
               nd[0] = 0;
               const int nx = l.heap[p + 3];
@@ -343,14 +344,14 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, co
             } else if (single) {
               nd[3] &= ~NF_EXISTS;                             // delete
             }
-            if (p < 0 || l.heap[p + 1] < 0) w.ms_done[j] = 1;
-            else { w.ms_pv[j] = l.heap[p]; w.ms_slot[j] = l.heap[p + 1]; w.ms_e[j] = l.heap[p + 2]; }
+            if (p < 0 || l.heap[p + 1] < 0) w.u.ms.done[j] = 1;
+            else { w.u.ms.pv[j] = l.heap[p]; w.u.ms.slot[j] = l.heap[p + 1]; w.u.ms.e[j] = l.heap[p + 2]; }
           }
         }
         wave_sync();
         if ((mm >> lane) & 1) {
-          slot = w.ms_slot[lane]; e = w.ms_e[lane]; pv = w.ms_pv[lane]; cnt = w.ms_cnt[lane];
-          done = w.ms_done[lane]; my_err = w.ms_err[lane];
+          slot = w.u.ms.slot[lane]; e = w.u.ms.e[lane]; pv = w.u.ms.pv[lane]; cnt = w.u.ms.cnt[lane];
+          done = w.u.ms.done[lane]; my_err = w.u.ms.err[lane];
         }
       }
     }
@@ -379,7 +380,7 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, co
       o[2] = cnt;
       for (int i = 0; i < cnt; i++) {
         const int64_t q = ev_pos(l, path[2 * i + 1]);
-        o[3 + 3 * i] = P.slot_name[path[2 * i]];
+        o[3 + 3 * i] = SLOT_NAME(l, path[2 * i]);
         o[4 + 3 * i] = int32_t(uint32_t(uint64_t(q)));
         o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
       }
@@ -453,7 +454,7 @@ __device__ __forceinline__ bool wave_round_conflict(const Lane& l, int32_t* conf
 // evaluation rounds, buffer commit, run numbering + queue placement, matchConstruction
 #ifdef KCEP_PHASES
 #define KWP_MARK(t) const uint64_t t = clock64()
-#define KWP_ADD(i, t) l.ph[i] += clock64() - t
+#define KWP_ADD(i, t) do { if (lane == 0) w.ka.ph[i] += clock64() - t; } while (0)
 #else
 #define KWP_MARK(t)
 #define KWP_ADD(i, t)
@@ -475,6 +476,9 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
     w.ka.scr_top = 0;
     w.ka.scr = scr;
     w.ka.scr_cap = scr ? A.scratch_words : 0;
+#ifdef KCEP_PHASES
+    for (int i = 0; i <= AK_N; i++) w.ka.kw[i] = 0;
+#endif
     ok = key_begin(l, A, seg, s_arena, arena_words, &w.ka) ? 1 : 0;
     if (ok) {
       lane_to_ws(w, l);
@@ -491,9 +495,6 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
     l.seg0 = A.seg_start[seg];
     l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
     l.wave = 0; l.cap_hit = 0;
-#ifdef KCEP_PHASES
-    for (int i = 0; i <= AK_N; i++) l.kw[i] = 0;
-#endif
   }
   l.wpool = &w.ka;
   // every lane: the key's fixed shape (lane 0's key_begin set it)
@@ -522,7 +523,8 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
   int64_t err_rec = -1;
   const bool proc = A.mode == CEP_MODE_PROCESSOR;
 #ifdef KCEP_PHASES
-  for (int i = 0; i < 11; i++) l.ph[i] = 0;
+  if (lane == 0)
+    for (int i = 0; i < 11; i++) w.ka.ph[i] = 0;
 #endif
   int32_t live_max = w.qlen;
   int64_t evals = 0;
@@ -546,18 +548,23 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
       const int k = x & (NW - 1);
       l.nodes[(int64_t(r) * ns) * NW + x] = (k == 1 || k == 2) ? -1 : 0;
     }
+    KWP_ADD(0, t_rec);
+    KWP_MARK(t_adm);
     if (proc) {
       if (!record_admitted(l, g)) { wave_sync(); continue; }
       for (int k = lane; k < w.qlen; k += GL) l.qa[4 * k] &= ~(1 << 17);   // isIgnored not serialised (Q3)
     }
     wave_sync();
+    KWP_ADD(5, t_adm);
+    KWP_MARK(t_eo);
     eval_event_only(l);
     const int n = w.qlen;
     evals += n;
     if (lane == 0) { l.rec_out_top = w.out_top; l.rec_nmatch = w.nmatch; }
     int qn = 0, flen = 0;
-    KWP_ADD(0, t_rec);
+    KWP_ADD(6, t_eo);
     for (int base = 0; base < n && !w.err && !w.overflow; base += GL) {
+      KWP_MARK(t_rp);
       const int my = base + lane;
       const bool act = my < n;
       Run run{0, 0, 0, 0};
@@ -571,7 +578,8 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
       int jj = 0;                                              // sequential mode: the lane evaluating
       uint64_t emask = 0, dmask = 0;
       bool err_lane = false;
-      KWP_MARK(t_ev);
+      KWP_ADD(7, t_rp);
+      KWP_MARK(t_ev2);
       for (;;) {
         // one evaluation pass: every lane its run with logged side effects (parallel), or -- for a
         // stateful round that conflicts (wave_round_conflict) -- lane jj alone with the lane kernel's
@@ -621,7 +629,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
         dmask = gp.ballot(dead);
         // a conflict is checked before the errors: a run may throw on a state an earlier run of the
         // round would have folded first
-        if (AGG && A.wave_agg && wave_round_conflict(l, w.conf, gp, act, run.seq, dmask)) {
+        if (AGG && A.wave_agg && wave_round_conflict(l, w.u.conf, gp, act, run.seq, dmask)) {
           seqd = true;
           l.tlen = 0; l.log_n = 0; l.nph = 0;                  // the parallel pass is discarded
           continue;
@@ -629,7 +637,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
         break;
       }
       wave_sync();
-      KWP_ADD(1, t_ev);
+      KWP_ADD(1, t_ev2);
       if (w.overflow) break;
       // commit in queue order
       KWP_MARK(t_cm);
@@ -641,16 +649,16 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
         if (lane == 0 && e) w.err = e;
         wave_sync();
       } else {
-        w.logp[lane] = l.log;
-        w.logn[lane] = l.log_n;
-        w.errc[lane] = err_lane ? l.err : 0;
+        w.u.sq.logp[lane] = l.log;
+        w.u.sq.logn[lane] = l.log_n;
+        w.u.sq.errc[lane] = err_lane ? l.err : 0;
         wave_sync();
         if (lane == 0) {                                       // the reference's order, sequentially
           ws_to_lane(l, w);
           l.err = 0; l.overflow = 0;
           for (int j = 0; j < nact && !l.err && !l.overflow; j++) {
-            const int32_t* lg = w.logp[j];
-            for (int k = 0; k < w.logn[j] && !l.err && !l.overflow; k++) {
+            const int32_t* lg = w.u.sq.logp[j];
+            for (int k = 0; k < w.u.sq.logn[j] && !l.err && !l.overflow; k++) {
               const int32_t* o = lg + k * WL;
               const int kind = o[0] & 0xFF, sid = (o[0] >> 8) & 0xFF, psid = (o[0] >> 16) & 0xFF;
               if (kind == WOP_PUT5) buf_put5(l, sid, o[1], psid, o[2], o[3]);
@@ -658,7 +666,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
               else if (kind == WOP_BRANCH) buf_branch(l, sid, o[1], o[3]);
             }
             if (l.err || l.overflow) break;
-            if ((emask >> j) & 1) { l.err = w.errc[j]; break; }
+            if ((emask >> j) & 1) { l.err = w.u.sq.errc[j]; break; }
             if ((dmask >> j) & 1) {                            // removePattern (:160-163)
               const int4 x = reinterpret_cast<const int4*>(l.qa)[base + j];
               buf_peek(l, x.x & 0xFF, x.z, x.y, true, nullptr, 0);
@@ -688,6 +696,8 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
       int tf = 0, tq = 0;
       const int ef = gp.excl_scan(nf, tf), eq = gp.excl_scan(nq, tq);
       wave_sync();
+      KWP_ADD(3, t_pl);
+      KWP_MARK(t_pl2);
       if (lane == 0) w.runs += nrun;
       // room in the next queue and the final list
       if (qn + tq > w.qb_cap) {
@@ -712,10 +722,11 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
       qn += tq;
       flen += tf;
       wave_sync();
-      KWP_ADD(3, t_pl);
+      KWP_ADD(10, t_pl2);
     }
     if (w.err) { err_rec = A.base + g; break; }
     if (w.overflow) break;
+    KWP_MARK(t_end);
     // swap the queues; matchConstruction (:151-158); the high-water mark on lane 0
     if (lane == 0) {
       int32_t* t = w.qa; w.qa = w.qb; w.qb = t;
@@ -735,20 +746,17 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
       lane_to_ws(w, l);
     }
     wave_sync();
+    KWP_ADD(8, t_end);
     if (w.err) { err_rec = A.base + g; break; }
     live_max = w.qlen > live_max ? w.qlen : live_max;
   }
   wave_sync();
-#ifdef KCEP_PHASES
-  for (int i = 0; i <= AK_N; i++)                                // the key's allocations, summed over its lanes
-    for (int d = GL / 2; d > 0; d >>= 1) l.kw[i] += __shfl_xor(l.kw[i], d, GL);
-#endif
   if (lane == 0) {
     ws_to_lane(l, w);
     l.pool_words = int64_t(w.ka.pool_words);
     l.wpool = nullptr;
     l.wave = 0;
-    key_end(l, A, seg, err_rec, live_max, evals, t0);
+    key_end(l, A, seg, err_rec, live_max, evals, t0, &w.ka);
   }
 }
 

@@ -40,7 +40,15 @@ ws = prof[:, 16]
 print("workspace words: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %d; heaviest key %d" %
       (ws.mean(), np.median(ws), np.percentile(ws, 90), np.percentile(ws, 99), ws.max(), ws[o[0]]))
 ph = prof[:, 4:15].astype(np.float64)
-if (ph >= 0).all():
+if (ph >= 0).all() and "--wave-phases" in sys.argv:   # the wave kernel's record loop (nfa_wave.h KWP_*)
+    names = ["nodes init", "evaluation", "commit", "placement scans", "matchConstruction", "admit+ignored",
+             "event-only preds", "round prologue", "record end (incl. matchConstruction)", "-", "placement writes"]
+    tot = ph.sum(axis=0)
+    full = cyc.sum() * 1e-6 * 2.1e9 / 1e0                  # (shader clocks ~ 2.1 GHz; for scale only)
+    print("wave record-loop clocks (sum over keys):", {nm: f"{t:.3e}" for nm, t in zip(names, tot)})
+    den = tot[[0, 1, 2, 3, 5, 6, 7, 8, 10]].sum()
+    print("shares:", {nm: round(float(t / den), 3) for nm, t in zip(names, tot) if nm != "-"})
+elif (ph >= 0).all():
     tot = ph.sum(axis=0)
     print("phase clock sums:", [f"{x:.3e}" for x in tot[:8]], "share:",
           [round(float(x / max(1.0, tot[:5].sum())), 3) for x in tot[:5]])
