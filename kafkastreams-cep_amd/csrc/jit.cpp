@@ -431,9 +431,10 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   const int waves = wenv ? std::min(8, std::max(1, atoi(wenv))) : 2;
   // the same for the wave kernel (KCEP_NFA_WAVE_OCC)
   const char* oenv = getenv("KCEP_NFA_WAVE_OCC");
-  // r05: 4 (C4 step 5.85 vs 6.40 ms at 3, with the stage fields as immediates and the phase-local LDS
-  // arrays unioned: 128 VGPRs, ~9.9 KB of LDS per wave); r02: 2: 13.3, 3: 10.8, 4: 11.8 ms
-  const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 4;
+  // 3 waves per SIMD (166 VGPRs, no spills).  r05, C4 with 16-byte frames: 4 waves (128 VGPRs) runs the
+  // kernel in 4.67 vs 4.92 ms but spills ~50 VGPRs, whose scratch lines reach HBM: 5.5 GB per launch
+  // against 0.28 GB (profiles/r05_c4_occupancy.txt); r02: 2: 13.3, 3: 10.8, 4: 11.8 ms
+  const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 3;
   // LDS arena words of the wave kernel's key workspace (KCEP_WAVE_ARENA, tuning only)
   const char* aenv = getenv("KCEP_WAVE_ARENA");
   if (aenv) o += "#define WAVE_ARENA " + std::to_string(std::min(8192, std::max(4, atoi(aenv)))) + "\n";

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void nf
 // one key per wave, one queued run per lane (nfa_wave.h); AGG: patterns with aggregates or
 // SequenceMatchers.  A persistent grid (nfa_wave_grid)
 template <bool AGG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void nfa_wave_kernel(NfaArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nfa_wave_kernel(NfaArgs A) {
   nfa_wave_body<AGG>(A);
 }
 

@@ -101,7 +101,6 @@ struct Lane {
   uint64_t slm, sle;           // event-only edge predicates on record r: values / deferred errors
   int64_t pool_words;          // taken from the pool (profile)
   // ---- wave mode (nfa_wave.h: one key per wave, one queued run per lane) ----
-  int32_t wave;                // 1: heap allocations are shared by the wave, buffer operations are logged
   int32_t* wtop;               // wave: the key's heap top, in LDS
   int32_t* log;                // wave: this lane's run's deferred buffer operations, WL words each
   int32_t log_cap, log_n;
@@ -221,8 +220,12 @@ __device__ __forceinline__ bool is_fwd_final(const Lane& l, int sid, int eps) { 
 }
 
 // ---- heap: versions and predecessor pointers ----
+// W: the wave kernel's parallel evaluation (nfa_wave.h) -- shared allocations and logged buffer
+// operations; a compile-time mode, so that the wave's workspace pointers stay wave-uniform (scalar
+// registers) through an evaluation instead of merging with the lane path's re-allocations
+template <bool W = false>
 __device__ __forceinline__ int heap_alloc(Lane& l, int words) {
-  if (l.wave) {                                    // versions are immutable: any allocation order will do
+  if constexpr (W) {                                    // versions are immutable: any allocation order will do
     const int at = lds_add(l.wtop, words);
     if (at + words > l.heapcap) { l.wgrow = 1; l.overflow = 1; return -1; }
     return at;
@@ -243,20 +246,22 @@ __device__ __forceinline__ void dw_copy(int32_t* h, int dst, int src, int len) {
   }
   for (; i < len; i++) h[dst + i] = h[src + i];
 }
+template <bool W>
 __device__ __forceinline__ int dw_add_stage_(Lane& l, int v) {            // DeweyVersion.addStage :95-97
   const int len = l.heap[v];
-  const int n = heap_alloc(l, len + 2);
+  const int n = heap_alloc<W>(l, len + 2);
   if (n < 0) return -1;
   l.heap[n] = len + 1;
   dw_copy(l.heap, n + 1, v + 1, len);
   l.heap[n + 1 + len] = 0;
   return n;
 }
+template <bool W>
 __device__ __forceinline__ int dw_add_run_(Lane& l, int v, int off) {     // DeweyVersion.addRun :62-67
   const int len = l.heap[v];
   const int idx = len - off;
   if (idx < 0 || idx >= len) { l.err = CEP_E_INDEX; return -1; }
-  const int n = heap_alloc(l, len + 1);
+  const int n = heap_alloc<W>(l, len + 1);
   if (n < 0) return -1;
   const int32_t bumped = int32_t(uint32_t(l.heap[v + 1 + idx]) + 1u);
   l.heap[n] = len;
@@ -264,15 +269,17 @@ __device__ __forceinline__ int dw_add_run_(Lane& l, int v, int off) {     // Dew
   l.heap[n + 1 + idx] = bumped;
   return n;
 }
+template <bool W = false>
 __device__ __forceinline__ int dw_add_stage(Lane& l, int v) {
   KPH_BEGIN(l, 7);
-  const int n = dw_add_stage_(l, v);
+  const int n = dw_add_stage_<W>(l, v);
   KPH_END(l, 7);
   return n;
 }
+template <bool W = false>
 __device__ __forceinline__ int dw_add_run(Lane& l, int v, int off) {
   KPH_BEGIN(l, 7);
-  const int n = dw_add_run_(l, v, off);
+  const int n = dw_add_run_<W>(l, v, off);
   KPH_END(l, 7);
   return n;
 }
@@ -332,9 +339,10 @@ __device__ __forceinline__ void wlog(Lane& l, int kind, int sid, int psid, int e
   l.log_n++;
 }
 // put 5-arg (SharedVersionedBufferStoreImpl.java:101-126)
+template <bool W = false>
 __device__ __forceinline__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_sid, int pev, int ver) {
   if (pev < 0) { l.err = CEP_E_NPE; return; }
-  if (l.wave) { wlog(l, WOP_PUT5, cur_sid, prev_sid, ev, pev, ver); return; }
+  if constexpr (W) { wlog(l, WOP_PUT5, cur_sid, prev_sid, ev, pev, ver); return; }
   const int ps = slot_of(l, prev_sid);
   if (!exists(node(l, ps, pev))) { l.err = CEP_E_ILLEGAL_STATE; return; }
   int32_t* c = node(l, slot_of(l, cur_sid), ev);
@@ -342,8 +350,9 @@ __device__ __forceinline__ void buf_put5(Lane& l, int cur_sid, int ev, int prev_
   add_pred(l, c, ver, ps, pev);
 }
 // put 3-arg (:149-157): a fresh node overwrites
+template <bool W = false>
 __device__ __forceinline__ void buf_put3(Lane& l, int cur_sid, int ev, int ver) {
-  if (l.wave) { wlog(l, WOP_PUT3, cur_sid, 0xFF, ev, -1, ver); return; }
+  if constexpr (W) { wlog(l, WOP_PUT3, cur_sid, 0xFF, ev, -1, ver); return; }
   int32_t* c = node(l, slot_of(l, cur_sid), ev);
   c[0] = 1; c[1] = -1; c[2] = -1; c[3] = NF_EXISTS;
   add_pred(l, c, ver, -1, 0);
@@ -365,9 +374,10 @@ __device__ __forceinline__ int first_compatible(const Lane& l, const int32_t* nd
   return p;
 }
 // branch (:132-142)
+template <bool W = false>
 __device__ __forceinline__ void buf_branch(Lane& l, int sid, int ev, int ver) {
   if (ev < 0) { l.err = CEP_E_NPE; return; }
-  if (l.wave) { wlog(l, WOP_BRANCH, sid, 0xFF, ev, ev, ver); return; }
+  if constexpr (W) { wlog(l, WOP_BRANCH, sid, 0xFF, ev, ev, ver); return; }
   int slot = slot_of(l, sid), e = ev, pv = ver;
   for (;;) {
     int32_t* nd = node(l, slot, e);
@@ -428,8 +438,9 @@ __device__ __forceinline__ int32_t* agg(Lane& l, int state, int seq) {
 // round evaluates against the aggregates as they were before it; a lane's writes are logged (WOP_AGG:
 // state, boxed type, sequence -- a placeholder for a sequence created in the round -- and the value)
 // and read back by the same lane first, then applied in queue order after the round (nfa_wave.h).
+template <bool W = false>
 __device__ __forceinline__ bool agg_read(Lane& l, int state, int seq, int32_t& tag, int64_t& v) {
-  if (l.wave) {
+  if constexpr (W) {
     for (int k = l.log_n - 1; k >= 0; k--) {
       const int32_t* o = l.log + k * WL;
       if ((o[0] & 0xFF) == WOP_AGG && ((o[0] >> 8) & 0xFF) == state && o[1] == seq) {
@@ -450,9 +461,10 @@ __device__ __forceinline__ bool agg_read(Lane& l, int state, int seq, int32_t& t
   v = int64_t(uint32_t(e[1])) | (int64_t(e[2]) << 32);
   return true;
 }
+template <bool W = false>
 __device__ __forceinline__ bool agg_write(Lane& l, int state, int seq, int32_t tag, int64_t v) {
   const int32_t lo = int32_t(uint32_t(uint64_t(v))), hi = int32_t(uint32_t(uint64_t(v) >> 32));
-  if (l.wave) {
+  if constexpr (W) {
     const int n0 = l.log_n;
     wlog(l, WOP_AGG, state, tag, seq, lo, hi);
     return l.log_n > n0;
@@ -505,10 +517,11 @@ struct Ctx {
 
 // scratch for a partial sequence's walk: above the heap top (wave mode: drawn from the shared heap,
 // since the other lanes allocate concurrently)
+template <bool W = false>
 __device__ __forceinline__ int32_t* seq_scratch(Lane& l) {
   const int need = 2 * l.nev + 2;
-  if (l.wave) {
-    const int at = heap_alloc(l, need);
+  if constexpr (W) {
+    const int at = heap_alloc<W>(l, need);
     return at < 0 ? nullptr : l.heap + at;
   }
   if (l.heap_top + need > l.heapcap && !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need, AK_HEAP))
@@ -565,9 +578,10 @@ __device__ __forceinline__ void seq_visit(const Lane& l, const int32_t* tmp, int
 
 // SequenceMatcher: average of a column over buffer.get(Matched(prev, prevEvent), version)
 // (SequenceMatcher.java:21-26), with Sequence's per-stage TreeSet de-duplication.
+template <bool W = false>
 __device__ __forceinline__ bool seq_avg(Lane& l, const Ctx& c, int col, int64_t& out) {
   if (c.prev_sid < 0 || c.pev < 0) { l.err = CEP_E_NPE; return false; }
-  int32_t* tmp = seq_scratch(l);                     // the walk visits at most one node per event
+  int32_t* tmp = seq_scratch<W>(l);                     // the walk visits at most one node per event
   if (!tmp) return false;
   const int cnt = buf_peek(l, c.prev_sid, c.pev, c.ver, false, tmp, l.nev + 1);
   if (cnt < 0) return false;
@@ -603,9 +617,10 @@ __device__ __forceinline__ int ev_cmp(const Lane& l, int a, int b) {
   else { x = ev_off(l, a); y = ev_off(l, b); }
   return x < y ? -1 : x > y ? 1 : 0;
 }
+template <bool W = false>
 __device__ __forceinline__ bool seq_agg(Lane& l, const Ctx& c, int kind, int col, int stage, int64_t& out) {
   if (c.prev_sid < 0 || c.pev < 0) { l.err = CEP_E_NPE; return false; }
-  int32_t* tmp = seq_scratch(l);
+  int32_t* tmp = seq_scratch<W>(l);
   if (!tmp) return false;
   const int cnt = buf_peek(l, c.prev_sid, c.pev, c.ver, false, tmp, l.nev + 1);
   if (cnt < 0) return false;
@@ -658,6 +673,7 @@ __device__ __forceinline__ bool seq_agg(Lane& l, const Ctx& c, int kind, int col
 
 // interpreter environment of the general kernel: the lane's current record,
 // the evaluating run's aggregates and partial sequence
+template <bool W = false>
 struct LaneEnv {
   Lane& l;
   const Ctx& c;
@@ -670,17 +686,18 @@ struct LaneEnv {
   __device__ __forceinline__ int64_t off() { return b_off(l, l.g); }
   __device__ __forceinline__ int64_t part() { return b_part(l, l.g); }
   __device__ __forceinline__ int32_t topic() { return b_topic(l, l.g); }
-  __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) { return agg_read(l, idx, c.seq, tag, v); }
-  __device__ __forceinline__ bool seq_avg(int col, int64_t& v) { return kcep::seq_avg(l, c, col, v); }
+  __device__ __forceinline__ bool state(int idx, int32_t& tag, int64_t& v) { return agg_read<W>(l, idx, c.seq, tag, v); }
+  __device__ __forceinline__ bool seq_avg(int col, int64_t& v) { return kcep::seq_avg<W>(l, c, col, v); }
   __device__ __forceinline__ bool seq_agg(int kind, int col, int stage, int64_t& v) {
-    return kcep::seq_agg(l, c, kind, col, stage, v);
+    return kcep::seq_agg<W>(l, c, kind, col, stage, v);
   }
   __device__ __forceinline__ void fail(int code) { l.err = code; }
 };
 
 // bytecode interpreter over the current record; returns false on error (l.err / l.overflow set)
+template <bool W = false>
 __device__ __forceinline__ bool run_code(Lane& l, int pc, const Ctx& c, int64_t& result) {
-  LaneEnv env{l, c, c.in_fold, c.curr_tag, c.curr};
+  LaneEnv<W> env{l, c, c.in_fold, c.curr_tag, c.curr};
 #ifdef KCEP_JIT
   return jit_eval(pc, env, result);
 #else
@@ -699,7 +716,7 @@ __device__ __forceinline__ void eval_event_only(Lane& l) {
   KCEP_UNROLL
   for (int i = 0; i < nsl; i++) {                  // uniform: lock-step interpreter, scalar code fetches
     const Ctx c{0, -1, -1, -1, false, 0, 0};
-    LaneEnv env{l, c, false, 0, 0};
+    LaneEnv<false> env{l, c, false, 0, 0};
     int64_t v = 0;
     const int e0 = l.err, o0 = l.overflow;
 #ifdef KCEP_JIT
@@ -718,8 +735,9 @@ __device__ __forceinline__ void eval_event_only(Lane& l) {
 
 // NFA.runs++ (NFA.java:297, :331).  Wave mode: a placeholder -(2 + k) for the lane's k-th increment;
 // the wave numbers them in queue order after the round (nfa_wave.h wave_fix_seq)
+template <bool W = false>
 __device__ __forceinline__ int next_seq(Lane& l) {
-  if (l.wave) return -(2 + l.nph++);
+  if constexpr (W) return -(2 + l.nph++);
   return ++l.runs;
 }
 
@@ -735,170 +753,196 @@ __device__ __forceinline__ bool push_run(Lane& l, int32_t*& q, int32_t& cap_runs
 }
 __device__ __forceinline__ bool push_t(Lane& l, const Run& x) { return push_run(l, l.tq, l.tq_cap, l.tlen, x); }
 
+// One level of NFA.evaluate's PROCEED/SKIP_PROCEED recursion (ComputationContext).  16 bytes: the
+// suspended parents sit in private memory (fr[], scratch), so their size is the kernel's scratch
+// footprint (with a 44-byte frame C4's wave kernel wrote ~0.4-2.8 GB of scratch lines back to HBM per
+// launch, depending on occupancy).  A context's stage, event and sequence are always the run's own
+// (NFA.java:222-237 only sets the version), so a frame keeps the version and two flags of it.
+constexpr uint32_t FR_NONE = 0xFF;     // prev stage: none (Stage.newEpsilonState(null, ...))
 struct Frame {
-  Run cs;                          // ComputationContext.computationStage
-  int16_t cur_sid, cur_eps, prev_sid, prev_eps;
-  int8_t medge[NFA_MAX_EDGES];
-  int8_t nm, i, pending;
-  uint8_t branching, ignored, consumed, proceed;
-  int32_t nbase, before;
+  int32_t ver;                 // the context's ComputationStage version
+  uint32_t st;                 // cur stage | cur epsilon target << 8 | prev stage << 16 | prev epsilon << 24
+  uint32_t fl;                 // bits 0-3 matched edges not taken yet, 4 branching, 5 ignored, 6 consumed,
+                               // 7 proceed, 8 / 9 the context stage's isBranching / isIgnored, 10-31 nbase
+  int32_t before;              // tq length when the child context was entered
+  __device__ __forceinline__ int cur_sid() const { return int(st & 0xFF); }
+  __device__ __forceinline__ int cur_eps() const { return int((st >> 8) & 0xFF); }
+  __device__ __forceinline__ int prev_sid() const { const uint32_t p = (st >> 16) & 0xFF; return p == FR_NONE ? -1 : int(p); }
+  __device__ __forceinline__ int prev_eps() const { return int(st >> 24); }
+  __device__ __forceinline__ bool flag(int b) const { return (fl >> b) & 1u; }
+  __device__ __forceinline__ void set(int b) { fl |= 1u << b; }
+  __device__ __forceinline__ int nbase() const { return int(fl >> 10); }
 };
+enum { FB_BRANCHING = 4, FB_IGNORED = 5, FB_CONSUMED = 6, FB_PROCEED = 7, FB_CBR = 8, FB_CIG = 9 };
+constexpr int FR_MAX_NBASE = 1 << 22;
+__device__ __forceinline__ uint32_t fr_st(int cur, int eps, int prev, int peps) {
+  return uint32_t(cur) | (uint32_t(eps) << 8) | (uint32_t(prev < 0 ? FR_NONE : uint32_t(prev)) << 16) | (uint32_t(peps) << 24);
+}
+// the context's ComputationStage: the run's stage, epsilon target, event and sequence, the frame's version
+__device__ __forceinline__ Run fr_cs(const Frame& f, const Run& run) {
+  return mk_run(r_sid(run), r_eps(run), f.ver, run.ev, run.seq, f.flag(FB_CBR), f.flag(FB_CIG));
+}
 
-// frame entry: matchEdgesAndGet (NFA.java:371-384) + isBranching (:392-397)
-__device__ __forceinline__ bool frame_enter(Lane& l, Frame& f) {
-  f.nm = 0; f.i = 0; f.pending = 0; f.consumed = 0; f.proceed = 0;
-  f.nbase = l.tlen;
-  uint32_t has = 0;
-  const bool eps = f.cur_eps != EPS_NONE;
-  const int sid = f.cur_sid;
-  const int ne = eps ? 1 : ST_NEDGES(l, sid);
+// frame entry: matchEdgesAndGet (NFA.java:371-384) + isBranching (:392-397); keeps f's stage, version
+// and context flags, resets the rest
+template <bool W>
+__device__ __forceinline__ bool frame_enter(Lane& l, Frame& f, const Run& run) {
+  if (l.tlen >= FR_MAX_NBASE) { l.overflow = 1; return false; }
+  f.fl = (f.fl & ((1u << FB_CBR) | (1u << FB_CIG))) | (uint32_t(l.tlen) << 10);
+  uint32_t has = 0, rem = 0;
+  const int cur = f.cur_sid(), ceps = f.cur_eps();
+  const bool eps = ceps != EPS_NONE;
+  const int ne = eps ? 1 : ST_NEDGES(l, cur);
   for (int e = 0; e < ne; e++) {
-    const int op = eps ? E_PROCEED : ST_OP(l, sid, e);
-    const int pc = eps ? -1 : ST_PRED(l, sid, e);
+    const int op = eps ? E_PROCEED : ST_OP(l, cur, e);
+    const int pc = eps ? -1 : ST_PRED(l, cur, e);
     bool ok = true;
     if (pc >= 0) {
-      const int sl = ST_SL(l, sid, e);
+      const int sl = ST_SL(l, cur, e);
       if (sl >= 0 && !((l.sle >> sl) & 1)) {
         ok = (l.slm >> sl) & 1;
       } else {
-        Ctx c{f.cs.seq, f.prev_sid >= 0 ? int(f.prev_sid) : -1, f.cs.ev, f.cs.ver, false, 0, 0};
+        Ctx c{run.seq, f.prev_sid(), run.ev, f.ver, false, 0, 0};
         int64_t v;
         KPH_BEGIN(l, 1);
-        const bool good = run_code(l, pc, c, v);
+        const bool good = run_code<W>(l, pc, c, v);
         KPH_END(l, 1);
         if (!good) return false;
         ok = v != 0;
       }
     }
-    if (ok) { f.medge[f.nm++] = int8_t(e); has |= 1u << op; }
+    if (ok) { rem |= 1u << e; has |= 1u << op; }
   }
   auto H = [&](int o) { return (has >> o) & 1u; };
-  f.branching = (H(E_PROCEED) && H(E_TAKE)) || (H(E_IGNORE) && H(E_TAKE)) || (H(E_IGNORE) && H(E_BEGIN)) ||
-                (H(E_IGNORE) && H(E_PROCEED));
-  f.ignored = H(E_IGNORE);
+  const bool branching = (H(E_PROCEED) && H(E_TAKE)) || (H(E_IGNORE) && H(E_TAKE)) || (H(E_IGNORE) && H(E_BEGIN)) ||
+                         (H(E_IGNORE) && H(E_PROCEED));
+  f.fl |= rem | (uint32_t(branching) << FB_BRANCHING) | (uint32_t(H(E_IGNORE)) << FB_IGNORED);
   return true;
 }
 
-// NFA.evaluate (NFA.java:190-341) for one run; results appended to tq
+// NFA.evaluate (NFA.java:190-341) for one run; results appended to tq.  W: the wave kernel's parallel
+// pass (logged buffer operations, shared heap, run-counter placeholders)
+template <bool W = false>
 __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
   // the current frame lives in registers; fr[] (scratch) holds only the suspended parents
   int d = 0;
   Frame f;
-  f.cs = run;
-  f.cur_sid = int16_t(r_sid(run));
-  f.cur_eps = int16_t(r_eps(run));
-  f.prev_sid = -1;
-  f.prev_eps = EPS_NONE;
-  if (!frame_enter(l, f)) return false;
+  f.ver = run.ver;
+  f.st = fr_st(r_sid(run), r_eps(run), -1, EPS_NONE);
+  f.fl = (uint32_t(r_br(run)) << FB_CBR) | (uint32_t(r_ig(run)) << FB_CIG);
+  f.before = 0;
+  if (!frame_enter<W>(l, f, run)) return false;
   for (;;) {
-    if (f.i < f.nm) {
-      const int e = f.medge[f.i++];
-      const bool eps = f.cur_eps != EPS_NONE;
-      const int op = eps ? E_PROCEED : ST_OP(l, f.cur_sid, e);
-      const int target = eps ? f.cur_eps : ST_TARGET(l, f.cur_sid, e);
-      const int ver = f.cs.ver, seq = f.cs.seq;
+    if (f.fl & 0xFu) {                                               // the next matched edge, in edge order
+      const int e = __builtin_ctz(f.fl & 0xFu);
+      f.fl &= ~(1u << e);
+      const int cur = f.cur_sid(), ceps = f.cur_eps();
+      const bool eps = ceps != EPS_NONE;
+      const int op = eps ? E_PROCEED : ST_OP(l, cur, e);
+      const int target = eps ? ceps : ST_TARGET(l, cur, e);
+      const int ver = f.ver, seq = run.seq;
       if (op == E_PROCEED || op == E_SKIP_PROCEED) {                 // :222-237
         if (d + 1 >= MAXD) { l.overflow = 1; return false; }
         Frame g;
-        g.cs = f.cs;
-        if (ST_NAME(l, target) != ST_NAME(l, f.cur_sid) && !r_br(f.cs) && !r_ig(f.cs)) {   // isForwardingToNextStage :343-349
-          const int nv = dw_add_stage(l, ver);
+        g.ver = f.ver;
+        g.fl = f.fl & ((1u << FB_CBR) | (1u << FB_CIG));
+        if (ST_NAME(l, target) != ST_NAME(l, cur) && !f.flag(FB_CBR) && !f.flag(FB_CIG)) {   // isForwardingToNextStage :343-349
+          const int nv = dw_add_stage<W>(l, ver);
           if (nv < 0) return false;
-          g.cs = mk_run(r_sid(f.cs), r_eps(f.cs), nv, f.cs.ev, f.cs.seq, false, false);   // setVersion
+          g.ver = nv;                                                // setVersion (a fresh stage: flags clear)
+          g.fl = 0;
         }
-        if (op == E_SKIP_PROCEED) { g.prev_sid = f.prev_sid; g.prev_eps = f.prev_eps; }
-        else { g.prev_sid = f.cur_sid; g.prev_eps = f.cur_eps; }
-        g.cur_sid = int16_t(target);
-        g.cur_eps = EPS_NONE;
+        g.st = op == E_SKIP_PROCEED ? fr_st(target, EPS_NONE, f.prev_sid(), f.prev_eps())
+                                    : fr_st(target, EPS_NONE, cur, ceps);
+        g.before = 0;
         f.before = l.tlen;
-        f.pending = 1;
         fr[d++] = f;                                                  // suspend the parent
         f = g;
-        if (!frame_enter(l, f)) return false;
+        if (!frame_enter<W>(l, f, run)) return false;
         continue;
       }
+      const int prev = f.prev_sid();
       if (op == E_TAKE) {                                            // :238-255
-        if (!push_t(l, mk_run(f.cur_sid, f.cur_sid, ver, l.r, seq, false, false))) return false;
+        if (!push_t(l, mk_run(cur, cur, ver, l.r, seq, false, false))) return false;
         int pv = ver;
-        if (!(!f.branching || f.ignored)) { pv = dw_add_run(l, ver, 1); if (pv < 0) return false; }
+        if (!(!f.flag(FB_BRANCHING) || f.flag(FB_IGNORED))) { pv = dw_add_run<W>(l, ver, 1); if (pv < 0) return false; }
         KPH_BEGIN(l, 2);
-        if (f.prev_sid >= 0) buf_put5(l, f.cur_sid, l.r, f.prev_sid, f.cs.ev, pv);
-        else buf_put3(l, f.cur_sid, l.r, pv);
+        if (prev >= 0) buf_put5<W>(l, cur, l.r, prev, run.ev, pv);
+        else buf_put3<W>(l, cur, l.r, pv);
         KPH_END(l, 2);
         if (l.err || l.overflow) return false;
-        f.consumed = 1;
+        f.set(FB_CONSUMED);
       } else if (op == E_BEGIN) {                                    // :256-271
         KPH_BEGIN(l, 2);
-        if (f.prev_sid >= 0) buf_put5(l, f.cur_sid, l.r, f.prev_sid, f.cs.ev, ver);
-        else buf_put3(l, f.cur_sid, l.r, ver);
+        if (prev >= 0) buf_put5<W>(l, cur, l.r, prev, run.ev, ver);
+        else buf_put3<W>(l, cur, l.r, ver);
         KPH_END(l, 2);
         if (l.err || l.overflow) return false;
-        if (!push_t(l, mk_run(f.cur_sid, target, ver, l.r, seq, false, false))) return false;
-        f.consumed = 1;
+        if (!push_t(l, mk_run(cur, target, ver, l.r, seq, false, false))) return false;
+        f.set(FB_CONSUMED);
       } else if (op == E_IGNORE) {                                   // :272-285
-        if (!f.branching && !push_t(l, mk_run(r_sid(f.cs), r_eps(f.cs), f.cs.ver, f.cs.ev, f.cs.seq, false, true)))
+        if (!f.flag(FB_BRANCHING) && !push_t(l, mk_run(r_sid(run), r_eps(run), f.ver, run.ev, run.seq, false, true)))
           return false;
       }
       continue;
     }
     // ---- after the edge loop ----
-    const int ver = f.cs.ver, seq = f.cs.seq, pev = f.cs.ev;
-    if (f.branching) {                                               // :289-317
-      if (f.consumed) {
-        const int nseq = next_seq(l);
-        const int last = f.ignored ? pev : l.r;
-        if (f.prev_sid < 0) { l.err = CEP_E_NPE; return false; }    // Stage.newEpsilonState(null, ...)
-        const bool pb = is_begin(l, f.prev_sid);
-        const int nv = dw_add_run(l, ver, pb ? 2 : 1);
+    const int ver = f.ver, seq = run.seq, pev = run.ev;
+    const int cur = f.cur_sid(), prev = f.prev_sid();
+    const bool consumed = f.flag(FB_CONSUMED);
+    if (f.flag(FB_BRANCHING)) {                                      // :289-317
+      if (consumed) {
+        const int nseq = next_seq<W>(l);
+        const int last = f.flag(FB_IGNORED) ? pev : l.r;
+        if (prev < 0) { l.err = CEP_E_NPE; return false; }           // Stage.newEpsilonState(null, ...)
+        const bool pb = is_begin(l, prev);
+        const int nv = dw_add_run<W>(l, ver, pb ? 2 : 1);
         if (nv < 0) return false;
-        if (!push_t(l, mk_run(f.prev_sid, f.cur_sid, nv, last, nseq, true, false))) return false;
+        if (!push_t(l, mk_run(prev, cur, nv, last, nseq, true, false))) return false;
         for (int k = 0; k < KCEP_PROG(l).ndefined; k++) {                    // AggregatesStoreImpl.branch
           const int st = KCEP_PROG(l).defined[k];
           int32_t t;
           int64_t v;
-          if (!agg_read(l, st, seq, t, v)) return false;
-          if (t && !agg_write(l, st, nseq, t, v)) return false;           // (a new sequence's row is null)
+          if (!agg_read<W>(l, st, seq, t, v)) return false;
+          if (t && !agg_write<W>(l, st, nseq, t, v)) return false;           // (a new sequence's row is null)
         }
         if (!pb) {
           KPH_BEGIN(l, 2);
-          buf_branch(l, f.prev_sid, pev, ver);
+          buf_branch<W>(l, prev, pev, ver);
           KPH_END(l, 2);
           if (l.err) return false;
         }
-      } else if (!f.proceed) {
-        if (!push_t(l, f.cs)) return false;
+      } else if (!f.flag(FB_PROCEED)) {
+        if (!push_t(l, fr_cs(f, run))) return false;
       }
     }
-    if (f.consumed && f.cur_eps == EPS_NONE && ST_NFOLDS(l, f.cur_sid) > 0) {   // evaluateAggregates :319-321, :362-369
-      const DevStage& s = stg(l, f.cur_sid);
+    if (consumed && f.cur_eps() == EPS_NONE && ST_NFOLDS(l, cur) > 0) {   // evaluateAggregates :319-321, :362-369
+      const DevStage& s = stg(l, cur);
       for (int k = 0; k < s.nfolds; k++) {
         int32_t ct;
         int64_t cv;
-        if (!agg_read(l, s.fold_state[k], seq, ct, cv)) return false;
+        if (!agg_read<W>(l, s.fold_state[k], seq, ct, cv)) return false;
         Ctx c{seq, -1, -1, ver, true, ct, cv};
         int64_t v;
-        if (!run_code(l, s.fold_code[k], c, v)) return false;
-        if (!agg_write(l, s.fold_state[k], seq, s.fold_type[k], v)) return false;
+        if (!run_code<W>(l, s.fold_code[k], c, v)) return false;
+        if (!agg_write<W>(l, s.fold_state[k], seq, s.fold_type[k], v)) return false;
         l.ov_own = 1;
       }
     }
-    const int csid = r_sid(f.cs), ceps = r_eps(f.cs);
+    const int csid = r_sid(run), ceps = r_eps(run);
     if (is_begin(l, csid) && !is_forwarding(l, csid, ceps)) {         // begin re-add :323-338
-      if (f.consumed) {
-        const int nseq = next_seq(l);
+      if (consumed) {
+        const int nseq = next_seq<W>(l);
         int nv = ver;
-        if (l.tlen != f.nbase) { nv = dw_add_run(l, ver, 1); if (nv < 0) return false; }
+        if (l.tlen != f.nbase()) { nv = dw_add_run<W>(l, ver, 1); if (nv < 0) return false; }
         if (!push_t(l, mk_run(csid, ceps, nv, -1, nseq, false, false))) return false;
       } else {
-        if (!push_t(l, f.cs)) return false;
+        if (!push_t(l, fr_cs(f, run))) return false;
       }
     }
     if (d == 0) return true;
     f = fr[--d];                                                      // resume the parent
-    if (f.pending) {
-      if (l.tlen > f.before) f.proceed = 1;
-      f.pending = 0;
-    }
+    if (l.tlen > f.before) f.set(FB_PROCEED);                         // its child produced runs
   }
 }
 
@@ -1221,7 +1265,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.seg0 = A.seg_start[seg];
   l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
   l.g = l.seg0;
-  l.wave = 0; l.wtop = nullptr; l.log = nullptr; l.log_cap = 0; l.log_n = 0; l.nph = 0; l.wgrow = 0;
+  l.wtop = nullptr; l.log = nullptr; l.log_cap = 0; l.log_n = 0; l.nph = 0; l.wgrow = 0;
   l.wpool = ka;
   l.cap_hit = 0;
   l.rec_out_top = 0;

@@ -494,10 +494,12 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
     l.A = &A; l.P = A.P;
     l.seg0 = A.seg_start[seg];
     l.L = int32_t(A.seg_start[seg + 1] - l.seg0);
-    l.wave = 0; l.cap_hit = 0;
+    l.cap_hit = 0;
   }
   l.wpool = &w.ka;
-  // every lane: the key's fixed shape (lane 0's key_begin set it)
+  // every lane: the key's fixed shape (lane 0's key_begin set it), as wave-uniform values
+  l.seg0 = gp.bcast(l.seg0);
+  l.L = gp.bcast(l.L);
   l.C = gp.bcast(l.C);
   l.nev = gp.bcast(l.nev);
   l.evw = gp.bcast(l.evw);
@@ -592,10 +594,8 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
           l.heap = w.heap; l.heapcap = w.heapcap;
         }
         if (me || !seqd) { l.tlen = 0; l.log_n = 0; l.nph = 0; l.err = 0; l.overflow = 0; l.wgrow = 0; l.ov_own = 0; }
-        l.wave = seqd ? 0 : 1;
         good = true;
-        if (me) good = evaluate(l, run, fr);
-        l.wave = 0;
+        if (me) good = seqd ? evaluate<false>(l, run, fr) : evaluate<true>(l, run, fr);
         if (seqd) {
           if (me) {
             if (good && l.tlen == 0) buf_peek(l, r_sid(run), run.ev, run.ver, true, nullptr, 0);   // removePattern
@@ -755,7 +755,6 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
     ws_to_lane(l, w);
     l.pool_words = int64_t(w.ka.pool_words);
     l.wpool = nullptr;
-    l.wave = 0;
     key_end(l, A, seg, err_rec, live_max, evals, t0, &w.ka);
   }
 }
