@@ -44,11 +44,9 @@ hipError_t nfa_wave_launch(const NfaArgs& A, int64_t grid, hipStream_t st, const
 int64_t nfa_wave_grid(int64_t nseg, bool agg, const JitModule* j);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
-hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
-                                   hipStream_t st);
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
-hipError_t nfa_compact_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_out,
-                              const int64_t* res_matches, const int64_t* moff, const int64_t* eoff,
+hipError_t nfa_compact_launch(int64_t nseg, int64_t nm, int64_t ne, const int32_t* key, const int64_t* seg_start,
+                              const int64_t* res_out, const int64_t* res_ent, const int64_t* moff, const int64_t* eoff,
                               int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st);
 hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_carry,
@@ -180,7 +178,7 @@ struct cep_session {
   bool h2d_wait = false;          // the push copied from pinned caller memory: wait for h2d_ev
   int zc_slot = -1;               // the push's kernels read ring slot zc_slot in place (zero copy)
   // ---- general workspace ----
-  DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_err, r_errrec, r_carry, ents,
+  DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_ent, r_err, r_errrec, r_carry,
       moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec;
   int64_t pool_words = 0;       // pool capacity to use (grows after an overflow)
   int64_t nseg = 0, g_matches = 0, g_entries = 0;
@@ -804,12 +802,12 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   cap.heap_mult = std::max<int32_t>(1, int32_t(cap.heap_mult * scale));
   cap.out_mult = std::max<int32_t>(1, int32_t(cap.out_mult * scale));
   const size_t sb = size_t(nseg) * 8;
-  if (s->r_matches.ensure(sb) || s->r_words.ensure(sb) || s->r_out.ensure(sb) || s->r_err.ensure(sb) ||
-      s->r_errrec.ensure(sb) || s->r_carry.ensure(sb) || s->ents.ensure(sb) || s->moff.ensure(sb) || s->eoff.ensure(sb))
+  if (s->r_matches.ensure(sb) || s->r_words.ensure(sb) || s->r_out.ensure(sb) || s->r_ent.ensure(sb) || s->r_err.ensure(sb) ||
+      s->r_errrec.ensure(sb) || s->r_carry.ensure(sb) || s->moff.ensure(sb) || s->eoff.ensure(sb))
     return fail(CEP_E_HIP, "allocation failed");
   // first-allocation words of every key (NfaCaps) plus the events carried into the batch
-  const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base;
-  const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 3 * D.nstates;
+  const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base + 16;
+  const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 4 + 3 * D.nstates;
   int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
   s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
   const int64_t pool_base = s->pool_words;         // what the batch starts with (kept for the next batch)
@@ -819,6 +817,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.res_matches = s->r_matches.as<int64_t>();
   A.res_words = s->r_words.as<int64_t>();
   A.res_out = s->r_out.as<int64_t>();
+  A.res_ent = s->r_ent.as<int64_t>();
   A.res_err = s->r_err.as<int32_t>();
   A.res_err_rec = s->r_errrec.as<int64_t>();
   A.res_carry = s->r_carry.as<int64_t>();
@@ -874,9 +873,8 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     timed = true;
     // the CSR's match / entry counts are scanned right away, so that one synchronisation reads them
     // with the pool flags (a retried attempt scans again)
-    HIPCHECK(nfa_entry_counts_launch(s->r_words.as<int64_t>(), s->r_matches.as<int64_t>(), nseg, s->ents.as<int64_t>(), st));
     HIPCHECK(exclusive_scan(s->r_matches.as<int64_t>(), nseg, s->moff.as<int64_t>(), scal + 3, s->scan_tmp.as<int64_t>(), st));
-    HIPCHECK(exclusive_scan(s->ents.as<int64_t>(), nseg, s->eoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), st));
+    HIPCHECK(exclusive_scan(s->r_words.as<int64_t>(), nseg, s->eoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), st));
     unsigned long long res[5];
     HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipMemcpyAsync(tots, scal + 3, 16, hipMemcpyDeviceToHost, st));
@@ -914,10 +912,10 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   if (s->o_record.ensure(nm * 8) || s->o_key.ensure(nm * 4) || s->o_entoff.ensure(nm * 8) ||
       s->o_name.ensure(ne * 4) || s->o_entrec.ensure(ne * 8))
     return fail(CEP_E_HIP, "allocation failed");
-  HIPCHECK(nfa_compact_launch(nseg, A.key, A.seg_start, s->r_out.as<int64_t>(), s->r_matches.as<int64_t>(),
-                              s->moff.as<int64_t>(), s->eoff.as<int64_t>(), s->o_record.as<int64_t>(),
-                              s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
-                              s->o_entrec.as<int64_t>(), st));
+  HIPCHECK(nfa_compact_launch(nseg, tots[0], tots[1], A.key, A.seg_start, s->r_out.as<int64_t>(),
+                              s->r_ent.as<int64_t>(), s->moff.as<int64_t>(), s->eoff.as<int64_t>(),
+                              s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
+                              s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
   if (s->carry) {                                  // NFAStore.put of every key of the batch
     HIPCHECK(carry_commit_launch(nseg, A.key, A.seg_start, s->r_carry.as<int64_t>(), s->r_err.as<int32_t>(),
                                  s->ctab.as<int64_t>(), st));
@@ -1134,7 +1132,7 @@ void cep_session_close(cep_session* s) {
   for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->wscratch, &s->dstage, &s->dl_ticket,
                   &s->h_topic, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
-                  &s->r_carry, &s->ents, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
+                  &s->r_carry, &s->r_ent, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
                   &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_segs, &s->r_blk, &s->r_len, &s->r_entoff,
                   &s->r_errcode, &s->r_errlist, &s->r_endof, &s->r_prof, &s->rtab, &s->rpool, &s->rpool2, &s->rtop, &s->e_key,
                   &s->e_topic, &s->e_part, &s->e_seg, &s->e_off, &s->e_ts, &s->e_pos, &s->rc_a, &s->rc_b, &s->rc_c,

@@ -144,8 +144,9 @@ struct NfaArgs {
   unsigned long long* cpool_top;
   int64_t* res_carry;             // carry: per segment, offset of the new blob (-1 none)
   int64_t* res_matches;           // per segment
-  int64_t* res_words;
-  int64_t* res_out;               // device address of the key's output region
+  int64_t* res_words;             // per segment: its matches' entries
+  int64_t* res_out;               // device address of the key's match headers (4 words per match, nfa_dev.h)
+  int64_t* res_ent;               // ... and of their entries (3 words per entry)
   int32_t* res_err;
   int64_t* res_err_rec;
   int32_t* flags;                 // [0] pool overflow lanes, [1] carry-pool overflow lanes, [2] bad key ids,

@@ -217,37 +217,41 @@ hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* t
   return hipGetLastError();
 }
 
-// per match [pos lo, pos hi, cnt, (name, pos lo, pos hi) x cnt]
-__global__ void nfa_compact(int64_t nseg, const int32_t* __restrict__ key, const int64_t* __restrict__ seg_start,
-                            const int64_t* __restrict__ res_out, const int64_t* __restrict__ res_matches,
-                            const int64_t* __restrict__ moff, const int64_t* __restrict__ eoff,
-                            int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
-                            int64_t* __restrict__ ent_off, int32_t* __restrict__ ent_name,
-                            int64_t* __restrict__ ent_record) {
-  const int64_t s = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (s >= nseg) return;
-  const int32_t* o = reinterpret_cast<const int32_t*>(uintptr_t(res_out[s]));
-  int64_t m = moff[s], e = eoff[s];
-  const int32_t k = key[seg_start[s]];
-  for (int64_t j = 0; j < res_matches[s]; j++) {
-    const int cnt = o[2];
-    match_record[m] = cw64(o);
-    match_key[m] = k;
-    ent_off[m] = e;
-    for (int i = 0; i < cnt; i++) {
-      ent_name[e + i] = o[3 + 3 * i];
-      ent_record[e + i] = cw64(o + 4 + 3 * i);
-    }
-    e += cnt;
-    m++;
-    o += 3 + 3 * cnt;
+// The segments' matches into one CSR in segment (key) order: one thread per match and one per entry,
+// each finding its segment by a binary search over the segments' exclusive prefixes (moff / eoff, in
+// L2), so that a key with thousands of matches is copied as fast as one with a single match.  A key's
+// match headers {pos lo, pos hi, entries, first entry} and entries {name, pos lo, pos hi} are each
+// contiguous in the pool (nfa_dev.h emit_match, nfa_wave.h wave_emit_matches).
+__device__ __forceinline__ int64_t seg_of(const int64_t* __restrict__ off, int64_t nseg, int64_t x) {
+  int64_t lo = 0, hi = nseg - 1;                   // the last segment whose range starts at or before x
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= x) lo = mid; else hi = mid - 1;
   }
+  return lo;
 }
-// entries per segment = (words - 3 * matches) / 3
-__global__ void nfa_entry_counts(const int64_t* __restrict__ words, const int64_t* __restrict__ matches, int64_t nseg,
-                                 int64_t* __restrict__ ents) {
-  const int64_t s = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (s < nseg) ents[s] = (words[s] - 3 * matches[s]) / 3;
+__global__ void nfa_compact_matches(int64_t nseg, int64_t nm, const int32_t* __restrict__ key,
+                                    const int64_t* __restrict__ seg_start, const int64_t* __restrict__ res_out,
+                                    const int64_t* __restrict__ moff, const int64_t* __restrict__ eoff,
+                                    int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
+                                    int64_t* __restrict__ ent_off) {
+  const int64_t m = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  const int64_t s = seg_of(moff, nseg, m);
+  const int4 h = reinterpret_cast<const int4*>(uintptr_t(res_out[s]))[m - moff[s]];
+  match_record[m] = int64_t(uint64_t(uint32_t(h.x)) | (uint64_t(uint32_t(h.y)) << 32));
+  match_key[m] = key[seg_start[s]];
+  ent_off[m] = eoff[s] + h.w;
+}
+__global__ void nfa_compact_entries(int64_t nseg, int64_t ne, const int64_t* __restrict__ res_ent,
+                                    const int64_t* __restrict__ eoff, int32_t* __restrict__ ent_name,
+                                    int64_t* __restrict__ ent_record) {
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  const int64_t s = seg_of(eoff, nseg, e);
+  const int32_t* x = reinterpret_cast<const int32_t*>(uintptr_t(res_ent[s])) + 3 * (e - eoff[s]);
+  ent_name[e] = x[0];
+  ent_record[e] = cw64(x + 1);
 }
 // NFAStoreImpl.put of every key of the batch: the key's table entry points at its new blob
 // (keys whose processing raised keep their previous state, like the failed task)
@@ -299,20 +303,17 @@ hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* i
   return hipGetLastError();
 }
 
-hipError_t nfa_entry_counts_launch(const int64_t* words, const int64_t* matches, int64_t nseg, int64_t* ents,
-                                   hipStream_t st) {
-  if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(nfa_entry_counts, dim3(unsigned((nseg + 255) / 256)), dim3(256), 0, st, words, matches, nseg, ents);
-  return hipGetLastError();
-}
-
-hipError_t nfa_compact_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_out,
-                              const int64_t* res_matches, const int64_t* moff, const int64_t* eoff,
+hipError_t nfa_compact_launch(int64_t nseg, int64_t nm, int64_t ne, const int32_t* key, const int64_t* seg_start,
+                              const int64_t* res_out, const int64_t* res_ent, const int64_t* moff, const int64_t* eoff,
                               int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st) {
   if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(nfa_compact, dim3(unsigned((nseg + 255) / 256)), dim3(256), 0, st, nseg, key, seg_start, res_out,
-                     res_matches, moff, eoff, match_record, match_key, ent_off, ent_name, ent_record);
+  if (nm > 0)
+    hipLaunchKernelGGL(nfa_compact_matches, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, nseg, nm, key, seg_start,
+                       res_out, moff, eoff, match_record, match_key, ent_off);
+  if (ne > 0)
+    hipLaunchKernelGGL(nfa_compact_entries, dim3(unsigned((ne + 255) / 256)), dim3(256), 0, st, nseg, ne, res_ent, eoff,
+                       ent_name, ent_record);
   return hipGetLastError();
 }
 

@@ -86,14 +86,16 @@ struct Lane {
   int32_t* heap;
   int32_t heapcap, heap_top;
   int32_t* out;
-  int32_t outcap, out_top;
+  int32_t outcap, out_top;     // match headers: 4 words each {stream position lo, hi, entries, first entry}
+  int32_t* oent;               // their entries: 3 words each {stage name, stream position lo, hi}
+  int32_t ecap, etop;          // (words / entries)
   int32_t qlen, tlen, flen;
   int32_t runs;                // internal run counter; NFAStates.runs = runs + runs_delta
   int64_t runs_delta;
   int32_t err;
   int32_t overflow;
   int32_t cap_hit;             // the key went over NfaArgs.max_key_words
-  int32_t rec_out_top;         // output words / matches before the current record (capacity rollback)
+  int32_t rec_etop;            // entries / matches before the current record (capacity rollback)
   int64_t rec_nmatch;
   int32_t r;                   // current local event
   int64_t g;                   // its batch record index
@@ -949,10 +951,10 @@ __device__ __forceinline__ bool evaluate(Lane& l, const Run& run, Frame* fr) {
 // room for the longest buffer walk: it visits strictly earlier events, so at
 // most one node per event of the key
 __device__ __forceinline__ bool reserve_walk(Lane& l) {
-  const int need_out = 3 + 3 * l.nev;
-  if (l.out_top + need_out > l.outcap &&
-      !regrow(l, l.out, l.outcap, l.out_top, int64_t(l.out_top) + need_out, AK_OUT))
+  if (l.out_top + 4 > l.outcap && !regrow(l, l.out, l.outcap, l.out_top, int64_t(l.out_top) + 4, AK_OUT))
     return false;
+  const int need_ent = 3 * (l.etop + l.nev);
+  if (need_ent > l.ecap && !regrow(l, l.oent, l.ecap, int64_t(3) * l.etop, need_ent, AK_OUT)) return false;
   const int need_heap = 2 * l.nev + 2;
   if (l.heap_top + need_heap > l.heapcap &&
       !regrow(l, l.heap, l.heapcap, l.heap_top, int64_t(l.heap_top) + need_heap, AK_HEAP))
@@ -972,13 +974,16 @@ __device__ __forceinline__ bool emit_match(Lane& l, const Run& y) {
   o[0] = int32_t(uint32_t(uint64_t(pos)));
   o[1] = int32_t(uint32_t(uint64_t(pos) >> 32));
   o[2] = cnt;
+  o[3] = l.etop;
+  int32_t* en = l.oent + int64_t(3) * l.etop;
   for (int i = 0; i < cnt; i++) {
     const int64_t q = ev_pos(l, tmp[2 * i + 1]);
-    o[3 + 3 * i] = SLOT_NAME(l, tmp[2 * i]);
-    o[4 + 3 * i] = int32_t(uint32_t(uint64_t(q)));
-    o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
+    en[3 * i] = SLOT_NAME(l, tmp[2 * i]);
+    en[3 * i + 1] = int32_t(uint32_t(uint64_t(q)));
+    en[3 * i + 2] = int32_t(uint32_t(uint64_t(q) >> 32));
   }
-  l.out_top += 3 + 3 * cnt;
+  l.out_top += 4;
+  l.etop += cnt;
   l.nmatch++;
   return true;
 }
@@ -1268,7 +1273,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.wtop = nullptr; l.log = nullptr; l.log_cap = 0; l.log_n = 0; l.nph = 0; l.wgrow = 0;
   l.wpool = ka;
   l.cap_hit = 0;
-  l.rec_out_top = 0;
+  l.rec_etop = 0;
   l.rec_nmatch = 0;
   l.err = 0; l.overflow = 0; l.nmatch = 0; l.flen = 0; l.tlen = 0; l.qlen = 0;
   l.nhwm = 0; l.runs = 1; l.runs_delta = 0; l.slm = 0; l.sle = 0;
@@ -1277,6 +1282,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   A.res_matches[seg] = 0;
   A.res_words[seg] = 0;
   A.res_out[seg] = 0;
+  A.res_ent[seg] = 0;
   A.res_err[seg] = 0;
   A.res_err_rec[seg] = -1;
   if (A.carry) A.res_carry[seg] = -1;
@@ -1297,13 +1303,14 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.qa_cap = l.qb_cap = l.tq_cap = l.fq_cap = A.cap.q0;
   l.seqcap = A.cap.seq_base + l.L + (blob ? blob[CB_NSEQ] : 0);
   l.heapcap = A.cap.heap_base + A.cap.heap_mult * l.nev;
-  l.outcap = A.cap.out_base + A.cap.out_mult * l.L;
+  l.outcap = 4 * (4 + l.L);                                             // match headers (grown on demand)
+  l.ecap = A.cap.out_base + A.cap.out_mult * l.L;                        // their entries
   const int64_t fixed = 3 * HWM_MAX + int64_t(NW) * ns * l.nev + 16 * int64_t(A.cap.q0) +
                         int64_t(3) * nst * l.seqcap + l.heapcap;
   const bool in_lds = arena && fixed <= arena_words;
   l.arena_used = in_lds ? int32_t(fixed) : -1;
   int32_t* p = in_lds ? arena : pool_alloc(l, fixed, AK_WS);
-  int32_t* out_at = p ? pool_alloc(l, l.outcap, AK_OUT, true) : nullptr;
+  int32_t* out_at = p ? pool_alloc(l, l.outcap + l.ecap, AK_OUT, true) : nullptr;   // headers, then entries
   if (!p || !out_at) {
     if (A.last_attempt || l.cap_hit) {                                 // handed back per key
       A.res_err[seg] = CEP_E_RUN_CAPACITY;
@@ -1323,7 +1330,8 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   l.aggs = p; p += int64_t(3) * nst * l.seqcap;
   l.heap = p;
   l.out = out_at;
-  l.heap_top = 0; l.out_top = 0;
+  l.oent = out_at + l.outcap;
+  l.heap_top = 0; l.out_top = 0; l.etop = 0;
   for (int64_t i = 0; i < int64_t(3) * nst * l.seqcap; i++) l.aggs[i] = 0;   // all states null
   if (blob) {
     if (!import_state(l, blob)) {
@@ -1412,7 +1420,8 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
     l.overflow = 0;
     if (l.nmatch > l.rec_nmatch) {                                     // none of the failing record's
       l.nmatch = l.rec_nmatch;                                         // matches is emitted
-      l.out_top = l.rec_out_top;
+      l.out_top = int32_t(4 * l.nmatch);
+      l.etop = l.rec_etop;
     }
   } else {
     A.res_err[seg] = l.overflow ? 0 : l.err;
@@ -1421,8 +1430,9 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
   if (l.overflow) atomicAdd(&A.flags[0], 1);
   if (A.res_err[seg]) atomicOr(A.err_any, 1ull);
   A.res_matches[seg] = l.nmatch;
-  A.res_words[seg] = l.out_top;
+  A.res_words[seg] = l.etop;                                           // entries
   A.res_out[seg] = int64_t(reinterpret_cast<uintptr_t>(l.out));
+  A.res_ent[seg] = int64_t(reinterpret_cast<uintptr_t>(l.oent));
 }
 
 // One lane runs one key segment (A.spread segments per wave).
@@ -1455,7 +1465,7 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
     }
     eval_event_only(l);
     evals += l.qlen;
-    l.rec_out_top = l.out_top;
+    l.rec_etop = l.etop;
     l.rec_nmatch = l.nmatch;
     if (!step(l, fr)) {
       if (l.err) err_rec = A.base + g;

@@ -100,6 +100,8 @@ template <int GL>
 struct WaveShared {
   int32_t *nodes, *heap, *qa, *qb, *fq, *out, *hwm, *aggs;
   int32_t heapcap, heap_top, qa_cap, qb_cap, fq_cap, qlen, outcap, out_top, nhwm, runs, seqcap;
+  int32_t* oent;                   // the match entries (headers in out)
+  int32_t ecap, etop;
   int64_t nmatch;
   KeyAlloc ka;                     // the key's allocator: its words, the wave's scratch region
   int32_t err, overflow, cap_hit;
@@ -121,6 +123,7 @@ __device__ __forceinline__ void ws_to_lane(Lane& l, const W& w) {
   l.aggs = w.aggs; l.seqcap = w.seqcap;
   l.heapcap = w.heapcap; l.heap_top = w.heap_top; l.qa_cap = w.qa_cap; l.qb_cap = w.qb_cap; l.fq_cap = w.fq_cap;
   l.qlen = w.qlen; l.outcap = w.outcap; l.out_top = w.out_top; l.nhwm = w.nhwm; l.runs = w.runs;
+  l.oent = w.oent; l.ecap = w.ecap; l.etop = w.etop;
   l.nmatch = w.nmatch; l.err = w.err; l.overflow = w.overflow; l.cap_hit = w.cap_hit;
 }
 template <class W>
@@ -129,6 +132,7 @@ __device__ __forceinline__ void lane_to_ws(W& w, const Lane& l) {
   w.aggs = l.aggs; w.seqcap = l.seqcap;
   w.heapcap = l.heapcap; w.heap_top = l.heap_top; w.qa_cap = l.qa_cap; w.qb_cap = l.qb_cap; w.fq_cap = l.fq_cap;
   w.qlen = l.qlen; w.outcap = l.outcap; w.out_top = l.out_top; w.nhwm = l.nhwm; w.runs = l.runs;
+  w.oent = l.oent; w.ecap = l.ecap; w.etop = l.etop;
   w.nmatch = l.nmatch; w.err = l.err; w.overflow = l.overflow; w.cap_hit = l.cap_hit;
 }
 
@@ -362,31 +366,38 @@ __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, co
       wave_sync();
       return true;
     }
-    // the matches, in final-run order: [pos lo, pos hi, cnt, (name, pos lo, pos hi) x cnt]
+    // the matches, in final-run order: a header per match {pos lo, pos hi, entries, first entry} (lane i's
+    // is the i-th), then the entries {name, pos lo, pos hi} of all of them, contiguous
     int total = 0;
-    const int words = act ? 3 + 3 * cnt : 0;
-    const int off = g.excl_scan(words, total);
-    if (w.out_top + total > w.outcap) {
+    const int off = g.excl_scan(act ? cnt : 0, total);
+    if (w.out_top + 4 * nact > w.outcap) {
       int32_t cap = w.outcap;
-      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + total, g, AK_OUT, false);
+      int32_t* na = wave_regrow(l, w, w.out, cap, w.out_top, int64_t(w.out_top) + 4 * nact, g, AK_OUT, false);
       if (!na) return false;
       if (lane == 0) { w.out = na; w.outcap = cap; }
       wave_sync();
     }
+    if (3 * (w.etop + total) > w.ecap) {
+      int32_t cap = w.ecap;
+      int32_t* na = wave_regrow(l, w, w.oent, cap, int64_t(3) * w.etop, int64_t(3) * (w.etop + total), g, AK_OUT, false);
+      if (!na) return false;
+      if (lane == 0) { w.oent = na; w.ecap = cap; }
+      wave_sync();
+    }
     if (act) {
-      int32_t* o = w.out + w.out_top + off;
-      o[0] = int32_t(uint32_t(uint64_t(pos)));
-      o[1] = int32_t(uint32_t(uint64_t(pos) >> 32));
-      o[2] = cnt;
+      const int first = w.etop + off;
+      const int4 h = make_int4(int32_t(uint32_t(uint64_t(pos))), int32_t(uint32_t(uint64_t(pos) >> 32)), cnt, first);
+      *reinterpret_cast<int4*>(w.out + w.out_top + 4 * lane) = h;
+      int32_t* en = w.oent + int64_t(3) * first;
       for (int i = 0; i < cnt; i++) {
         const int64_t q = ev_pos(l, path[2 * i + 1]);
-        o[3 + 3 * i] = SLOT_NAME(l, path[2 * i]);
-        o[4 + 3 * i] = int32_t(uint32_t(uint64_t(q)));
-        o[5 + 3 * i] = int32_t(uint32_t(uint64_t(q) >> 32));
+        en[3 * i] = SLOT_NAME(l, path[2 * i]);
+        en[3 * i + 1] = int32_t(uint32_t(uint64_t(q)));
+        en[3 * i + 2] = int32_t(uint32_t(uint64_t(q) >> 32));
       }
     }
     wave_sync();
-    if (lane == 0) { w.out_top += total; w.nmatch += nact; }
+    if (lane == 0) { w.out_top += 4 * nact; w.etop += total; w.nmatch += nact; }
     wave_sync();
   }
   return true;
@@ -508,7 +519,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
   l.tq_cap = gp.bcast(l.tq_cap);
   l.runs_delta = gp.bcast(l.runs_delta);
   l.pool_words = 0;
-  l.rec_out_top = 0; l.rec_nmatch = 0;
+  l.rec_etop = 0; l.rec_nmatch = 0;
   l.slm = 0; l.sle = 0; l.flen = 0; l.tlen = 0;
   ws_to_lane(l, w);
   // private run lists and operation logs: written by every evaluation and read back by the commit
@@ -562,7 +573,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
     eval_event_only(l);
     const int n = w.qlen;
     evals += n;
-    if (lane == 0) { l.rec_out_top = w.out_top; l.rec_nmatch = w.nmatch; }
+    if (lane == 0) { l.rec_etop = w.etop; l.rec_nmatch = w.nmatch; }
     int qn = 0, flen = 0;
     KWP_ADD(6, t_eo);
     for (int base = 0; base < n && !w.err && !w.overflow; base += GL) {

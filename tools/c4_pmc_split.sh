@@ -14,7 +14,7 @@ run() {  # name, scratch, counters...
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $D -o ${nm}_$sc -- python3 bench.py --config c4 --steps 2 --warmup 1 --no-cpu-baseline --no-host-input --carry-batches 1 --processor-batch , --handoff-cap 0 > $D/${nm}_$sc.log 2>&1 || return 1
   echo "pass $nm scratch=$sc ok"
 }
-for sc in default 0; do
+for sc in ${SCRATCH_VARIANTS:-default 0}; do
   run a $sc TCP_TCC_RW_WRITE_REQ_sum TCP_TCC_NC_WRITE_REQ_sum TCP_TCC_UC_WRITE_REQ_sum TCP_TCC_CC_WRITE_REQ_sum || exit 1
   run b $sc TCC_NORMAL_WRITEBACK_sum TCC_NORMAL_EVICT_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum || exit 1
   run c $sc TCP_TCC_RW_READ_REQ_sum TCP_TCC_NC_READ_REQ_sum TCP_TCC_UC_READ_REQ_sum TCP_TCC_CC_READ_REQ_sum || exit 1
