@@ -226,7 +226,7 @@ int cep_batch_errors(const cep_session* s, int64_t* records, int32_t* codes, int
    NFA.evaluate / edge predicates / buffer put+branch / removePattern / matchConstruction /
    getPointerByVersion scans / predecessor appends / Dewey version copies, then counts of scans /
    predecessor entries examined / digit-by-digit version checks (-1 each when the session runs the
-   built-in kernel), then 0 (reserved), the workspace words the key took (wave scratch region + device
+   built-in kernel), then the key's start (wall clock, 100 MHz ticks), the workspace words the key took (wave scratch region + device
    pool), then those words per allocation kind -- first workspace, match output, heap, run queues,
    private run lists / logs, aggregates, other -- and the device pool's share of them (-1 each when the
    session runs the built-in kernel)}; 25 int64 per key;

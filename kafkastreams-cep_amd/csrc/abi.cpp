@@ -45,6 +45,8 @@ int64_t nfa_wave_grid(int64_t nseg, bool agg, const JitModule* j);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
+hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
+                               int64_t* out1, int64_t* total0, int64_t* total1, int64_t* tmp, hipStream_t st);
 hipError_t nfa_compact_launch(int64_t nseg, int64_t nm, int64_t ne, const int32_t* key, const int64_t* seg_start,
                               const int64_t* res_out, const int64_t* res_ent, const int64_t* moff, const int64_t* eoff,
                               int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
@@ -64,6 +66,10 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
                                unsigned long long* out, int64_t* tot_cnt, int64_t* tot_len, int64_t* scan_tmp,
                                hipStream_t st);
 int64_t runs_sim_waves(int64_t n, int32_t chunk);
+bool runs_emit_scan(const int64_t* stat, int64_t n, int32_t chunk, int64_t* pre, int64_t* tot_cnt, int64_t* tot_len,
+                    hipStream_t st);
+hipError_t runs_emit_launch(const RunsArgs& R, const int32_t* end_of, const int64_t* pre, int span, int64_t* match_record,
+                            int32_t* match_key, int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st);
 hipError_t runs_results_launch(const unsigned long long* ctl, const int64_t* nm, const int64_t* top, int64_t* h,
                                hipStream_t st);
 hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, int64_t* len,
@@ -182,6 +188,7 @@ struct cep_session {
       moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec;
   int64_t pool_words = 0;       // pool capacity to use (grows after an overflow)
   int64_t nseg = 0, g_matches = 0, g_entries = 0;
+  int64_t nseg_hint = 0;        // the last general batch's segment count (pool estimate of the next)
   // ---- carried per-key state (CEP_SESSION_CARRY): NFAStore equivalent ----
   bool carry = false;
   int64_t base = 0;             // stream position of the next batch's record 0
@@ -255,6 +262,11 @@ struct RoctxRange {
 bool getenv_flag(const char* name) {
   const char* v = getenv(name);
   return v && v[0] == '1';
+}
+// an on-by-default path switched off by NAME=0
+bool getenv_flag_off(const char* name) {
+  const char* v = getenv(name);
+  return v && v[0] == '0' && v[1] == 0;
 }
 
 // the halo arguments of the last stencil batch (its stamp and stream position)
@@ -601,9 +613,9 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   }
   if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
       s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 4) * 8) ||
-      s->flag.ensure(size_t(2 * runs_sim_waves(n, runs_chunk(n)) + 8) * 8) ||
+      s->flag.ensure(size_t(6 * runs_sim_waves(n, runs_chunk(n)) + 8) * 8) ||
       s->idx.ensure(size_t(2 * runs_sim_waves(n, runs_chunk(n)) + 8) * 8) || s->r_endof.ensure(size_t(n) * 4) ||
-      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 4) ||
+      s->r_segs.ensure(size_t(n) * RUNS_MAX_SEGS * 2) ||
       s->r_errlist.ensure(size_t(std::min<int64_t>(n, kRunsErrCap)) * 24))
     return fail(CEP_E_HIP, "allocation failed");
   RunsArgs A{};
@@ -621,7 +633,8 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.match_key = s->rk.as<unsigned long long>();
   A.match_cap = n;
   A.err_code = s->r_errcode.as<int32_t>();
-  A.segs = s->r_segs.as<uint32_t>();             // the runs' consumed stages, for runs_expand
+  A.segs = s->r_segs.as<uint16_t>();             // the runs' consumed stages, for runs_emit / runs_expand
+  A.segn = s->pat->prog.dev.nstages - 1 <= 4 ? 4 : RUNS_MAX_SEGS;   // (a run consumes each stage at most once)
   A.seg_over = ctl + 3;
   A.err_list = s->r_errlist.as<unsigned long long>();
   A.err_n = ctl + 5;
@@ -634,9 +647,16 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                            s->jit ? s->jit->runs_sim : nullptr));
   HIPCHECK(hipEventRecord(s->ev1, st));
   int64_t* scal0 = s->scal.as<int64_t>();
-  HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), n, A.chunk, s->idx.as<int64_t>(),
-                               s->rk.as<unsigned long long>(), scal0 + 3, reinterpret_cast<int64_t*>(ctl + 2),
-                               s->scan_tmp.as<int64_t>(), st));
+  // the completed runs counted by the chunk they end in and scanned (runs_emit's placement), or -- too
+  // many chunks for that scan, or the sort forced -- compacted in start order for runs_order / the sort
+  // (KCEP_RUNS_EMIT=0 / KCEP_RUNS_RADIX=1: the tests' hooks onto those paths for batches runs_emit takes)
+  const bool emit_scan = !getenv_flag("KCEP_RUNS_RADIX") && !getenv_flag_off("KCEP_RUNS_EMIT") &&
+                         runs_emit_scan(s->flag.as<int64_t>(), n, A.chunk, s->idx.as<int64_t>(), scal0 + 3,
+                                        reinterpret_cast<int64_t*>(ctl + 2), st);
+  if (!emit_scan)
+    HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), n, A.chunk, s->idx.as<int64_t>(),
+                                 s->rk.as<unsigned long long>(), scal0 + 3, reinterpret_cast<int64_t*>(ctl + 2),
+                                 s->scan_tmp.as<int64_t>(), st));
   if (rcarry) {                                    // the keys' new tails: from their oldest still-open start
     if (s->rc_c.ensure(size_t(nb + 2) * 8) || s->rc_d.ensure(size_t(nb + 2) * 8))
       return fail(CEP_E_HIP, "allocation failed");
@@ -706,9 +726,23 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
       s->scan_tmp.ensure(size_t(nm / 1024 + 4) * 8) || s->o_record.ensure(nmb * 8) || s->o_key.ensure(nmb * 4) ||
       s->o_entoff.ensure(nmb * 8) || s->o_name.ensure(neb * 4) || s->o_entrec.ensure(neb * 8))
     return fail(CEP_E_HIP, "allocation failed");
+  int64_t* scal = s->scal.as<int64_t>();
+  if (emit_scan && nm > 0 && !res[3] && res[4] < uint64_t(A.chunk)) {
+    // every run shorter than a chunk: the CSR in one pass over the end chunks (runs_emit)
+    HIPCHECK(runs_emit_launch(A, s->r_endof.as<int32_t>(), s->idx.as<int64_t>(), int(res[4]), s->o_record.as<int64_t>(),
+                              s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
+                              s->o_entrec.as<int64_t>(), st));
+    HIPCHECK(hipEventRecord(s->eb1, st));
+    s->g_matches = nm;
+    s->g_entries = ne;
+    return CEP_OK;
+  }
+  if (emit_scan)                                   // (the start-ordered list the paths below read)
+    HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), n, A.chunk, s->idx.as<int64_t>(),
+                                 s->rk.as<unsigned long long>(), scal0 + 3, reinterpret_cast<int64_t*>(ctl + 2),
+                                 s->scan_tmp.as<int64_t>(), st));
   // (completing record, start) order: a windowed rank when every run spans <= 1024 records
   // (runs_order), else rocPRIM's radix sort over the completing record's bits
-  int64_t* scal = s->scal.as<int64_t>();
   // the entry offsets are scanned straight into the output's ent_off (runs_expand reads them there);
   // runs_order writes the sorted runs' lengths itself
   if (nm > 0 && res[4] <= 1024 && !getenv_flag("KCEP_RUNS_RADIX")) {
@@ -724,7 +758,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
                                nullptr, nullptr, nullptr, st, true,
                                s->jit ? s->jit->runs_write : nullptr));
   }
-  if (!res[3] && !getenv_flag("KCEP_RUNS_REWALK")) {
+  if (!res[3]) {
     // the traversals from the stage segments runs_sim recorded
     HIPCHECK(runs_expand_launch(A, s->rk_sorted.as<unsigned long long>(), nm, s->o_entoff.as<int64_t>(), ne,
                                 s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
@@ -772,29 +806,36 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     HIPCHECK(hipEventRecord(s->eb1, st));
     return CEP_OK;
   }
-  // segments: one per key run of the grouped batch
-  const size_t nb = size_t(n / 1024 + 2) * 8;
-  if (s->flag.ensure(size_t(n) * 8) || s->idx.ensure(size_t(n) * 8) || s->seg.ensure(size_t(n + 1) * 8) ||
-      s->scan_tmp.ensure(nb) || s->scal.ensure(64) || s->ctl.ensure(64))
+  // segments: one per key run of the grouped batch.  A wave-kernel batch of a session that has run one
+  // before leaves the count on the device (NfaArgs.nseg_dev, read by the kernel and the scans): no host
+  // round trip before the kernel -- per-segment buffers are sized for n segments, the pool estimate is the
+  // last batch's (a pool overflow re-runs the batch with a larger one, as always)
+  const bool dev_count = s->wave && !s->carry && s->nseg_hint > 0 && n < (int64_t(1) << 31);
+  const size_t nb = size_t(n / 1024 + 2) * 16;
+  if (s->seg.ensure(size_t(n + 1) * 8) || s->scan_tmp.ensure(nb) || s->scal.ensure(64) || s->ctl.ensure(64))
     return fail(CEP_E_HIP, "allocation failed");
   int64_t* scal = s->scal.as<int64_t>();
-  HIPCHECK(nfa_segments(A.key, n, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
-                        s->scan_tmp.as<int64_t>(), st));
-  int64_t segs[2] = {0, 0};                       // segment count, carry key-check flags
-  if (s->carry) {
-    HIPCHECK(hipMemsetAsync(scal + 1, 0, 8, st));
-    HIPCHECK(carry_keycheck_launch(n, scal, A.key, s->seg.as<int64_t>(), int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
-                                   s->kstamp.as<int32_t>(), ++s->batch_no, reinterpret_cast<unsigned long long*>(scal + 1),
-                                   st));
+  HIPCHECK(nfa_segments(A.key, n, nullptr, nullptr, s->seg.as<int64_t>(), scal, s->scan_tmp.as<int64_t>(), st));
+  int64_t nseg = n;                               // (an upper bound until the kernel's results are read)
+  if (!dev_count) {
+    int64_t segs[2] = {0, 0};                     // segment count, carry key-check flags
+    if (s->carry) {
+      HIPCHECK(hipMemsetAsync(scal + 1, 0, 8, st));
+      HIPCHECK(carry_keycheck_launch(n, scal, A.key, s->seg.as<int64_t>(), int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
+                                     s->kstamp.as<int32_t>(), ++s->batch_no, reinterpret_cast<unsigned long long*>(scal + 1),
+                                     st));
+    }
+    HIPCHECK(hipMemcpyAsync(segs, scal, sizeof segs, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    nseg = segs[0];
+    if (segs[1] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    if (segs[1] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+    if (nseg >= (int64_t(1) << 31)) return fail(CEP_E_ARG, "too many keys in one batch");
   }
-  HIPCHECK(hipMemcpyAsync(segs, scal, sizeof segs, hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipStreamSynchronize(st));
-  const int64_t nseg = segs[0];
-  if (segs[1] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
-  if (segs[1] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
-  if (nseg >= (int64_t(1) << 31)) return fail(CEP_E_ARG, "too many keys in one batch");
+  const int64_t nseg_est = dev_count ? s->nseg_hint : nseg;
   s->nseg = nseg;
   A.nseg = int32_t(nseg);
+  A.nseg_dev = dev_count ? scal : nullptr;
   A.seg_start = s->seg.as<int64_t>();
   const DevProgram& D = P.dev;
   NfaCaps cap = kCaps;
@@ -808,7 +849,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   // first-allocation words of every key (NfaCaps) plus the events carried into the batch
   const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base + 16;
   const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 4 + 3 * D.nstates;
-  int64_t est = nseg * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
+  int64_t est = nseg_est * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
   s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
   const int64_t pool_base = s->pool_words;         // what the batch starts with (kept for the next batch)
   A.cap = cap;
@@ -873,12 +914,21 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     timed = true;
     // the CSR's match / entry counts are scanned right away, so that one synchronisation reads them
     // with the pool flags (a retried attempt scans again)
-    HIPCHECK(exclusive_scan(s->r_matches.as<int64_t>(), nseg, s->moff.as<int64_t>(), scal + 3, s->scan_tmp.as<int64_t>(), st));
-    HIPCHECK(exclusive_scan(s->r_words.as<int64_t>(), nseg, s->eoff.as<int64_t>(), scal + 4, s->scan_tmp.as<int64_t>(), st));
+    HIPCHECK(exclusive_scan_pair(s->r_matches.as<int64_t>(), s->r_words.as<int64_t>(), nseg, A.nseg_dev,
+                                 s->moff.as<int64_t>(), s->eoff.as<int64_t>(), scal + 3, scal + 4,
+                                 s->scan_tmp.as<int64_t>(), st));
     unsigned long long res[5];
+    int64_t sc[5];                                 // [0] segments, [3] matches, [4] entries
     HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(tots, scal + 3, 16, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(sc, scal, sizeof sc, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
+    tots[0] = sc[3];
+    tots[1] = sc[4];
+    if (dev_count && attempt == 0) {               // the exact count from here on
+      nseg = sc[0];
+      s->nseg = nseg;
+      A.nseg = int32_t(nseg);
+    }
     s->g_any_err = res[4] != 0;
     const int32_t* fl = reinterpret_cast<const int32_t*>(res + 2);
     if (fl[2]) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
@@ -906,6 +956,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     }
   }
   // compaction into the CSR (counts scanned with the last attempt)
+  s->nseg_hint = nseg;
   s->g_matches = tots[0];
   s->g_entries = tots[1];
   const size_t nm = size_t(std::max<int64_t>(tots[0], 1)), ne = size_t(std::max<int64_t>(tots[1], 1));

@@ -426,18 +426,13 @@ std::shared_ptr<const JitModule> jit_runs(const Program& P, std::string& why) {
 std::string jit_source_general(const Program& P, std::string& why, bool phases) {
   std::string o = phases ? "#define KCEP_PHASES 1\n#include \"interp.h\"\n" : "#include \"interp.h\"\n";
   if (!gen_program(P, o, why)) return "";
-  // waves per SIMD the register budget is cut for (KCEP_NFA_WAVES, tuning only)
-  const char* wenv = getenv("KCEP_NFA_WAVES");
-  const int waves = wenv ? std::min(8, std::max(1, atoi(wenv))) : 2;
-  // the same for the wave kernel (KCEP_NFA_WAVE_OCC)
-  const char* oenv = getenv("KCEP_NFA_WAVE_OCC");
-  // 3 waves per SIMD (166 VGPRs, no spills).  r05, C4 with 16-byte frames: 4 waves (128 VGPRs) runs the
-  // kernel in 4.67 vs 4.92 ms but spills ~50 VGPRs, whose scratch lines reach HBM: 5.5 GB per launch
-  // against 0.28 GB (profiles/r05_c4_occupancy.txt); r02: 2: 13.3, 3: 10.8, 4: 11.8 ms
-  const int wave_occ = oenv ? std::min(8, std::max(1, atoi(oenv))) : 3;
-  // LDS arena words of the wave kernel's key workspace (KCEP_WAVE_ARENA, tuning only)
-  const char* aenv = getenv("KCEP_WAVE_ARENA");
-  if (aenv) o += "#define WAVE_ARENA " + std::to_string(std::min(8192, std::max(4, atoi(aenv)))) + "\n";
+  // waves per SIMD the register budgets are cut for: the lane kernel 2; the wave kernel 3 (166 VGPRs, no
+  // spills).  r05, C4 with 16-byte frames: 4 waves (128 VGPRs) ran the kernel in 4.67 vs 4.92 ms but
+  // spilled ~50 VGPRs, whose scratch lines reach HBM: 5.5 GB per launch against 0.28 GB
+  // (profiles/r05_c4_occupancy.txt); r02: 2: 13.3, 3: 10.8, 4: 11.8 ms.  The wave kernel's LDS arena
+  // (nfa_wave.h WAVE_ARENA) stays at 1024 words: 512 5.82-5.85, 1280 4.95-4.97, 1536 4.95-4.96, 1792
+  // 5.25-5.26, 2048 5.21-5.24 vs 1024 4.97-4.98 ms kernel (r05, gpurun_out/ab/arena*)
+  const int waves = 2, wave_occ = 3;
   const std::string agg = wave_stateful(P.dev) || P.has_seq ? "true" : "false";
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "
        "__attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + R"())) void kcep_nfa_kernel(kcep::NfaArgs A) {

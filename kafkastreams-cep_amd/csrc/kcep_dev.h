@@ -130,7 +130,8 @@ struct NfaArgs {
   int64_t n;
   int64_t base;                   // stream position of batch record 0 (carry sessions; else 0)
   int32_t mode;
-  int32_t nseg;
+  int32_t nseg;                   // key segments (an upper bound when nseg_dev is set)
+  const int64_t* nseg_dev;        // wave kernel: the segment count on the device (nullptr: nseg is exact)
   const int64_t* seg_start;       // nseg + 1
   int32_t* pool;                  // per-batch workspace pool
   int64_t pool_cap;
@@ -185,11 +186,12 @@ struct RunsArgs {
   unsigned long long* err_list;
   unsigned long long* err_n;
   int64_t err_cap;
-  // runs_sim: the stages a run consumed, as up to RUNS_MAX_SEGS segments per start record j:
-  // segs[j * RUNS_MAX_SEGS + i] = stage << 24 | offset of the segment's first record from j,
-  // terminated by ~0u when shorter (a run's consumed stages never increase, runs.hip); null: off
-  uint32_t* segs;
-  unsigned long long* seg_over;   // set when a run needs more segments or an offset >= 2^24
+  // runs_sim: the stages a run consumed, as up to segn (4 or 8) segments per start record j:
+  // segs[j * segn + i] = stage << 12 | offset of the segment's first record from j (stage < 16, offset
+  // < 4096), terminated by 0xFFFF when shorter (a run's consumed stages never increase, runs.hip); null: off
+  uint16_t* segs;
+  int32_t segn;
+  unsigned long long* seg_over;   // set when a run needs more segments, a stage >= 16 or an offset >= 4096
   // carry sessions (runs.hip, carried tails): stream position of every record (null: base + index);
   // runs ending or failing at a position < emit_from were handled by an earlier batch (not emitted)
   const int64_t* pos;

@@ -39,6 +39,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/kcep.h"
 #include "kcep_internal.h"
 #include "interp.h"
@@ -60,21 +62,75 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void nf
 }
 
 // ---- segments, scans, output compaction, carry commit ----
-__global__ void seg_mark(const int32_t* __restrict__ key, int64_t n, int64_t* __restrict__ flag) {
-  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) flag[i] = (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+// Key segments of a grouped batch in three passes over 1024-record blocks: boundaries per block, the
+// blocks' exclusive prefix (scan_sums_reg), then every boundary's segment start.  flag / idx (optional:
+// the runs carry build reads them) get the per-record boundary flag and its exclusive prefix.
+__device__ __forceinline__ int64_t block_excl_256(int64_t v, int64_t* s, int64_t& total) {
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const int64_t y = threadIdx.x >= unsigned(d) ? s[threadIdx.x - d] : 0;
+    __syncthreads();
+    s[threadIdx.x] += y;
+    __syncthreads();
+  }
+  total = s[255];
+  return s[threadIdx.x] - v;
 }
-__global__ void seg_scatter(const int64_t* __restrict__ flag, const int64_t* __restrict__ idx, int64_t n,
-                            int64_t* __restrict__ seg_start) {
-  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n && flag[i]) seg_start[idx[i]] = i;
-  if (i == 0) seg_start[idx[n - 1] + flag[n - 1]] = n;
+__global__ void seg_count(const int32_t* __restrict__ key, int64_t n, int64_t* __restrict__ bsum) {
+  __shared__ int64_t s[256];
+  const int64_t b0 = int64_t(blockIdx.x) * 1024 + threadIdx.x * 4;
+  int64_t acc = 0;
+  for (int k = 0; k < 4; k++) {
+    const int64_t i = b0 + k;
+    if (i < n) acc += (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+  }
+  int64_t tot = 0;
+  block_excl_256(acc, s, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+__global__ void seg_write(const int32_t* __restrict__ key, int64_t n, const int64_t* __restrict__ boff,
+                          const int64_t* __restrict__ nseg, int64_t* __restrict__ seg_start, int64_t* __restrict__ flag,
+                          int64_t* __restrict__ idx) {
+  __shared__ int64_t s[256];
+  const int64_t b0 = int64_t(blockIdx.x) * 1024 + threadIdx.x * 4;
+  int f[4], acc = 0;
+  for (int k = 0; k < 4; k++) {
+    const int64_t i = b0 + k;
+    f[k] = i < n && (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+    acc += f[k];
+  }
+  int64_t tot = 0;
+  int64_t run = boff[blockIdx.x] + block_excl_256(acc, s, tot);
+  for (int k = 0; k < 4; k++) {
+    const int64_t i = b0 + k;
+    if (i >= n) break;
+    if (f[k]) seg_start[run] = i;
+    if (flag) { flag[i] = f[k]; idx[i] = run; }
+    run += f[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) seg_start[*nseg] = n;
 }
 
-// exclusive scan, 1024 elements per block: (1) block sums, (2) scan of block sums
-// in one block, (3) per-block scan + offset
-__global__ void scan_blocks(const int64_t* __restrict__ in, int64_t n, int64_t* __restrict__ bsum) {
+// exclusive scans, 1024 elements per block: (1) block sums, (2) scan of block sums in one block,
+// (3) per-block scan + offset.  Two arrays of one length at once (blockIdx.y / the block of pass 2
+// picks the array; tmp holds 2 x the block count); n_dev (optional): the length on the device, at
+// most n (the grid is sized by n).
+struct ScanPair {
+  const int64_t* in[2];
+  int64_t* out[2];
+  int64_t* total[2];
+  int64_t n;
+  const int64_t* n_dev;
+  int64_t nb;                     // blocks of the grid (from n)
+};
+__device__ __forceinline__ int64_t scan_len(const ScanPair& S) {
+  return S.n_dev ? (*S.n_dev < S.n ? *S.n_dev : S.n) : S.n;
+}
+__global__ void scan_blocks(ScanPair S, int64_t* __restrict__ bsum) {
   __shared__ int64_t s[256];
+  const int64_t n = scan_len(S);
+  const int64_t* __restrict__ in = S.in[blockIdx.y];
   const int64_t b0 = int64_t(blockIdx.x) * 1024;
   int64_t acc = 0;
   for (int k = 0; k < 4; k++) {
@@ -84,10 +140,10 @@ __global__ void scan_blocks(const int64_t* __restrict__ in, int64_t n, int64_t* 
   s[threadIdx.x] = acc;
   __syncthreads();
   for (int d = 128; d > 0; d >>= 1) {
-    if (threadIdx.x < d) s[threadIdx.x] += s[threadIdx.x + d];
+    if (threadIdx.x < unsigned(d)) s[threadIdx.x] += s[threadIdx.x + d];
     __syncthreads();
   }
-  if (threadIdx.x == 0) bsum[blockIdx.x] = s[0];
+  if (threadIdx.x == 0) bsum[blockIdx.y * S.nb + blockIdx.x] = s[0];
 }
 __global__ void scan_sums(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
   __shared__ int64_t s[256];
@@ -98,7 +154,7 @@ __global__ void scan_sums(int64_t* __restrict__ bsum, int64_t nb, int64_t* __res
     s[threadIdx.x] = v;
     __syncthreads();
     for (int d = 1; d < 256; d <<= 1) {
-      const int64_t y = threadIdx.x >= d ? s[threadIdx.x - d] : 0;
+      const int64_t y = threadIdx.x >= unsigned(d) ? s[threadIdx.x - d] : 0;
       __syncthreads();
       s[threadIdx.x] += y;
       __syncthreads();
@@ -113,7 +169,7 @@ __global__ void scan_sums(int64_t* __restrict__ bsum, int64_t nb, int64_t* __res
 // thread holds its 16 consecutive sums in registers, one wave-level and one block-level scan (the loop
 // above walks the sums 256 at a time, two barriers per step: 44 us for 10 M elements)
 constexpr int SCAN_REG = 16;
-__global__ __launch_bounds__(1024) void scan_sums_reg(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
+__device__ __forceinline__ void scan_sums_reg_body(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
   __shared__ int64_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t per = (nb + 1023) / 1024, a = tid * per;
@@ -138,25 +194,28 @@ __global__ __launch_bounds__(1024) void scan_sums_reg(int64_t* __restrict__ bsum
     if (i < per && a + i < nb) { bsum[a + i] = run; run += v[i]; }
   if (tid == 1023) *total = run;
 }
-__global__ void scan_final(const int64_t* __restrict__ in, int64_t n, const int64_t* __restrict__ bsum,
-                           int64_t* __restrict__ out) {
+__global__ __launch_bounds__(1024) void scan_sums_reg(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
+  scan_sums_reg_body(bsum, nb, total);
+}
+__global__ __launch_bounds__(1024) void scan_sums_pair(ScanPair S, int64_t* __restrict__ bsum) {
+  const int64_t nb = (scan_len(S) + 1023) / 1024;
+  scan_sums_reg_body(bsum + blockIdx.x * S.nb, nb, S.total[blockIdx.x]);
+}
+__global__ void scan_final(ScanPair S, const int64_t* __restrict__ bsum) {
   __shared__ int64_t s[256];
+  const int64_t n = scan_len(S);
+  const int64_t* __restrict__ in = S.in[blockIdx.y];
+  int64_t* __restrict__ out = S.out[blockIdx.y];
   const int64_t b0 = int64_t(blockIdx.x) * 1024;
+  if (b0 >= n) return;                             // (whole block: the barriers below stay uniform)
   int64_t v[4], acc = 0;
   for (int k = 0; k < 4; k++) {
     const int64_t i = b0 + threadIdx.x * 4 + k;
     v[k] = i < n ? in[i] : 0;
     acc += v[k];
   }
-  s[threadIdx.x] = acc;
-  __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {
-    const int64_t y = threadIdx.x >= d ? s[threadIdx.x - d] : 0;
-    __syncthreads();
-    s[threadIdx.x] += y;
-    __syncthreads();
-  }
-  int64_t run = bsum[blockIdx.x] + s[threadIdx.x] - acc;
+  int64_t tot = 0;
+  int64_t run = bsum[blockIdx.y * S.nb + blockIdx.x] + block_excl_256(acc, s, tot);
   for (int k = 0; k < 4; k++) {
     const int64_t i = b0 + threadIdx.x * 4 + k;
     if (i < n) out[i] = run;
@@ -210,10 +269,27 @@ hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* t
                           hipStream_t st) {
   if (n <= 0) return hipMemsetAsync(total, 0, sizeof(int64_t), st);
   const int64_t nb = (n + 1023) / 1024;
-  hipLaunchKernelGGL(scan_blocks, dim3(unsigned(nb)), dim3(256), 0, st, in, n, tmp);
+  const ScanPair S{{in, in}, {out, out}, {total, total}, n, nullptr, nb};
+  hipLaunchKernelGGL(scan_blocks, dim3(unsigned(nb)), dim3(256), 0, st, S, tmp);
   if (nb <= int64_t(SCAN_REG) * 1024) hipLaunchKernelGGL(scan_sums_reg, dim3(1), dim3(1024), 0, st, tmp, nb, total);
   else hipLaunchKernelGGL(scan_sums, dim3(1), dim3(256), 0, st, tmp, nb, total);
-  hipLaunchKernelGGL(scan_final, dim3(unsigned(nb)), dim3(256), 0, st, in, n, tmp, out);
+  hipLaunchKernelGGL(scan_final, dim3(unsigned(nb)), dim3(256), 0, st, S, tmp);
+  return hipGetLastError();
+}
+
+// Two exclusive scans of one length n (or *n_dev <= n, read on the device) in one set of launches;
+// tmp: 2 x ceil(n / 1024) words.  Up to 16 M elements.
+hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
+                               int64_t* out1, int64_t* total0, int64_t* total1, int64_t* tmp, hipStream_t st) {
+  const int64_t nb = (std::max<int64_t>(n, 1) + 1023) / 1024;
+  if (nb > int64_t(SCAN_REG) * 1024) {
+    hipError_t e = exclusive_scan(in0, n, out0, total0, tmp, st);
+    return e != hipSuccess ? e : exclusive_scan(in1, n, out1, total1, tmp, st);
+  }
+  const ScanPair S{{in0, in1}, {out0, out1}, {total0, total1}, std::max<int64_t>(n, 0), n_dev, nb};
+  hipLaunchKernelGGL(scan_blocks, dim3(unsigned(nb), 2), dim3(256), 0, st, S, tmp);
+  hipLaunchKernelGGL(scan_sums_pair, dim3(2), dim3(1024), 0, st, S, tmp);
+  hipLaunchKernelGGL(scan_final, dim3(unsigned(nb), 2), dim3(256), 0, st, S, tmp);
   return hipGetLastError();
 }
 
@@ -292,14 +368,16 @@ __global__ void carry_move(int64_t* __restrict__ ctab, int64_t nkeys, const int3
   ctab[k] = off[k];
 }
 
+// flag / idx: nullptr, or n words each (the runs carry build's per-record boundary flags); tmp:
+// ceil(n / 1024) + 1 words.  *nseg: the segment count (device).
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st) {
   if (n <= 0) return hipMemsetAsync(nseg, 0, sizeof(int64_t), st);
-  const unsigned b = unsigned((n + 255) / 256);
-  hipLaunchKernelGGL(seg_mark, dim3(b), dim3(256), 0, st, key, n, flag);
-  hipError_t e = exclusive_scan(flag, n, idx, nseg, tmp, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_scatter, dim3(b), dim3(256), 0, st, flag, idx, n, seg_start);
+  const int64_t nb = (n + 1023) / 1024;
+  hipLaunchKernelGGL(seg_count, dim3(unsigned(nb)), dim3(256), 0, st, key, n, tmp);
+  if (nb <= int64_t(SCAN_REG) * 1024) hipLaunchKernelGGL(scan_sums_reg, dim3(1), dim3(1024), 0, st, tmp, nb, nseg);
+  else hipLaunchKernelGGL(scan_sums, dim3(1), dim3(256), 0, st, tmp, nb, nseg);
+  hipLaunchKernelGGL(seg_write, dim3(unsigned(nb)), dim3(256), 0, st, key, n, tmp, nseg, seg_start, flag, idx);
   return hipGetLastError();
 }
 

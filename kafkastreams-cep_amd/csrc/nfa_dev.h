@@ -1404,7 +1404,7 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
 #else
     for (int i = 0; i < 11; i++) pr[3 + i] = -1;
 #endif
-    pr[14] = 0;                                                        // (reserved)
+    pr[14] = int64_t(t0);                                                // start (wall clock, 100 MHz)
     pr[15] = l.pool_words;
 #ifdef KCEP_PHASES
     for (int i = 0; i <= AK_N; i++) pr[16 + i] = prof ? int64_t(prof->kw[i]) : -1;   // words per kind, the pool's share

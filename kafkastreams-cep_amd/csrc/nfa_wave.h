@@ -38,7 +38,7 @@ constexpr int WAVE = 64;
 // ms per step): arena 2048 + lists in the pool 8.43; 1024 + 16 7.78; 1024 + 12 8.02; 1024 + 20 8.23;
 // 1280 + 16 8.22; 768 + 16 9.75; 512 + 32 10.9; 4 waves per SIMD 11.2
 #ifndef WAVE_ARENA
-#define WAVE_ARENA 1024                    // LDS words per key workspace (KCEP_WAVE_ARENA A/B: 0 = pool only)
+#define WAVE_ARENA 1024                    // LDS words per key workspace (jit.cpp: the sizes measured)
 #endif
 #ifndef WAVE_PRIV
 #define WAVE_PRIV 16                       // LDS words per lane for its private run list + operation log
@@ -782,11 +782,12 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
   __shared__ __attribute__((aligned(16))) int32_t s_priv[WAVE * WAVE_PRIV];
   const Grp<WAVE> gp{int(threadIdx.x), 0};
   int32_t* scr = A.scratch_words > 0 ? A.scratch + int64_t(blockIdx.x) * A.scratch_words : nullptr;
+  const int32_t nseg = A.nseg_dev ? int32_t(*A.nseg_dev) : A.nseg;   // (counted on the device: no host round trip)
   for (;;) {
     int seg = 0;
     if (gp.gl == 0) seg = atomicAdd(A.seg_next, 1);
     seg = gp.bcast(seg);
-    if (seg >= A.nseg) break;                      // every wave of the grid reaches this
+    if (seg >= nseg) break;                        // every wave of the grid reaches this
     wave_key<AGG, WAVE>(A, seg, gp, ws, s_arena, ARENA, s_priv, scr);
     wave_sync();
   }

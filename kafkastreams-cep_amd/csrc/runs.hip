@@ -80,6 +80,14 @@ __global__ __launch_bounds__(256) void runs_compact(const int32_t* __restrict__ 
 // pre[w], pre[W + w]; the totals into *tot_cnt / *tot_len
 // (each thread sums a contiguous run of chunks, one block scan of the thread sums, then the thread
 // writes its run's prefixes: one pass, two barriers)
+// by_end: the chunks' runs counted by the chunk they END in (runs_sim's stat[2W..6W): those ending in
+// chunk w are chunk w's own plus chunk w - 1's that ran over)
+template <bool by_end>
+__device__ __forceinline__ int64_t chunk_stat(const int64_t* __restrict__ stat, int64_t W, int q, int64_t w) {
+  if (!by_end) return stat[q * W + w];
+  return stat[(2 + q) * W + w] + (w > 0 ? stat[(4 + q) * W + w - 1] : 0);
+}
+template <bool by_end>
 __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restrict__ stat, int64_t nw, int64_t W,
                                                         int64_t* __restrict__ pre, int64_t* __restrict__ tot_cnt,
                                                         int64_t* __restrict__ tot_len) {
@@ -91,8 +99,8 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
     int64_t cc[8], ll[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      cc[q] = w + q < w1 ? stat[w + q] : 0;
-      ll[q] = w + q < w1 ? stat[W + w + q] : 0;
+      cc[q] = w + q < w1 ? chunk_stat<by_end>(stat, W, 0, w + q) : 0;
+      ll[q] = w + q < w1 ? chunk_stat<by_end>(stat, W, 1, w + q) : 0;
     }
 #pragma unroll
     for (int q = 0; q < 8; q++) { c += cc[q]; l += ll[q]; }
@@ -110,8 +118,8 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
   for (int64_t w = w0; w < w1; w++) {
     pre[w] = oc;
     pre[W + w] = ol;
-    oc += stat[w];
-    ol += stat[W + w];
+    oc += chunk_stat<by_end>(stat, W, 0, w);
+    ol += chunk_stat<by_end>(stat, W, 1, w);
   }
   if (threadIdx.x == 1023) {
     int64_t tc = 0, tl = 0;
@@ -127,7 +135,7 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
 // overlaps run i, so with every run's span e - s <= W: j < i has s_j >= s_i - W, j > i has s_j < e_i <=
 // s_i + W, and (distinct starts) |i - j| <= W.  A workgroup ranks 256 runs against the window of runs
 // [first - W, last + W] staged in LDS (W <= RUNS_ORDER_MAX_W; wider batches take the radix sort).
-static_assert(RUNS_MAX_SEGS == 8, "runs_expand loads a run's segments as two uint4");
+static_assert(RUNS_MAX_SEGS == 8, "a run's segments are at most one uint4 of 16-bit words");
 constexpr int RUNS_ORDER_MAX_W = 1024;
 constexpr int RUNS_ORDER_WIN = 256 + 2 * RUNS_ORDER_MAX_W;
 // The backward count skips whole groups of 16 window entries whose latest end is <= e: no run there
@@ -179,8 +187,31 @@ __global__ __launch_bounds__(256) void runs_order(const unsigned long long* __re
 // entries final stage first (peek, SharedVersionedBufferStoreImpl.java:176-201).  A workgroup owns
 // 256 consecutive matches and writes their entries as one contiguous range, thread-strided (coalesced
 // stores); an entry finds its match by a binary search over the workgroup's entry offsets in LDS.
+// the stage of the record `o` records after the run's start, from its packed segments (runs_sim)
+__device__ __forceinline__ uint32_t seg_word(const uint4& v, int i) {
+  const uint32_t w = i < 2 ? v.x : i < 4 ? v.y : i < 6 ? v.z : v.w;
+  return (i & 1) ? w >> 16 : w & 0xFFFF;
+}
+__device__ __forceinline__ int seg_stage(const uint4& v, int segn, int64_t o) {
+  int stage = 0;
+#pragma unroll
+  for (int i = 0; i < RUNS_MAX_SEGS; i++) {        // the segment holding offset o (segments ascend)
+    if (i >= segn) break;
+    const uint32_t w = seg_word(v, i);
+    if (w == 0xFFFF) break;
+    if (int64_t(w & 0xFFF) <= o) stage = int(w >> 12);
+  }
+  return stage;
+}
+__device__ __forceinline__ uint4 seg_load(const uint16_t* __restrict__ segs, int segn, int64_t j) {
+  if (segn == 4) {
+    const uint2 a = *reinterpret_cast<const uint2*>(segs + j * 4);
+    return make_uint4(a.x, a.y, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  }
+  return *reinterpret_cast<const uint4*>(segs + j * 8);
+}
 __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
-                                                   const int64_t* __restrict__ pos, const uint32_t* __restrict__ segs,
+                                                   const int64_t* __restrict__ pos, const uint16_t* __restrict__ segs, int segn,
                                                    const unsigned long long* __restrict__ sorted, int64_t nm,
                                                    const int64_t* __restrict__ ent_off, int64_t ne, int64_t base,
                                                    int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
@@ -188,7 +219,7 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
                                                    int64_t* __restrict__ ent_record) {
   __shared__ int64_t s_at[257];
   __shared__ int64_t s_j[256], s_e[256];
-  __shared__ uint32_t s_seg[256][RUNS_MAX_SEGS];
+  __shared__ uint4 s_seg[256];
   const int tid = threadIdx.x;
   const int64_t m0 = int64_t(blockIdx.x) * 256, m = m0 + tid;
   const int cnt = nm - m0 < 256 ? int(nm - m0) : 256;
@@ -202,12 +233,7 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
     match_record[m] = pos ? pos[e] : base + e;
     match_key[m] = key[j];
     if (ent_off_out != ent_off) ent_off_out[m] = at;
-    // the segments as two 16-B vectors, the second only when the first holds no terminator
-    const uint4* sv = reinterpret_cast<const uint4*>(segs + j * RUNS_MAX_SEGS);
-    const uint4 a = sv[0];
-    const uint4 b = a.w == ~0u ? make_uint4(~0u, ~0u, ~0u, ~0u) : sv[1];
-    s_seg[tid][0] = a.x; s_seg[tid][1] = a.y; s_seg[tid][2] = a.z; s_seg[tid][3] = a.w;
-    s_seg[tid][4] = b.x; s_seg[tid][5] = b.y; s_seg[tid][6] = b.z; s_seg[tid][7] = b.w;
+    s_seg[tid] = seg_load(segs, segn, j);
   }
   if (tid == 0) s_at[cnt] = m0 + cnt < nm ? ent_off[m0 + cnt] : ne;
   __syncthreads();
@@ -220,15 +246,141 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
     }
     const int64_t j = s_j[lo], e = s_e[lo];
     const int64_t o = (e - j) - (x - s_at[lo]);       // offset of the entry's record from the start
-    uint32_t stage = 0;
-#pragma unroll
-    for (int i = 0; i < RUNS_MAX_SEGS; i++) {        // the segment holding offset o (segments ascend)
-      const uint32_t w = s_seg[lo][i];
-      if (w != ~0u && int64_t(w & 0xFFFFFFu) <= o) stage = w >> 24;
-      if (w == ~0u) break;
-    }
-    ent_name[x] = P->st[stage].name;
+    ent_name[x] = P->st[seg_stage(s_seg[lo], segn, o)].name;
     ent_record[x] = pos ? pos[j + o] : base + j + o;
+  }
+}
+
+// The CSR straight from runs_sim's results when every completed run spans fewer records than a chunk
+// (so a run ends in its start's chunk or the next): one workgroup per chunk of END records [c0, c1).
+// Its runs start in [c0 - span, c1); they are bucketed by end record in LDS (counting sort, each
+// bucket then ordered by start), which is (completing record, start) order -- NFA.matchPattern's --
+// and placed at the chunk's prefix of the end-chunk counts / entry counts (runs_chunk_scan<true>).
+// Match headers, then the entries (final stage first, peek :176-201) thread-strided over the chunk's
+// contiguous entry range, each entry's stage from its run's packed segments.  Replaces runs_compact +
+// runs_order + the entry-offset scan + runs_expand (one pass over end_of and the segments instead of a
+// start-ordered list, a sorted copy, a length array and gathers at start positions).
+constexpr int RUNS_EMIT_MAX = 2 * RUNS_CHUNK;      // window of starts: chunk + span < 2 chunks
+__global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
+                                                 const int64_t* __restrict__ pos, int64_t base,
+                                                 const uint16_t* __restrict__ segs, int segn,
+                                                 const int32_t* __restrict__ end_of, int64_t n, int chunk, int span,
+                                                 const int64_t* __restrict__ pre, int64_t W,
+                                                 int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
+                                                 int64_t* __restrict__ ent_off, int32_t* __restrict__ ent_name,
+                                                 int64_t* __restrict__ ent_record) {
+  __shared__ int32_t s_cnt[RUNS_CHUNK + 1], s_fill[RUNS_CHUNK];
+  __shared__ int32_t s_run[RUNS_EMIT_MAX];         // window offset of the start | end slot << 11
+  __shared__ int32_t s_at[RUNS_EMIT_MAX + 1];      // the runs' entry offsets in the chunk
+  __shared__ int32_t s_w[4];
+  const int tid = threadIdx.x;
+  const int64_t c = blockIdx.x, c0 = c * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+  const int E = int(c1 - c0);
+  const int64_t lo = c0 - span > 0 ? c0 - span : 0;
+  const int L = int(c1 - lo);                      // <= chunk + span < RUNS_EMIT_MAX
+  for (int x = tid; x < E; x += 256) { s_cnt[x] = 0; s_fill[x] = 0; }
+  __syncthreads();
+  int32_t my[RUNS_EMIT_MAX / 256];                 // this thread's window entries: end slot, or -1
+#pragma unroll
+  for (int q = 0; q < RUNS_EMIT_MAX / 256; q++) {
+    const int x = tid + 256 * q;
+    my[q] = -1;
+    if (x < L) {
+      const int64_t e = end_of[lo + x];
+      if (e >= c0 && e < c1) {
+        my[q] = int32_t(e - c0);
+        atomicAdd(&s_cnt[my[q]], 1);
+      }
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the end slots' counts (up to 4 per thread)
+  int v[4], acc = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int x = 4 * tid + q;
+    v[q] = x < E ? s_cnt[x] : 0;
+    acc += v[q];
+  }
+  int inc = acc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(inc, d, 64);
+    if ((tid & 63) >= d) inc += y;
+  }
+  if ((tid & 63) == 63) s_w[tid >> 6] = inc;
+  __syncthreads();
+  int run = inc - acc;
+  for (int w = 0; w < (tid >> 6); w++) run += s_w[w];
+  const int M = s_w[0] + s_w[1] + s_w[2] + s_w[3];  // the chunk's runs
+  __syncthreads();                                 // (s_cnt read above before it is overwritten)
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int x = 4 * tid + q;
+    if (x < E) s_cnt[x] = run;
+    run += v[q];
+  }
+  if (tid == 0) s_cnt[E] = M;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < RUNS_EMIT_MAX / 256; q++)
+    if (my[q] >= 0) s_run[s_cnt[my[q]] + atomicAdd(&s_fill[my[q]], 1)] = (tid + 256 * q) | my[q] << 11;
+  __syncthreads();
+  // each end record's runs by start (insertion sort: buckets hold a few runs)
+  for (int x = tid; x < E; x += 256) {
+    const int b0 = s_cnt[x], b1 = s_cnt[x + 1];
+    for (int i = b0 + 1; i < b1; i++) {
+      const int32_t t = s_run[i];
+      int k = i - 1;
+      while (k >= b0 && s_run[k] > t) { s_run[k + 1] = s_run[k]; k--; }
+      s_run[k + 1] = t;
+    }
+  }
+  __syncthreads();
+  // the runs' entry offsets: thread tid owns runs [R tid, R tid + R)
+  const int R = (M + 255) / 256;
+  int lens = 0;
+  for (int i = R * tid; i < R * tid + R && i < M; i++) {
+    const int32_t r = s_run[i];
+    lens += int(c0 + (r >> 11) - (lo + (r & 2047))) + 1;
+  }
+  inc = lens;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(inc, d, 64);
+    if ((tid & 63) >= d) inc += y;
+  }
+  __syncthreads();                                 // (s_w of the first scan read)
+  if ((tid & 63) == 63) s_w[tid >> 6] = inc;
+  __syncthreads();
+  run = inc - lens;
+  for (int w = 0; w < (tid >> 6); w++) run += s_w[w];
+  const int NE = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  for (int i = R * tid; i < R * tid + R && i < M; i++) {
+    s_at[i] = run;
+    const int32_t r = s_run[i];
+    run += int(c0 + (r >> 11) - (lo + (r & 2047))) + 1;
+  }
+  if (tid == 0) s_at[M] = NE;
+  __syncthreads();
+  const int64_t mb = pre[c], eb = pre[W + c];
+  for (int i = tid; i < M; i += 256) {
+    const int64_t e = c0 + (s_run[i] >> 11);
+    match_record[mb + i] = pos ? pos[e] : base + e;
+    match_key[mb + i] = key[e];
+    ent_off[mb + i] = eb + s_at[i];
+  }
+  for (int x = tid; x < NE; x += 256) {
+    int a = 0, b = M - 1;                          // the last run whose range starts at or before x
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (s_at[mid] <= x) a = mid; else b = mid - 1;
+    }
+    const int32_t r = s_run[a];
+    const int64_t j = lo + (r & 2047), e = c0 + (r >> 11);
+    const int64_t o = (e - j) - (x - s_at[a]);     // offset of the entry's record from the start
+    ent_name[eb + x] = P->st[seg_stage(seg_load(segs, segn, j), segn, o)].name;
+    ent_record[eb + x] = pos ? pos[j + o] : base + j + o;
   }
 }
 
@@ -404,7 +556,7 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
   const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
   if (chunk > RUNS_CHUNK || chunk < 64 || (chunk & (chunk - 1))) return hipErrorInvalidValue;
   if (nw <= (int64_t(1) << 16)) {
-    hipLaunchKernelGGL(runs_chunk_scan, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
+    hipLaunchKernelGGL(runs_chunk_scan<false>, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
   } else {
     hipError_t e = exclusive_scan(stat, nw, pre, tot_cnt, scan_tmp, st);
     if (e == hipSuccess) e = exclusive_scan(stat + W, nw, pre + W, tot_len, scan_tmp, st);
@@ -450,8 +602,29 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
                               int64_t ne, int64_t* match_record, int32_t* match_key, int64_t* ent_off_out, int32_t* ent_name,
                               int64_t* ent_record, hipStream_t st) {
   if (nm <= 0) return hipSuccess;
-  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, sorted, nm,
+  hipLaunchKernelGGL(runs_expand, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, R.P, R.key, R.pos, R.segs, R.segn, sorted, nm,
                      ent_off, ne, R.base, match_record, match_key, ent_off_out, ent_name, ent_record);
+  return hipGetLastError();
+}
+
+// runs_emit's chunk prefixes: the runs and entries ending in each chunk, scanned (pre: 2 W entries),
+// with the batch's totals into *tot_cnt / *tot_len.  False when the chunks are too many for one
+// scanning workgroup (then the batch takes runs_compact + runs_order / the sort instead).
+bool runs_emit_scan(const int64_t* stat, int64_t n, int32_t chunk, int64_t* pre, int64_t* tot_cnt, int64_t* tot_len,
+                    hipStream_t st) {
+  const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
+  if (n <= 0 || nw > (int64_t(1) << 16) || chunk > RUNS_CHUNK) return false;
+  hipLaunchKernelGGL(runs_chunk_scan<true>, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
+  return true;
+}
+// the CSR from runs_sim's results (runs_emit_scan's pre); span: the longest completed span (< chunk)
+hipError_t runs_emit_launch(const RunsArgs& R, const int32_t* end_of, const int64_t* pre, int span, int64_t* match_record,
+                            int32_t* match_key, int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st) {
+  const int64_t nw = (R.n + R.chunk - 1) / R.chunk, W = int64_t(runs_blocks(R.n, R.chunk)) * (RT / 64);
+  if (R.n <= 0) return hipSuccess;
+  if (span < 0 || span >= R.chunk || R.chunk > RUNS_CHUNK || !R.segs) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(runs_emit, dim3(unsigned(nw)), dim3(256), 0, st, R.P, R.key, R.pos, R.base, R.segs, R.segn, end_of,
+                     R.n, R.chunk, span, pre, W, match_record, match_key, ent_off, ent_name, ent_record);
   return hipGetLastError();
 }
 

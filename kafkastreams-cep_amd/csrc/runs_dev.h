@@ -236,7 +236,9 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
 // end_of[j] = completing record of the run started at record j (-1 none, -2 open at the key's last
 // carried record), and per wave chunk w its completed runs and their total length, stat[w] and
 // stat[W + w] (W = the launch's waves: runs_compact places the chunk's runs at the scan of the
-// counts, so no per-record flag array and no device-wide scan over it); the longest completed span
+// counts, so no per-record flag array and no device-wide scan over it); the same split by the chunk
+// the run ENDS in -- this chunk, stat[2W + w] / stat[3W + w], or the next one, stat[4W + w] /
+// stat[5W + w] (runs_emit, when every span is shorter than a chunk); the longest completed span
 // into *A.max_span.  With A.segs, also the run's consumed stages as segments (so runs_expand writes
 // the traversal without walking the run again).  Both are staged in LDS: a lane's segments while its
 // run is open (stored once, as two 16-B vectors, when the run completes -- and not at all when it
@@ -245,12 +247,12 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
 template <class Tab>
 __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, int64_t* __restrict__ stat,
                                               int32_t* __restrict__ end_of) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_seg[RT][RUNS_MAX_SEGS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_seg[RT][RUNS_MAX_SEGS];
   __shared__ int32_t s_end[RT / 64][RUNS_CHUNK];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
   const int64_t i0 = wave * A.chunk, i1 = i0 + A.chunk < A.n ? i0 + A.chunk : A.n;
-  uint32_t* const myseg = s_seg[threadIdx.x];
+  uint16_t* const myseg = s_seg[threadIdx.x];
   if (i0 < A.n) {
     int64_t seg_item = -1;                                      // the lane's current start record
     int seg_last = -1, seg_n = 0;
@@ -276,14 +278,10 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
           }
           if (A.segs && res.end >= 0 && !old_end) {
             if (seg_item != i) seg_n = 0;
-            for (int q = seg_n; q < RUNS_MAX_SEGS; q++) myseg[q] = ~0u;   // terminator (and padding)
-            uint4* d = reinterpret_cast<uint4*>(A.segs + i * RUNS_MAX_SEGS);
-            const uint4* sp = reinterpret_cast<const uint4*>(myseg);
-            d[0] = sp[0];
-            // runs_expand reads the second vector only when the first has no terminator (C3: never).
-            // (A dense layout -- first vectors 16 B apart, second ones in an array after them -- measured
-            // more write traffic, 322 vs 235 MB per launch on C3, and was not kept)
-            if (seg_n >= 4) d[1] = sp[1];
+            for (int q = seg_n; q < RUNS_MAX_SEGS; q++) myseg[q] = 0xFFFF;   // terminator (and padding)
+            // one 8- or 16-byte store per completed run (dense by start record)
+            if (A.segn == 4) *reinterpret_cast<uint2*>(A.segs + i * 4) = *reinterpret_cast<const uint2*>(myseg);
+            else *reinterpret_cast<uint4*>(A.segs + i * 8) = *reinterpret_cast<const uint4*>(myseg);
           }
         },
         [&](int64_t i, int64_t r, int stage) {
@@ -292,12 +290,12 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
           if (stage == seg_last) return;
           seg_last = stage;
           const int64_t off = r - i;
-          if (seg_n >= RUNS_MAX_SEGS || off >= (int64_t(1) << 24)) { atomicOr(A.seg_over, 1ull); return; }
-          myseg[seg_n++] = uint32_t(stage) << 24 | uint32_t(off);
+          if (seg_n >= A.segn || off >= 4096 || stage >= 16) { atomicOr(A.seg_over, 1ull); return; }
+          myseg[seg_n++] = uint16_t(stage << 12 | int(off));
         });
   }
   __syncthreads();                                              // (every wave reaches it)
-  int64_t cnt = 0, len = 0, span = 0;
+  int64_t cnt = 0, len = 0, span = 0, cnt_own = 0, len_own = 0;
   for (int64_t k = lane; k < i1 - i0; k += 64) {
     const int32_t e = s_end[wv][k];
     end_of[i0 + k] = e;                                         // (-2: open, carried)
@@ -306,6 +304,7 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
       cnt++;
       len += d + 1;
       span = d > span ? d : span;
+      if (e < i1) { cnt_own++; len_own += d + 1; }
     }
   }
   if (i0 >= A.n) return;
@@ -313,6 +312,8 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
   for (int d = 32; d >= 1; d >>= 1) {
     cnt += __shfl_xor(cnt, d, 64);
     len += __shfl_xor(len, d, 64);
+    cnt_own += __shfl_xor(cnt_own, d, 64);
+    len_own += __shfl_xor(len_own, d, 64);
     const int64_t y = __shfl_xor(span, d, 64);
     span = y > span ? y : span;
   }
@@ -320,6 +321,10 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
     const int64_t W = int64_t(gridDim.x) * (RT / 64);
     stat[wave] = cnt;
     stat[W + wave] = len;
+    stat[2 * W + wave] = cnt_own;
+    stat[3 * W + wave] = len_own;
+    stat[4 * W + wave] = cnt - cnt_own;
+    stat[5 * W + wave] = len - len_own;
     // the longest span: a plain read first, so that the chunks agreeing with it add no contended atomic
     // (one atomicMax per 256 records on one word cost runs_compact ~400 us at 10 M records)
     if (span > 0 && (unsigned long long)span > __hip_atomic_load(A.max_span, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))

@@ -331,3 +331,23 @@ def test_pool_regrowth_is_bounded_and_given_back(monkeypatch):
     mine = [m for m in product_matches(s2, out) if m[1] not in failed]
     wantk = [m for m in oracle_matches(ir, heavy, [hval], [1], O.MODE_PROCESSOR) if m[1] not in failed]
     assert mine == wantk and len(mine) > 0
+
+
+def test_segment_count_stays_on_device():
+    """After a session's first batch the wave path leaves the batch's segment count on the device
+    (NfaArgs.nseg_dev, abi.cpp push_general): no host round trip before the kernel, buffers sized for n
+    segments, the pool estimated from the last batch.  Batches with many more keys than the last (the
+    pool estimate falls short: the batch re-runs on a larger pool), many fewer, and a single key --
+    each against the oracle."""
+    from kcep import synth
+    ir = synth.c4_pattern().to_ir(PL.I32)
+    s = N.Session(N.CompiledPattern(ir), 40000, force_path=N.PATH_GENERAL, lane_nfa=False)
+    total = 0
+    for nk, L in ((50, 12), (3000, 12), (7, 16), (1, 9), (2000, 8)):
+        key, val, _ = synth.c4_stream_np(nk, L=L)
+        want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
+        s.push(len(key), key, [val])
+        got = product_matches(s, s.collect())
+        assert got == want, (nk, L)
+        total += len(want)
+    assert total > 0

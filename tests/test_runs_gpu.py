@@ -70,18 +70,40 @@ def walk(n, seed, lo=-5, hi=6):
     return (100 + np.cumsum(np.random.default_rng(seed).integers(lo, hi, n))).astype(np.int32)
 
 
-@pytest.mark.parametrize("order", ["window", "radix"])
-@pytest.mark.parametrize("nkeys,per_key", [(1, 3000), (300, 40), (5000, 7)])
+@pytest.mark.parametrize("order", ["emit", "window", "radix"])
+@pytest.mark.parametrize("nkeys,per_key", [(1, 3000), (300, 40), (5000, 7), (20000, 12)])
 def test_c3_stock_random(nkeys, per_key, order, monkeypatch):
-    """Both orderings of the completed runs: the windowed rank (runs_order, every run spanning at
-    most 1024 records) and rocPRIM's radix sort (KCEP_RUNS_RADIX=1, also taken by wider batches)."""
+    """Every placement of the completed runs: by end chunk straight from runs_sim's results (runs_emit,
+    every run shorter than a chunk), the windowed rank (runs_order, every run spanning at most 1024
+    records; KCEP_RUNS_EMIT=0 or longer runs) and rocPRIM's radix sort (KCEP_RUNS_RADIX=1, also taken
+    by wider batches)."""
     monkeypatch.setenv("KCEP_RUNS_RADIX", "1" if order == "radix" else "0")
+    monkeypatch.setenv("KCEP_RUNS_EMIT", "0" if order != "emit" else "1")
     rng = np.random.default_rng(nkeys)
     key = np.repeat(np.arange(nkeys, dtype=np.int32), rng.poisson(per_key, nkeys) + 1)
     val = walk(len(key), nkeys)
     want, got, oerr, gerr = both(PL.c3_stock().to_ir(I32), key, [val], [1])
     assert oerr is None and gerr is None
     assert got == want and len(got) > 10
+
+
+def test_run_longer_than_the_segment_offsets():
+    """A run spanning more records than runs_sim's 12-bit segment offsets hold (4096) sets the segment
+    overflow flag: the batch's traversals are then written by walking every completed run again
+    (runs_write) -- wider than a chunk too, so the runs are ordered by the radix sort.  Against the
+    oracle, next to short runs of other keys."""
+    rng = np.random.default_rng(5)
+    long_key = np.concatenate([[0], np.ones(5000, np.int32), [2]]).astype(np.int32)
+    short = rng.integers(0, 3, 4000).astype(np.int32)
+    val = np.concatenate([short[:2000], long_key, short[2000:]])
+    key = np.concatenate([np.full(2000, 1), np.full(len(long_key), 2), np.full(2000, 3)]).astype(np.int32)
+    ir = (QueryBuilder().select("a").where(Event.value() == 0).then()
+          .select("b").oneOrMore().where(Event.value() == 1).then()
+          .select("c").where(Event.value() >= 2).build().to_ir(I32))
+    want, got, oerr, gerr = both(ir, key, [val], [1])
+    assert oerr is None and gerr is None
+    assert got == want
+    assert any(len(m[2]) == 5002 for m in got)
 
 
 def test_c3_generator():

@@ -36,9 +36,13 @@ def test_golden_stencil(name):
     assert len(got) == len(fx["expected"]["sequences"])
 
 
+@pytest.mark.parametrize("kernel", ["plain", "keyed"])
 @pytest.mark.parametrize("n,K", [(0, 1), (1, 1), (2, 1), (3, 1), (4095, 3), (4096, 7), (4097, 1), (8191, 50),
                                  (12289, 13), (100_003, 1000), (200_000, 100_000), (65_537, 1)])
-def test_c2_random(n, K):
+def test_c2_random(n, K, kernel, monkeypatch):
+    """Both stencil kernels on resident batches: the keyless plain one (the default for k <= 7) and the
+    keyed one carry sessions run (KCEP_STENCIL_KEYED=1 routes a resident batch through it)."""
+    monkeypatch.setenv("KCEP_STENCIL_KEYED", "1" if kernel == "keyed" else "0")
     key, val, order = synth.c2_stream_np(n, K)
     ir = c2_ir()
     want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR, offset=order, ts=order)

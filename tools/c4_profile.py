@@ -61,6 +61,22 @@ elif (ph >= 0).all():
         print(nm, "scans", int(tot[8]), "entries/scan", round(float(tot[9] / max(1, tot[8])), 2),
               "digit checks/scan", round(float(tot[10] / max(1, tot[8])), 2),
               "clocks/scan", round(float(tot[5] / max(1, tot[8])), 1))
+t0 = prof[:, 15].astype(np.float64)
+if (t0 > 0).all():                                     # the grid's busy timeline: keys in flight over time
+    t1 = t0 + prof[:, 3]
+    lo, hi = t0.min(), t1.max()
+    ev_t = np.concatenate([t0, t1]); ev_d = np.concatenate([np.ones(len(t0)), -np.ones(len(t1))])
+    o2 = np.argsort(ev_t, kind="stable")
+    inflight = np.cumsum(ev_d[o2]); tt = ev_t[o2]
+    full = inflight.max()
+    busy = np.sum(inflight[:-1] * np.diff(tt)) / (full * (hi - lo))
+    below = tt[np.nonzero(inflight < 0.9 * full)[0]]
+    tail_start = below[below > lo + 0.5 * (hi - lo)].min() if (below > lo + 0.5 * (hi - lo)).any() else hi
+    print(f"timeline: span {(hi - lo) / 100:.0f} us, keys in flight max {int(full)}, mean occupancy {busy:.3f}, "
+          f"tail (<90% in flight) {(hi - tail_start) / 100:.0f} us; last key starts {(t0.max() - lo) / 100:.0f} us")
+    late = np.argsort(-t1)[:5]
+    print("  last to finish (key, start us, us):",
+          [(int(prof[i, 0]), round((t0[i] - lo) / 100, 1), round(float(cyc[i]), 1)) for i in late])
 kinds = ["first workspace", "match output", "heap", "run queues", "private lists", "aggregates", "other"]
 kw = prof[:, 17:25].astype(np.float64)
 if (kw >= 0).all():
