@@ -242,8 +242,8 @@ def main():
             # these paths write their CSR in later launches (runs_write / nfa_compact), so the bytes
             # are divided by the whole step's device time (HIP events around cep_push_batch)
             roof_ms = sum(batch_ms) / len(batch_ms)
-            roof_kernel = "whole cep_push_batch (" + ("runs_sim + sort + runs_write" if sess.path == N.PATH_RUNS
-                                                       else "nfa_kernel + compaction") + ")"
+            roof_kernel = "whole cep_push_batch (" + ("runs_sim + runs_emit" if sess.path == N.PATH_RUNS
+                                                       else "nfa kernel + compaction") + ")"
         achieved = kernel_bytes / (roof_ms * 1e-3) / 1e9
         value = tot_events * args.steps / t_max
         build = N.lib().cep_version().decode().rsplit(" ", 1)[-1]
@@ -280,7 +280,9 @@ def main():
             line["config"]["exchange"] = exch
         if sess.path in (N.PATH_GENERAL, N.PATH_RUNS):
             line["batch_ms"] = roof_ms
-            line["first_kernel"] = {"name": {N.PATH_GENERAL: "kcep_nfa_kernel" if sess.jit else "nfa_kernel",
+            gname = ("kcep_nfa_wave" if sess.wave else "kcep_nfa_kernel") if sess.jit else (
+                "nfa_wave_kernel" if sess.wave else "nfa_kernel")
+            line["first_kernel"] = {"name": {N.PATH_GENERAL: gname,
                                              N.PATH_RUNS: "kcep_runs_sim" if sess.jit else "runs_sim"}[sess.path],
                                     "ms": avg_kernel_ms}
         if sess.path == N.PATH_GENERAL:

@@ -207,6 +207,9 @@ void cep_session_close(cep_session* s);
 int cep_session_path(const cep_session* s);
 /* 1 if the session runs kernels compiled for its pattern (see CEP_SESSION_INTERPRET), else 0 */
 int cep_session_jit(const cep_session* s);
+/* General path: 1 if the session runs one key per wave (kcep_nfa_wave, CEP_SESSION_WAVE_NFA), 0 if one
+   key per lane (kcep_nfa_kernel) or another path */
+int cep_session_wave(const cep_session* s);
 /* General path: the most live runs (NFA run queue length, NFAStates.java:33-37) any key held during the
    last batch -- C4's run-explosion high-water mark.  -1 if the last batch ran on another path. */
 int cep_live_run_hwm(const cep_session* s, int64_t* hwm);

@@ -1253,6 +1253,8 @@ int cep_session_jit(const cep_session* s) {
   return (s->path == CEP_PATH_RUNS && s->jit) || (s->path == CEP_PATH_GENERAL && s->jitg) ? 1 : 0;
 }
 
+int cep_session_wave(const cep_session* s) { return s && s->path == CEP_PATH_GENERAL && s->wave ? 1 : 0; }
+
 int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t cap, size_t* needed) {
   if (!p || !needed) return fail(CEP_E_ARG, "null argument");
   const bool runs = path == CEP_PATH_RUNS && p->prog.runs_ok, general = path == CEP_PATH_GENERAL && p->prog.general_ok;

@@ -36,6 +36,30 @@ __device__ __forceinline__ double bc_f(int64_t b) { return __builtin_bit_cast(do
 __device__ __forceinline__ int64_t bc_b(double d) { return __builtin_bit_cast(int64_t, d); }
 __device__ __forceinline__ int64_t bc_sx32(int64_t x) { return int64_t(int32_t(uint32_t(uint64_t(x)))); }
 
+// 32-bit integer division without a branch: the float-reciprocal estimate of 2^32 / d refined once,
+// then the quotient corrected twice (the same exact sequence the compiler expands `/` into, but as
+// straight-line selects: a predicate's divide is then one basic block, so two predicates of a stage
+// that divide the same operands share it, and no exec-mask juggling surrounds it).  d != 0.
+__device__ __forceinline__ uint32_t bc_udiv32(uint32_t n, uint32_t d) {
+  uint32_t inv = uint32_t(__builtin_amdgcn_rcpf(float(d)) * 4294966784.0f);   // 0x4f7ffffe
+  inv += __umulhi(inv, (0u - d) * inv);
+  uint32_t q = __umulhi(n, inv);
+  uint32_t r = n - q * d;
+  const bool c1 = r >= d;
+  q = c1 ? q + 1 : q;
+  r = c1 ? r - d : r;
+  return r >= d ? q + 1 : q;
+}
+// Java int division / remainder (wrapping: MIN_VALUE / -1 == MIN_VALUE, MIN_VALUE % -1 == 0); y != 0
+__device__ __forceinline__ int32_t bc_sdiv32(int32_t x, int32_t y) {
+  const uint32_t ax = x < 0 ? 0u - uint32_t(x) : uint32_t(x), ay = y < 0 ? 0u - uint32_t(y) : uint32_t(y);
+  const uint32_t q = bc_udiv32(ax, ay);
+  return int32_t((x ^ y) < 0 ? 0u - q : q);
+}
+__device__ __forceinline__ int32_t bc_srem32(int32_t x, int32_t y) {
+  return int32_t(uint32_t(x) - uint32_t(bc_sdiv32(x, y)) * uint32_t(y));
+}
+
 // One binary opcode with Java semantics: 0, or the exception it raises.  The
 // interpreters call it with a loaded opcode, the per-pattern kernels (jit.cpp)
 // with a constant one, so both evaluate every operator through this one body.
@@ -50,13 +74,13 @@ __device__ __forceinline__ int bc_bin(int op, int64_t x, int64_t y, int64_t& z) 
     // divisor is made safe instead of branching around the divide, so a predicate's failure checks
     // stay branch-free (jit.cpp)
     case BC_DIV_I32: {
-      const int32_t yy = (y == 0 || y == -1) ? 1 : int32_t(y);
-      z = y == 0 ? 0 : y == -1 ? bc_sx32(0 - x) : int64_t(int32_t(x) / yy);
+      const int32_t yy = y == 0 ? 1 : int32_t(y);
+      z = y == 0 ? 0 : int64_t(bc_sdiv32(int32_t(x), yy));
       return y == 0 ? CEP_E_ARITHMETIC : 0;
     }
     case BC_REM_I32: {
-      const int32_t yy = (y == 0 || y == -1) ? 1 : int32_t(y);
-      z = (y == 0 || y == -1) ? 0 : int64_t(int32_t(x) % yy);
+      const int32_t yy = y == 0 ? 1 : int32_t(y);
+      z = y == 0 ? 0 : int64_t(bc_srem32(int32_t(x), yy));
       return y == 0 ? CEP_E_ARITHMETIC : 0;
     }
     case BC_ADD_I64: z = int64_t(uint64_t(x) + uint64_t(y)); break;
@@ -66,12 +90,12 @@ __device__ __forceinline__ int bc_bin(int op, int64_t x, int64_t y, int64_t& z) 
     case BC_DIV_I64: {
       const int64_t yy = (y == 0 || y == -1) ? 1 : y;
       z = y == 0 ? 0 : y == -1 ? int64_t(0ull - uint64_t(x))
-          : (bc_sx32(x) == x && bc_sx32(yy) == yy) ? int64_t(int32_t(x) / int32_t(yy)) : x / yy;
+          : (bc_sx32(x) == x && bc_sx32(yy) == yy) ? int64_t(bc_sdiv32(int32_t(x), int32_t(yy))) : x / yy;
       return y == 0 ? CEP_E_ARITHMETIC : 0;
     }
     case BC_REM_I64: {
       const int64_t yy = (y == 0 || y == -1) ? 1 : y;
-      z = (y == 0 || y == -1) ? 0 : (bc_sx32(x) == x && bc_sx32(yy) == yy) ? int64_t(int32_t(x) % int32_t(yy)) : x % yy;
+      z = (y == 0 || y == -1) ? 0 : (bc_sx32(x) == x && bc_sx32(yy) == yy) ? int64_t(bc_srem32(int32_t(x), int32_t(yy))) : x % yy;
       return y == 0 ? CEP_E_ARITHMETIC : 0;
     }
     case BC_ADD_F64: z = bc_b(bc_f(x) + bc_f(y)); break;

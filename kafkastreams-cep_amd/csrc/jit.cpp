@@ -322,11 +322,16 @@ bool gen_program(const Program& P, std::string& o, std::string& why, bool branch
   o += "  }\n  env.fail(CEP_E_BAD_IR);\n  return false;\n}\n";
   o += R"(struct JitTab {
   __device__ __forceinline__ const DevProgram& prog() const { return kcep_prog; }
+  // every lane evaluates (a pure function of its env, which the caller keeps loadable for idle lanes;
+  // their results are dropped): with no branch around a predicate, the first computation of a
+  // subexpression dominates its repeats in the stage's later predicates and folds, and the compiler
+  // folds them (C3: the running average's divide, three per record on the oneOrMore stage -> one)
   template <class Env>
   __device__ __forceinline__ bool eval(int pc, Env& env, bool active, int64_t& v) const {
-    v = 0;
-    if (!active) return true;
-    return jit_eval(pc, env, v);
+    int64_t r = 0;
+    const bool ok = jit_eval(pc, env, r);
+    v = active ? r : 0;
+    return ok || !active;
   }
 };
 }  // namespace kcep

@@ -92,18 +92,24 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
                                                         int64_t* __restrict__ pre, int64_t* __restrict__ tot_cnt,
                                                         int64_t* __restrict__ tot_len) {
   __shared__ int64_t s_c[16], s_l[16];
+  constexpr int REG = 16;                          // up to 16 K chunks: each thread's sums stay in registers
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t per = (nw + 1023) / 1024, w0 = int64_t(threadIdx.x) * per, w1 = w0 + per < nw ? w0 + per : nw;
   int64_t c = 0, l = 0;
-  for (int64_t w = w0; w < w1; w += 8) {           // 8 loads of each array in flight, then the sums
-    int64_t cc[8], ll[8];
+  int64_t cc[REG], ll[REG];
+  if (per <= REG) {                                // every load in flight at once
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      cc[q] = w + q < w1 ? chunk_stat<by_end>(stat, W, 0, w + q) : 0;
-      ll[q] = w + q < w1 ? chunk_stat<by_end>(stat, W, 1, w + q) : 0;
+    for (int q = 0; q < REG; q++) {
+      cc[q] = w0 + q < w1 ? chunk_stat<by_end>(stat, W, 0, w0 + q) : 0;
+      ll[q] = w0 + q < w1 ? chunk_stat<by_end>(stat, W, 1, w0 + q) : 0;
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) { c += cc[q]; l += ll[q]; }
+    for (int q = 0; q < REG; q++) { c += cc[q]; l += ll[q]; }
+  } else {
+    for (int64_t w = w0; w < w1; w++) {
+      c += chunk_stat<by_end>(stat, W, 0, w);
+      l += chunk_stat<by_end>(stat, W, 1, w);
+    }
   }
   int64_t ic = c, il = l;
 #pragma unroll
@@ -115,11 +121,22 @@ __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restric
   __syncthreads();
   int64_t oc = ic - c, ol = il - l;
   for (int q = 0; q < wv; q++) { oc += s_c[q]; ol += s_l[q]; }
-  for (int64_t w = w0; w < w1; w++) {
-    pre[w] = oc;
-    pre[W + w] = ol;
-    oc += chunk_stat<by_end>(stat, W, 0, w);
-    ol += chunk_stat<by_end>(stat, W, 1, w);
+  if (per <= REG) {
+#pragma unroll
+    for (int q = 0; q < REG; q++)
+      if (w0 + q < w1) {
+        pre[w0 + q] = oc;
+        pre[W + w0 + q] = ol;
+        oc += cc[q];
+        ol += ll[q];
+      }
+  } else {
+    for (int64_t w = w0; w < w1; w++) {
+      pre[w] = oc;
+      pre[W + w] = ol;
+      oc += chunk_stat<by_end>(stat, W, 0, w);
+      ol += chunk_stat<by_end>(stat, W, 1, w);
+    }
   }
   if (threadIdx.x == 1023) {
     int64_t tc = 0, tl = 0;
@@ -269,12 +286,19 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
                                                  int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
                                                  int64_t* __restrict__ ent_off, int32_t* __restrict__ ent_name,
                                                  int64_t* __restrict__ ent_record) {
-  __shared__ int32_t s_cnt[RUNS_CHUNK + 1], s_fill[RUNS_CHUNK];
-  __shared__ int32_t s_run[RUNS_EMIT_MAX];         // window offset of the start | end slot << 11
-  __shared__ int32_t s_at[RUNS_EMIT_MAX + 1];      // the runs' entry offsets in the chunk
+  // dynamic LDS sized by the window (runs_emit_lds): at most chunk + span runs end in the chunk
+  extern __shared__ __attribute__((aligned(16))) unsigned char emit_lds[];
+  const int WN = chunk + span + 1;
+  uint2* const s_seg = reinterpret_cast<uint2*>(emit_lds);   // the runs' packed segments (segn == 4)
+  int32_t* const s_run = reinterpret_cast<int32_t*>(s_seg + WN);   // window offset of the start | end slot << 11
+  int32_t* const s_at = s_run + WN;                // the runs' entry offsets in the chunk (WN + 1) ...
+  int32_t* const s_fill = s_at;                    // ... and, before them, the end slots' fill cursors
+  int32_t* const s_cnt = s_at + WN + 1;            // end slot counts, then their prefix (chunk + 1)
   __shared__ int32_t s_w[4];
+  __shared__ int32_t s_name[16];
   const int tid = threadIdx.x;
   const int64_t c = blockIdx.x, c0 = c * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+  if (tid < 16) s_name[tid] = tid < P->nstages ? P->st[tid].name : 0;
   const int E = int(c1 - c0);
   const int64_t lo = c0 - span > 0 ? c0 - span : 0;
   const int L = int(c1 - lo);                      // <= chunk + span < RUNS_EMIT_MAX
@@ -284,15 +308,12 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
 #pragma unroll
   for (int q = 0; q < RUNS_EMIT_MAX / 256; q++) {
     const int x = tid + 256 * q;
-    my[q] = -1;
-    if (x < L) {
-      const int64_t e = end_of[lo + x];
-      if (e >= c0 && e < c1) {
-        my[q] = int32_t(e - c0);
-        atomicAdd(&s_cnt[my[q]], 1);
-      }
-    }
+    const int64_t e = x < L ? int64_t(end_of[lo + x]) : -1;
+    my[q] = e >= c0 && e < c1 ? int32_t(e - c0) : -1;
   }
+#pragma unroll
+  for (int q = 0; q < RUNS_EMIT_MAX / 256; q++)
+    if (my[q] >= 0) atomicAdd(&s_cnt[my[q]], 1);
   __syncthreads();
   // exclusive scan of the end slots' counts (up to 4 per thread)
   int v[4], acc = 0;
@@ -313,9 +334,8 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   int run = inc - acc;
   for (int w = 0; w < (tid >> 6); w++) run += s_w[w];
   const int M = s_w[0] + s_w[1] + s_w[2] + s_w[3];  // the chunk's runs
-  __syncthreads();                                 // (s_cnt read above before it is overwritten)
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
+  for (int q = 0; q < 4; q++) {                    // (each thread rewrites only the counts it read)
     const int x = 4 * tid + q;
     if (x < E) s_cnt[x] = run;
     run += v[q];
@@ -342,7 +362,7 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   int lens = 0;
   for (int i = R * tid; i < R * tid + R && i < M; i++) {
     const int32_t r = s_run[i];
-    lens += int(c0 + (r >> 11) - (lo + (r & 2047))) + 1;
+    lens += int(c0 - lo) + (r >> 11) - (r & 2047) + 1;
   }
   inc = lens;
 #pragma unroll
@@ -350,8 +370,7 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
     const int y = __shfl_up(inc, d, 64);
     if ((tid & 63) >= d) inc += y;
   }
-  __syncthreads();                                 // (s_w of the first scan read)
-  if ((tid & 63) == 63) s_w[tid >> 6] = inc;
+  if ((tid & 63) == 63) s_w[tid >> 6] = inc;     // (s_w's first use was read before the last barrier)
   __syncthreads();
   run = inc - lens;
   for (int w = 0; w < (tid >> 6); w++) run += s_w[w];
@@ -359,17 +378,24 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   for (int i = R * tid; i < R * tid + R && i < M; i++) {
     s_at[i] = run;
     const int32_t r = s_run[i];
-    run += int(c0 + (r >> 11) - (lo + (r & 2047))) + 1;
+    run += int(c0 - lo) + (r >> 11) - (r & 2047) + 1;
   }
   if (tid == 0) s_at[M] = NE;
   __syncthreads();
+  // match headers, and every run's segments into LDS (all loads of the pass in flight together)
   const int64_t mb = pre[c], eb = pre[W + c];
   for (int i = tid; i < M; i += 256) {
-    const int64_t e = c0 + (s_run[i] >> 11);
+    const int32_t r = s_run[i];
+    const int64_t e = c0 + (r >> 11);
+    if (segn == 4) s_seg[i] = *reinterpret_cast<const uint2*>(segs + (lo + (r & 2047)) * 4);
     match_record[mb + i] = pos ? pos[e] : base + e;
     match_key[mb + i] = key[e];
     ent_off[mb + i] = eb + s_at[i];
   }
+  __syncthreads();
+  // the entries, thread-strided (coalesced stores): each finds its run by a binary search over the
+  // runs' entry offsets and its stage in the run's segments, both in LDS.  (A per-run layout loop --
+  // one thread walking each of its runs' entries -- diverged on the long runs: 714 vs 282 us.)
   for (int x = tid; x < NE; x += 256) {
     int a = 0, b = M - 1;                          // the last run whose range starts at or before x
     while (a < b) {
@@ -377,10 +403,13 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
       if (s_at[mid] <= x) a = mid; else b = mid - 1;
     }
     const int32_t r = s_run[a];
-    const int64_t j = lo + (r & 2047), e = c0 + (r >> 11);
-    const int64_t o = (e - j) - (x - s_at[a]);     // offset of the entry's record from the start
-    ent_name[eb + x] = P->st[seg_stage(seg_load(segs, segn, j), segn, o)].name;
-    ent_record[eb + x] = pos ? pos[j + o] : base + j + o;
+    const int jo = r & 2047;                       // the start, from lo
+    const int o = int(c0 - lo) + (r >> 11) - jo - (x - s_at[a]);   // the entry's record, from the start
+    const uint4 sg = segn == 4 ? make_uint4(s_seg[a].x, s_seg[a].y, 0xFFFFFFFFu, 0xFFFFFFFFu)
+                               : seg_load(segs, segn, lo + jo);
+    const int64_t rec = lo + jo + o;
+    ent_name[eb + x] = s_name[seg_stage(sg, segn, o)];
+    ent_record[eb + x] = pos ? pos[rec] : base + rec;
   }
 }
 
@@ -623,7 +652,8 @@ hipError_t runs_emit_launch(const RunsArgs& R, const int32_t* end_of, const int6
   const int64_t nw = (R.n + R.chunk - 1) / R.chunk, W = int64_t(runs_blocks(R.n, R.chunk)) * (RT / 64);
   if (R.n <= 0) return hipSuccess;
   if (span < 0 || span >= R.chunk || R.chunk > RUNS_CHUNK || !R.segs) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(runs_emit, dim3(unsigned(nw)), dim3(256), 0, st, R.P, R.key, R.pos, R.base, R.segs, R.segn, end_of,
+  const size_t lds = size_t(R.chunk + span + 1) * 16 + size_t(R.chunk + 1) * 4 + 4;
+  hipLaunchKernelGGL(runs_emit, dim3(unsigned(nw)), dim3(256), lds, st, R.P, R.key, R.pos, R.base, R.segs, R.segn, end_of,
                      R.n, R.chunk, span, pre, W, match_record, match_key, ent_off, ent_name, ent_record);
   return hipGetLastError();
 }

@@ -150,6 +150,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
       if (next >= i1) break;
       continue;
     }
+    const int64_t gs = alive ? r : i0;                          // a loadable record for idle lanes (JitTab)
     KCEP_UNROLL
     for (int s = nst - 1; s >= 1; s--) {
       const bool here = alive && ps == s;
@@ -160,7 +161,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
       KCEP_UNROLL
       for (int e = 0; e < st.nedges; e++) {
         if (st.pred[e] < 0) { matched |= 1u << e; continue; }
-        RunEnv env{A, r, rs, 0, false, 0, 0, cv};
+        RunEnv env{A, gs, rs, 0, false, 0, 0, cv};
         int64_t v;
         const bool act = here && ok;
         if (!T.eval(st.pred[e], env, act, v)) {
@@ -187,7 +188,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
 #pragma unroll
         for (int q = 0; q < RUNS_MAX_STATES; q++)
           if (q == sidx) { ct = rs.tag[q]; cvv = rs.val[q]; }
-        RunEnv env{A, r, rs, 0, true, ct, cvv, cv};
+        RunEnv env{A, gs, rs, 0, true, ct, cvv, cv};
         int64_t v;
         const bool act = consume && ok;
         if (!T.eval(st.fold_code[f], env, act, v)) {

@@ -72,7 +72,7 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_session_close", "cep_session_path", "cep_push_batch", "cep_device_match_count", "cep_collect",
            "cep_checksum", "cep_last_kernel_ms", "cep_last_batch_ms", "cep_last_error", "cep_version",
            "cep_state_export", "cep_state_import", "cep_state_clear", "cep_key_state", "cep_stream_position",
-           "cep_session_jit", "cep_pattern_kernel_source", "cep_pattern_build_kernels", "cep_live_run_hwm",
+           "cep_session_jit", "cep_session_wave", "cep_pattern_kernel_source", "cep_pattern_build_kernels", "cep_live_run_hwm",
            "cep_batch_errors", "cep_session_set_timing",
            "cep_key_profile", "cep_key_hash", "cep_key_shard", "cep_shard_plan", "cep_partition", "cep_gather",
            "cep_match_count_to", "cep_state_evict", "cep_state_import_keys", "cep_state_positions",
@@ -124,6 +124,7 @@ def lib():
     L.cep_stream_position.argtypes = [P]
     L.cep_stream_position.restype = C.c_int64
     L.cep_session_jit.argtypes = [P]
+    L.cep_session_wave.argtypes = [P]
     L.cep_live_run_hwm.argtypes = [P, C.POINTER(C.c_int64)]
     L.cep_session_set_timing.argtypes = [P, C.c_int32]
     L.cep_batch_errors.argtypes = [P, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
@@ -247,6 +248,7 @@ class Session:
         check(lib().cep_session_open(pattern.h, C.byref(o), C.byref(self.h)))
         self.path = lib().cep_session_path(self.h)
         self.jit = bool(lib().cep_session_jit(self.h))
+        self.wave = bool(lib().cep_session_wave(self.h))
         self._keep = None
 
     def close(self):

@@ -193,3 +193,48 @@ def test_device_resident_checksum_c3():
     nm, cs = s.checksum()
     b = O.BatchArrays(key.cpu().numpy(), [val.cpu().numpy()], [1], ts=ts.cpu().numpy())
     assert (nm, cs) == O.baseline(O.OraclePattern(ir), b, O.MODE_PROCESSOR, 16)
+
+
+@pytest.mark.parametrize("op", ["div", "rem", "div_long"])
+def test_integer_division_is_exact(op):
+    """The predicates' integer divide (interp.h bc_udiv32: float-reciprocal estimate, two corrections,
+    no branch) against Java semantics over the whole int range: quotients and remainders of random
+    operands of every magnitude, divisors +-1, MIN_VALUE / -1 (wraps), MIN_VALUE % -1 == 0, and a
+    zero divisor (ArithmeticException at its record).  A record matches iff the device's result equals
+    the expected column; the expected column is off by one on a third of the records."""
+    rng = np.random.default_rng(11)
+    n = 60000
+    mag = rng.integers(0, 32, n)
+    a = (rng.integers(-(2 ** 31), 2 ** 31, n) >> rng.integers(0, 31, n)).astype(np.int64)
+    b = (rng.integers(-(2 ** 31), 2 ** 31, n) >> mag).astype(np.int64)
+    b[b == 0] = 7
+    edge = [(-(2 ** 31), -1), (-(2 ** 31), 1), (2 ** 31 - 1, -1), (-(2 ** 31), -(2 ** 31)), (2 ** 31 - 1, 2 ** 31 - 1),
+            (-(2 ** 31), 2 ** 31 - 1), (5, -(2 ** 31)), (-7, 2), (7, -2), (-7, -2), (0, -5), (4294967, 65536)]
+    for i, (x, y) in enumerate(edge):
+        a[i], b[i] = x, y
+    if op == "div_long":                                           # beyond 32 bits: the 64-bit divide
+        a[20:60] = rng.integers(-(2 ** 62), 2 ** 62, 40)
+        b[40:60] = rng.integers(2 ** 33, 2 ** 40, 20) * rng.choice([-1, 1], 20)
+    q = (np.abs(a) // np.abs(b)) * np.sign(a) * np.sign(b)       # truncating, exact in int64
+    r = a - q * b                                                  # (MIN_VALUE % -1 == 0)
+    if op != "div_long":
+        q = np.where((a == -(2 ** 31)) & (b == -1), -(2 ** 31), q)   # Integer.MIN_VALUE / -1 wraps
+    want = q if op != "rem" else r
+    c = (want + rng.integers(-1, 2, n) * (rng.random(n) < 0.34)).astype(np.int64)
+    if op != "div_long":
+        c = np.clip(c, -(2 ** 31), 2 ** 31 - 1)
+    b[n - 5] = 0                                                   # the task fails there
+    key = np.zeros(n, np.int32)
+    if op == "div_long":
+        sch = Schema([("a", "i64"), ("b", "i64"), ("c", "i64")])
+        pred = Event.field("a") / Event.field("b") == Event.field("c")
+        cols, types = [a, b, c], [2, 2, 2]
+    else:
+        sch = Schema([("a", "i32"), ("b", "i32"), ("c", "i32")])
+        ex = Event.field("a") / Event.field("b") if op == "div" else Event.field("a") % Event.field("b")
+        pred = ex == Event.field("c")
+        cols, types = [a.astype(np.int32), b.astype(np.int32), c.astype(np.int32)], [1, 1, 1]
+    ir = QueryBuilder().select("s").where(pred).build().to_ir(sch)
+    want_m, got, oerr, gerr = both(ir, key, cols, types)
+    assert oerr is not None and gerr == oerr and oerr[1] == n - 5
+    assert got == want_m and len(got) > n // 2

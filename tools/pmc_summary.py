@@ -2,6 +2,9 @@
 
 usage: python tools/pmc_summary.py TAG_DIR KERNEL EVENTS OUT_PREFIX CONFIG
 
+KERNEL: one kernel, or a comma-separated list whose bytes are summed (a whole step: the runs /
+general paths write their CSR in later launches, so their traffic is the step's)
+
 Reads gpurun_out/prof/TAG/{trace_kernel_stats,pmc_fetch_counter_collection,
 pmc_write_counter_collection}.csv and writes
   profiles/OUT_PREFIX_kernel_stats.csv   (copy of the rocprofv3 --stats summary)
@@ -43,7 +46,9 @@ def main():
                 "write_bytes": write.get(k)} for k in sorted(set(fetch) | set(write))}
     with open(os.path.join(prof, f"{prefix}_pmc.json"), "w") as f:
         json.dump({"tag": tag, "per_launch": rows}, f, indent=1)
-    k = rows[kernel]
+    names = kernel.split(",")
+    k = {"fetch_bytes_corrected": sum(rows[x]["fetch_bytes_corrected"] or 0 for x in names if x in rows),
+         "write_bytes": sum(rows[x]["write_bytes"] or 0 for x in names if x in rows)}
     # the library build the counters were taken on: the bench line of the kernel-trace pass
     build = None
     try:
@@ -60,6 +65,10 @@ def main():
            "commit": commit,
            "fetch_bytes_per_launch": k["fetch_bytes_corrected"], "write_bytes_per_launch": k["write_bytes"],
            "hbm_bytes_per_launch": k["fetch_bytes_corrected"] + k["write_bytes"]}
+    if len(names) > 1:
+        out["kernel"] = "whole cep_push_batch (every kernel of the step, one launch each)"
+        out["per_kernel_MB"] = {x: round(((rows[x]["fetch_bytes_corrected"] or 0) + (rows[x]["write_bytes"] or 0)) / 1e6, 1)
+                                for x in names if x in rows}
     with open(os.path.join(prof, "pmc_traffic.json" if cfg == "c2" else f"pmc_traffic_{cfg}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
