@@ -435,8 +435,9 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
   // spills).  r05, C4 with 16-byte frames: 4 waves (128 VGPRs) ran the kernel in 4.67 vs 4.92 ms but
   // spilled ~50 VGPRs, whose scratch lines reach HBM: 5.5 GB per launch against 0.28 GB
   // (profiles/r05_c4_occupancy.txt); r02: 2: 13.3, 3: 10.8, 4: 11.8 ms.  The wave kernel's LDS arena
-  // (nfa_wave.h WAVE_ARENA) stays at 1024 words: 512 5.82-5.85, 1280 4.95-4.97, 1536 4.95-4.96, 1792
-  // 5.25-5.26, 2048 5.21-5.24 vs 1024 4.97-4.98 ms kernel (r05, gpurun_out/ab/arena*)
+  // (nfa_wave.h WAVE_ARENA) is 1664 words: C4 kernel 512 5.82-5.85, 1024 4.97-4.98, 1280 4.95-4.97,
+  // 1536 4.94-4.96, 1664 4.94, 1792 5.25-5.26, 2048 5.21-5.24 ms (past ~1700 words a CU holds fewer
+  // waves); HBM bytes per launch 1024: 275 MB, 1536: 234, 1664: 232 (profiles/r05_c4_arena.txt)
   const int waves = 2, wave_occ = 3;
   const std::string agg = wave_stateful(P.dev) || P.has_seq ? "true" : "false";
   o += "#include \"nfa_dev.h\"\n#include \"nfa_wave.h\"\nextern \"C\" __global__ __launch_bounds__(64) "

@@ -38,7 +38,7 @@ constexpr int WAVE = 64;
 // ms per step): arena 2048 + lists in the pool 8.43; 1024 + 16 7.78; 1024 + 12 8.02; 1024 + 20 8.23;
 // 1280 + 16 8.22; 768 + 16 9.75; 512 + 32 10.9; 4 waves per SIMD 11.2
 #ifndef WAVE_ARENA
-#define WAVE_ARENA 1024                    // LDS words per key workspace (jit.cpp: the sizes measured)
+#define WAVE_ARENA 1664                    // LDS words per key workspace (jit.cpp: the sizes measured)
 #endif
 #ifndef WAVE_PRIV
 #define WAVE_PRIV 16                       // LDS words per lane for its private run list + operation log
