@@ -45,12 +45,14 @@ int64_t nfa_wave_grid(int64_t nseg, bool agg, const JitModule* j);
 hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* idx, int64_t* seg_start, int64_t* nseg,
                         int64_t* tmp, hipStream_t st);
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
+hipError_t set_words_launch(int64_t* w, int n, int at, int64_t v, hipStream_t st);
+hipError_t gather_words_launch(const int64_t* a, int na, const int64_t* b, int nb, int64_t* h, hipStream_t st);
 hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
                                int64_t* out1, int64_t* total0, int64_t* total1, int64_t* tmp, hipStream_t st);
-hipError_t nfa_compact_launch(int64_t nseg, int64_t nm, int64_t ne, const int32_t* key, const int64_t* seg_start,
-                              const int64_t* res_out, const int64_t* res_ent, const int64_t* moff, const int64_t* eoff,
-                              int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
-                              int64_t* ent_record, hipStream_t st);
+hipError_t nfa_compact_launch(int64_t nseg, const int64_t* nseg_dev, int64_t nm, int64_t ne, const int64_t* tot_dev,
+                              const int32_t* key, const int64_t* seg_start, const int64_t* res_out, const int64_t* res_ent,
+                              const int64_t* moff, const int64_t* eoff, int64_t* match_record, int32_t* match_key,
+                              int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st);
 hipError_t carry_commit_launch(int64_t nseg, const int32_t* key, const int64_t* seg_start, const int64_t* res_carry,
                                const int32_t* res_err, int64_t* ctab, hipStream_t st);
 hipError_t carry_keycheck_launch(int64_t max_seg, const int64_t* nseg, const int32_t* key, const int64_t* seg_start,
@@ -224,7 +226,8 @@ struct cep_session {
   DBuf rtab, rpool, rpool2, rtop, e_key, e_topic, e_part, e_seg, e_off, e_ts, e_pos, rc_a, rc_b, rc_c, rc_d, gc_len, gc_off;
   DBuf e_cols[16];
   int64_t rpool_cap = 0, rpool_used = 0;   // tail records (5 + ncols int64 words each)
-  int64_t* h_res = nullptr;                // runs path: the batch's counts, written by the device into pinned memory
+  int64_t* h_res = nullptr;                // runs / general paths: the batch's counts, written by the device into
+                                           // pinned memory (16 words)
   bool collected = false;                  // the CSR above is the last batch's: a second collect re-uses it
   cep_matches last{};
   std::vector<uint8_t> evict_buf;          // cep_state_evict's blobs
@@ -667,7 +670,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   }
   // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow (one
   // small kernel writes them into pinned host memory: no copy commands, which cost ~25 us of gaps)
-  if (!s->h_res) HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&s->h_res), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  if (!s->h_res) HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&s->h_res), 128, hipHostMallocMapped | hipHostMallocCoherent));
   int64_t* h_res_dev = nullptr;
   HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_res_dev), s->h_res, 0));
   HIPCHECK(runs_results_launch(ctl, scal0 + 3, rcarry ? s->rtop.as<int64_t>() : nullptr, h_res_dev, st));
@@ -892,7 +895,14 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   bool grew = false;                               // the pool was regrown for this batch: given back after it
   bool pool_at_limit = false;                      // the pool cannot grow further: overflowing keys are handed back
   int64_t tots[2] = {0, 0};                        // matches, entries of the batch
+  // the CSR's arrays as the earlier batches left them: a first attempt that fits them is compacted
+  // before the host reads its totals (one synchronisation per batch instead of two)
+  const int64_t cap_m = int64_t(std::min({s->o_record.cap / 8, s->o_key.cap / 4, s->o_entoff.cap / 8}));
+  const int64_t cap_e = int64_t(std::min(s->o_name.cap / 4, s->o_entrec.cap / 8));
+  bool spec = false;                               // the first attempt's compaction is enqueued
+  int attempts = 0;
   for (int attempt = 0;; attempt++) {
+    attempts = attempt + 1;
     if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
     if (s->carry && s->cpool_used + nseg * 64 > s->cpool_words) {
       if ((rc = carry_gc(s, 2 * (s->cpool_used + nseg * 64), st))) return rc;
@@ -904,8 +914,8 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     A.cpool_cap = s->carry ? s->cpool_words : 0;
     A.last_attempt = attempt >= kMaxRetry || pool_at_limit ? 1 : 0;   // then an overflowing key is handed back per key
     A.max_key_words = s->opts.max_key_words;
-    unsigned long long init[6] = {0, (unsigned long long)s->cpool_used, 0, 0, 0, 0};   // [5]: next segment
-    HIPCHECK(hipMemcpyAsync(ctl, init, sizeof init, hipMemcpyHostToDevice, st));
+    // ctl: pool top, carry-pool top, flags (2 words), err_any, next segment (a kernel, not a copy command)
+    HIPCHECK(set_words_launch(reinterpret_cast<int64_t*>(ctl), 6, 1, s->cpool_used, st));
     if (!timed) HIPCHECK(hipEventRecord(s->ev0, st));
     A.seg_next = reinterpret_cast<int32_t*>(ctl + 5);
     if (s->wave) HIPCHECK(nfa_wave_launch(A, wgrid, st, s->jitg.get()));
@@ -917,11 +927,26 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     HIPCHECK(exclusive_scan_pair(s->r_matches.as<int64_t>(), s->r_words.as<int64_t>(), nseg, A.nseg_dev,
                                  s->moff.as<int64_t>(), s->eoff.as<int64_t>(), scal + 3, scal + 4,
                                  s->scan_tmp.as<int64_t>(), st));
+    if (attempt == 0 && cap_m > 0 && cap_e > 0) {
+      HIPCHECK(nfa_compact_launch(nseg, A.nseg_dev, cap_m, cap_e, scal + 3, A.key, A.seg_start, s->r_out.as<int64_t>(),
+                                  s->r_ent.as<int64_t>(), s->moff.as<int64_t>(), s->eoff.as<int64_t>(),
+                                  s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
+                                  s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
+      spec = true;
+    }
+    // the flags and counts into pinned host memory by one small kernel (two copy commands cost ~25 us
+    // of gaps), then the batch's one synchronisation
+    if (!s->h_res) HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&s->h_res), 128, hipHostMallocMapped | hipHostMallocCoherent));
+    int64_t* h_res_dev = nullptr;
+    HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_res_dev), s->h_res, 0));
+    HIPCHECK(gather_words_launch(reinterpret_cast<const int64_t*>(ctl), 5, scal, 5, h_res_dev, st));
+    HIPCHECK(hipStreamSynchronize(st));
     unsigned long long res[5];
     int64_t sc[5];                                 // [0] segments, [3] matches, [4] entries
-    HIPCHECK(hipMemcpyAsync(res, ctl, sizeof res, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipMemcpyAsync(sc, scal, sizeof sc, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    for (int q = 0; q < 5; q++) {
+      res[q] = (unsigned long long)s->h_res[q];
+      sc[q] = s->h_res[5 + q];
+    }
     tots[0] = sc[3];
     tots[1] = sc[4];
     if (dev_count && attempt == 0) {               // the exact count from here on
@@ -959,14 +984,19 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->nseg_hint = nseg;
   s->g_matches = tots[0];
   s->g_entries = tots[1];
-  const size_t nm = size_t(std::max<int64_t>(tots[0], 1)), ne = size_t(std::max<int64_t>(tots[1], 1));
-  if (s->o_record.ensure(nm * 8) || s->o_key.ensure(nm * 4) || s->o_entoff.ensure(nm * 8) ||
-      s->o_name.ensure(ne * 4) || s->o_entrec.ensure(ne * 8))
-    return fail(CEP_E_HIP, "allocation failed");
-  HIPCHECK(nfa_compact_launch(nseg, tots[0], tots[1], A.key, A.seg_start, s->r_out.as<int64_t>(),
-                              s->r_ent.as<int64_t>(), s->moff.as<int64_t>(), s->eoff.as<int64_t>(),
-                              s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
-                              s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
+  if (!(spec && attempts == 1 && tots[0] <= cap_m && tots[1] <= cap_e)) {
+    // (arrays grown with a quarter of headroom, so that the next batches compact speculatively)
+    const size_t nm = size_t(std::max<int64_t>(tots[0], 1)), ne = size_t(std::max<int64_t>(tots[1], 1));
+    const size_t hm = nm + nm / 4 + 256, he = ne + ne / 4 + 256;
+    if ((s->o_record.cap < nm * 8 && s->o_record.ensure(hm * 8)) || (s->o_key.cap < nm * 4 && s->o_key.ensure(hm * 4)) ||
+        (s->o_entoff.cap < nm * 8 && s->o_entoff.ensure(hm * 8)) || (s->o_name.cap < ne * 4 && s->o_name.ensure(he * 4)) ||
+        (s->o_entrec.cap < ne * 8 && s->o_entrec.ensure(he * 8)))
+      return fail(CEP_E_HIP, "allocation failed");
+    HIPCHECK(nfa_compact_launch(nseg, nullptr, tots[0], tots[1], nullptr, A.key, A.seg_start, s->r_out.as<int64_t>(),
+                                s->r_ent.as<int64_t>(), s->moff.as<int64_t>(), s->eoff.as<int64_t>(),
+                                s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
+                                s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), st));
+  }
   if (s->carry) {                                  // NFAStore.put of every key of the batch
     HIPCHECK(carry_commit_launch(nseg, A.key, A.seg_start, s->r_carry.as<int64_t>(), s->r_err.as<int32_t>(),
                                  s->ctab.as<int64_t>(), st));

@@ -277,6 +277,29 @@ hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* t
   return hipGetLastError();
 }
 
+// w[0..n) = 0 except w[at] = v
+__global__ void set_words(int64_t* __restrict__ w, int n, int at, int64_t v) {
+  const int t = threadIdx.x;
+  if (t < n) w[t] = t == at ? v : 0;
+}
+hipError_t set_words_launch(int64_t* w, int n, int at, int64_t v, hipStream_t st) {
+  if (n > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(set_words, dim3(1), dim3(64), 0, st, w, n, at, v);
+  return hipGetLastError();
+}
+// a[0..na) then b[0..nb) into h (pinned host memory mapped for the device): the host's view of a batch
+__global__ void gather_words(const int64_t* __restrict__ a, int na, const int64_t* __restrict__ b, int nb,
+                             int64_t* __restrict__ h) {
+  const int t = threadIdx.x;
+  if (t < na) h[t] = a[t];
+  else if (t < na + nb) h[t] = b[t - na];
+}
+hipError_t gather_words_launch(const int64_t* a, int na, const int64_t* b, int nb, int64_t* h, hipStream_t st) {
+  if (na + nb > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_words, dim3(1), dim3(64), 0, st, a, na, b, nb, h);
+  return hipGetLastError();
+}
+
 // Two exclusive scans of one length n (or *n_dev <= n, read on the device) in one set of launches;
 // tmp: 2 x ceil(n / 1024) words.  Up to 16 M elements.
 hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
@@ -306,25 +329,29 @@ __device__ __forceinline__ int64_t seg_of(const int64_t* __restrict__ off, int64
   }
   return lo;
 }
-__global__ void nfa_compact_matches(int64_t nseg, int64_t nm, const int32_t* __restrict__ key,
+// tot_dev / nseg_dev (optional): the batch's match / entry totals and segment count on the device, the
+// grid sized by an upper bound (a compaction enqueued before the host has read them)
+__global__ void nfa_compact_matches(int64_t nseg, const int64_t* __restrict__ nseg_dev, int64_t nm,
+                                    const int64_t* __restrict__ tot_dev, const int32_t* __restrict__ key,
                                     const int64_t* __restrict__ seg_start, const int64_t* __restrict__ res_out,
                                     const int64_t* __restrict__ moff, const int64_t* __restrict__ eoff,
                                     int64_t* __restrict__ match_record, int32_t* __restrict__ match_key,
                                     int64_t* __restrict__ ent_off) {
   const int64_t m = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (m >= nm) return;
-  const int64_t s = seg_of(moff, nseg, m);
+  if (m >= (tot_dev && tot_dev[0] < nm ? tot_dev[0] : nm)) return;
+  const int64_t s = seg_of(moff, nseg_dev ? *nseg_dev : nseg, m);
   const int4 h = reinterpret_cast<const int4*>(uintptr_t(res_out[s]))[m - moff[s]];
   match_record[m] = int64_t(uint64_t(uint32_t(h.x)) | (uint64_t(uint32_t(h.y)) << 32));
   match_key[m] = key[seg_start[s]];
   ent_off[m] = eoff[s] + h.w;
 }
-__global__ void nfa_compact_entries(int64_t nseg, int64_t ne, const int64_t* __restrict__ res_ent,
+__global__ void nfa_compact_entries(int64_t nseg, const int64_t* __restrict__ nseg_dev, int64_t ne,
+                                    const int64_t* __restrict__ tot_dev, const int64_t* __restrict__ res_ent,
                                     const int64_t* __restrict__ eoff, int32_t* __restrict__ ent_name,
                                     int64_t* __restrict__ ent_record) {
   const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (e >= ne) return;
-  const int64_t s = seg_of(eoff, nseg, e);
+  if (e >= (tot_dev && tot_dev[1] < ne ? tot_dev[1] : ne)) return;
+  const int64_t s = seg_of(eoff, nseg_dev ? *nseg_dev : nseg, e);
   const int32_t* x = reinterpret_cast<const int32_t*>(uintptr_t(res_ent[s])) + 3 * (e - eoff[s]);
   ent_name[e] = x[0];
   ent_record[e] = cw64(x + 1);
@@ -381,17 +408,17 @@ hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* i
   return hipGetLastError();
 }
 
-hipError_t nfa_compact_launch(int64_t nseg, int64_t nm, int64_t ne, const int32_t* key, const int64_t* seg_start,
-                              const int64_t* res_out, const int64_t* res_ent, const int64_t* moff, const int64_t* eoff,
-                              int64_t* match_record, int32_t* match_key, int64_t* ent_off, int32_t* ent_name,
-                              int64_t* ent_record, hipStream_t st) {
+hipError_t nfa_compact_launch(int64_t nseg, const int64_t* nseg_dev, int64_t nm, int64_t ne, const int64_t* tot_dev,
+                              const int32_t* key, const int64_t* seg_start, const int64_t* res_out, const int64_t* res_ent,
+                              const int64_t* moff, const int64_t* eoff, int64_t* match_record, int32_t* match_key,
+                              int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st) {
   if (nseg <= 0) return hipSuccess;
   if (nm > 0)
-    hipLaunchKernelGGL(nfa_compact_matches, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, nseg, nm, key, seg_start,
-                       res_out, moff, eoff, match_record, match_key, ent_off);
+    hipLaunchKernelGGL(nfa_compact_matches, dim3(unsigned((nm + 255) / 256)), dim3(256), 0, st, nseg, nseg_dev, nm, tot_dev,
+                       key, seg_start, res_out, moff, eoff, match_record, match_key, ent_off);
   if (ne > 0)
-    hipLaunchKernelGGL(nfa_compact_entries, dim3(unsigned((ne + 255) / 256)), dim3(256), 0, st, nseg, ne, res_ent, eoff,
-                       ent_name, ent_record);
+    hipLaunchKernelGGL(nfa_compact_entries, dim3(unsigned((ne + 255) / 256)), dim3(256), 0, st, nseg, nseg_dev, ne, tot_dev,
+                       res_ent, eoff, ent_name, ent_record);
   return hipGetLastError();
 }
 

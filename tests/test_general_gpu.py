@@ -320,9 +320,11 @@ def test_pool_regrowth_is_bounded_and_given_back(monkeypatch):
     free1 = torch.cuda.mem_get_info()[0]
     assert len(got) == 2 * len(want)
     assert free1 >= free0 - (64 << 20)                     # the regrown pool was given back
-    # a second session on the same device, with a pool budget the batch cannot fit in
+    # a second session on the same device, with a pool budget the batch cannot fit in (longer keys:
+    # their workspace outgrows the first pool estimate, which is linear in the records)
+    heavy, hval, _ = synth.c4_stream_np(800, L=19)
     s2 = N.Session(N.CompiledPattern(ir), len(heavy), force_path=N.PATH_GENERAL, lane_nfa=False,
-                   max_pool_bytes=12 << 20)              # ~4.1 M words needed, 3 M allowed
+                   max_pool_bytes=12 << 20)              # 3 M words allowed
     s2.push(len(heavy), heavy, [hval])
     out = s2.collect(raise_on_error=False)
     rec, code = s2.batch_errors()
@@ -338,7 +340,9 @@ def test_segment_count_stays_on_device():
     (NfaArgs.nseg_dev, abi.cpp push_general): no host round trip before the kernel, buffers sized for n
     segments, the pool estimated from the last batch.  Batches with many more keys than the last (the
     pool estimate falls short: the batch re-runs on a larger pool), many fewer, and a single key --
-    each against the oracle."""
+    each against the oracle.  The CSR compaction is enqueued before the host reads the batch's totals
+    when the arrays the earlier batches left fit them (the small batches here) and after it otherwise
+    (the larger ones)."""
     from kcep import synth
     ir = synth.c4_pattern().to_ir(PL.I32)
     s = N.Session(N.CompiledPattern(ir), 40000, force_path=N.PATH_GENERAL, lane_nfa=False)
