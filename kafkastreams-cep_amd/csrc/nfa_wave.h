@@ -105,7 +105,8 @@ struct WaveShared {
   int64_t nmatch;
   KeyAlloc ka;                     // the key's allocator: its words, the wave's scratch region
   int32_t err, overflow, cap_hit;
-  int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy
+  int32_t* grown;                  // a shared array lane 0 re-allocated (pool), for the copy ...
+  int64_t grown_n;                 // ... and its capacity
   int32_t *arena, arena_used, arena_cap;   // the key's LDS arena, its bump pointer (re-allocations go there first), size
   // scratch of one phase of a record at a time (the phases never overlap): ~2.3 KB less LDS per wave
   union {
@@ -150,13 +151,24 @@ __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int3
       w.grown = w.arena + w.arena_used;
       w.arena_used += int32_t((nc + 3) & ~int64_t(3));
     } else {
-      w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc, kind, !lds_ok);
+      // past the arena: 4x while the wave's scratch region has room for it (words never touched cost
+      // no traffic, and every regrow copies the array: fewer copies, fewer bytes), else 2x
+      const int64_t n4 = int64_t(cap) * 4 > need ? int64_t(cap) * 4 : need;
+      w.grown = nullptr;
+      if (lds_ok && w.ka.scr && int64_t(w.ka.scr_top) + ((n4 + 3) & ~int64_t(3)) <= w.ka.scr_cap &&
+          n4 <= (int64_t(1) << 30)) {
+        w.grown = pool_alloc(l, n4, kind);
+        if (w.grown) nc = n4;
+      }
+      if (!w.grown) w.grown = nc > (int64_t(1) << 30) ? nullptr : pool_alloc(l, nc, kind, !lds_ok);
     }
+    w.grown_n = nc;
     if (!w.grown) { w.overflow = 1; w.cap_hit |= l.cap_hit; }
   }
   wave_sync();
   int32_t* na = w.grown;
   if (!na) return nullptr;
+  nc = w.grown_n;
   for (int64_t i = g.gl; i < used; i += GL) na[i] = a[i];
   cap = int32_t(nc);
   wave_sync();
