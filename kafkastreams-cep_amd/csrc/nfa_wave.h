@@ -151,9 +151,10 @@ __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int3
       w.grown = w.arena + w.arena_used;
       w.arena_used += int32_t((nc + 3) & ~int64_t(3));
     } else {
-      // past the arena: 4x while the wave's scratch region has room for it (words never touched cost
-      // no traffic, and every regrow copies the array: fewer copies, fewer bytes), else 2x
-      const int64_t n4 = int64_t(cap) * 4 > need ? int64_t(cap) * 4 : need;
+      // past the arena: 16x while the wave's scratch region has room for it (words never touched cost
+      // no traffic, and every regrow copies the array: fewer copies, fewer bytes), else 2x.  C4 HBM
+      // bytes per launch at 2x / 4x / 8x / 16x: 232 / 210 / 176 / 171 MB (profiles/r05_c4_arena.txt)
+      const int64_t n4 = int64_t(cap) * 16 > need ? int64_t(cap) * 16 : need;
       w.grown = nullptr;
       if (lds_ok && w.ka.scr && int64_t(w.ka.scr_top) + ((n4 + 3) & ~int64_t(3)) <= w.ka.scr_cap &&
           n4 <= (int64_t(1) << 30)) {
