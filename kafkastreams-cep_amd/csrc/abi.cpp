@@ -66,14 +66,15 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
                               int64_t* ent_record, hipStream_t st);
 hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64_t n, int32_t chunk, int64_t* pre,
                                unsigned long long* out, int64_t* tot_cnt, int64_t* tot_len, int64_t* scan_tmp,
-                               hipStream_t st);
+                               hipStream_t st, int64_t n_grid);
 int64_t runs_sim_waves(int64_t n, int32_t chunk);
 bool runs_emit_scan(const int64_t* stat, int64_t n, int32_t chunk, int64_t* pre, int64_t* tot_cnt, int64_t* tot_len,
-                    hipStream_t st);
+                    hipStream_t st, const int64_t* n_dev);
 hipError_t runs_emit_launch(const RunsArgs& R, const int32_t* end_of, const int64_t* pre, int span, int64_t* match_record,
-                            int32_t* match_key, int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st);
+                            int32_t* match_key, int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st,
+                            int64_t n_grid);
 hipError_t runs_results_launch(const unsigned long long* ctl, const int64_t* nm, const int64_t* top, int64_t* h,
-                               hipStream_t st);
+                               hipStream_t st, const int64_t* x);
 hipError_t runs_order_launch(const unsigned long long* in, int64_t nm, int w, unsigned long long* out, int64_t* len,
                              hipStream_t st);
 hipError_t runs_sort(const unsigned long long* in, unsigned long long* out, int64_t nm, int bits, void* tmp,
@@ -567,6 +568,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     return CEP_OK;
   }
   const bool rcarry = tail_session(s);
+  bool nosync = false;                            // carry: the extended batch's size read after the launches
   RcExt X{};
   const int32_t* bkey = in.key;                   // the batch's own key column (segments index it)
   if (rcarry) {
@@ -584,16 +586,31 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     RcIn B{};
     B.key = in.key; B.topic = in.topic; B.partition = in.partition; B.offset = in.offset; B.ts = in.ts;
     for (int c = 0; c < 16; c++) B.cols[c] = in.cols[c];
+    const int32_t mk = int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX));
     HIPCHECK(runs_carry_build(B, nb, s->base, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
                               s->rtab.as<int64_t>(), s->rpool.as<int64_t>(), s->rc_a.as<int64_t>(), s->rc_b.as<int64_t>(),
-                              scal + 5, s->scan_tmp.as<int64_t>(), X, st, true));
-    int64_t h[6];
-    HIPCHECK(hipMemcpyAsync(h, scal, sizeof h, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    if (h[1] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
-    if (h[1] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
-    n = nb + h[5];
-    if (n >= (int64_t(1) << 31)) return fail(CEP_E_RUN_CAPACITY, "carried tails make the batch exceed 2^31 records");
+                              scal + 5, s->scan_tmp.as<int64_t>(), X, st, true, mk));
+    // The extended batch's size (the batch plus its keys' carried tails) stays on the device: the launches
+    // are sized by a bound -- the batch plus every tail record the pool holds -- and read the count
+    // (scal[7]); the key checks are read with the batch's results, and a failing batch leaves the tail
+    // pool and table untouched (rc_tail_*).  Unless a forced ordering path or a batch too large for the
+    // one-workgroup chunk scan needs the count first.
+    const int64_t nmax = nb + s->rpool_used;
+    nosync = !getenv_flag("KCEP_RUNS_RADIX") && !getenv_flag_off("KCEP_RUNS_EMIT") && nmax < (int64_t(1) << 31) &&
+             (nmax + runs_chunk(nmax) - 1) / runs_chunk(nmax) <= (int64_t(1) << 16);
+    if (nosync) {
+      n = nmax;
+      if ((rc = tail_reserve(s, n, st))) return rc;  // room for the new tails (at most every record)
+      HIPCHECK(runs_carry_count(scal + 7, nb, scal + 5, st));
+    } else {
+      int64_t h[6];
+      HIPCHECK(hipMemcpyAsync(h, scal, sizeof h, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (h[1] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+      if (h[1] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+      n = nb + h[5];
+      if (n >= (int64_t(1) << 31)) return fail(CEP_E_RUN_CAPACITY, "carried tails make the batch exceed 2^31 records");
+    }
     const size_t e4 = size_t(n) * 4, e8 = size_t(n) * 8;
     if (s->e_key.ensure(e4) || s->e_topic.ensure(e4) || s->e_part.ensure(e4) || s->e_seg.ensure(e4) ||
         s->e_off.ensure(e8) || s->e_ts.ensure(e8) || s->e_pos.ensure(e8))
@@ -609,11 +626,12 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     }
     HIPCHECK(runs_carry_build(B, nb, s->base, s->flag.as<int64_t>(), s->idx.as<int64_t>(), s->seg.as<int64_t>(), scal,
                               s->rtab.as<int64_t>(), s->rpool.as<int64_t>(), s->rc_a.as<int64_t>(), s->rc_b.as<int64_t>(),
-                              scal + 5, s->scan_tmp.as<int64_t>(), X, st, false));
+                              scal + 5, s->scan_tmp.as<int64_t>(), X, st, false, mk));
     in.key = X.key; in.topic = X.topic; in.partition = X.partition; in.offset = X.offset; in.ts = X.ts;
     for (int c = 0; c < X.ncols; c++) in.cols[c] = X.cols[c];
-    if ((rc = tail_reserve(s, n, st))) return rc;    // room for the new tails (at most every record)
+    if (!nosync && (rc = tail_reserve(s, n, st))) return rc;   // room for the new tails (at most every record)
   }
+  const int64_t n_grid = n;                       // what the runs_sim grid is sized by
   if (s->rk.ensure(size_t(n) * 8) || s->rk_sorted.ensure(size_t(n) * 8) || s->r_errcode.ensure(size_t(n) * 4) ||
       s->ctl.ensure(64) || s->scal.ensure(64) || s->scan_tmp.ensure(size_t(n / 1024 + 4) * 8) ||
       s->flag.ensure(size_t(6 * runs_sim_waves(n, runs_chunk(n)) + 8) * 8) ||
@@ -626,6 +644,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   A.key = in.key; A.topic = in.topic; A.partition = in.partition; A.offset = in.offset; A.ts = in.ts;
   for (int c = 0; c < 16; c++) A.cols[c] = in.cols[c];
   A.n = n;
+  A.n_dev = nosync ? s->scal.as<int64_t>() + 7 : nullptr;
   A.base = 0;
   A.pos = rcarry ? X.pos : nullptr;               // carry: stream positions; runs ending in a tail are old
   A.emit_from = s->base;
@@ -655,26 +674,34 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   // (KCEP_RUNS_EMIT=0 / KCEP_RUNS_RADIX=1: the tests' hooks onto those paths for batches runs_emit takes)
   const bool emit_scan = !getenv_flag("KCEP_RUNS_RADIX") && !getenv_flag_off("KCEP_RUNS_EMIT") &&
                          runs_emit_scan(s->flag.as<int64_t>(), n, A.chunk, s->idx.as<int64_t>(), scal0 + 3,
-                                        reinterpret_cast<int64_t*>(ctl + 2), st);
-  if (!emit_scan)
+                                        reinterpret_cast<int64_t*>(ctl + 2), st, A.n_dev);
+  if (!emit_scan)                                  // (never with nosync: it was decided on the same bound)
     HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), n, A.chunk, s->idx.as<int64_t>(),
                                  s->rk.as<unsigned long long>(), scal0 + 3, reinterpret_cast<int64_t*>(ctl + 2),
-                                 s->scan_tmp.as<int64_t>(), st));
+                                 s->scan_tmp.as<int64_t>(), st, n_grid));
   if (rcarry) {                                    // the keys' new tails: from their oldest still-open start
     if (s->rc_c.ensure(size_t(nb + 2) * 8) || s->rc_d.ensure(size_t(nb + 2) * 8))
       return fail(CEP_E_HIP, "allocation failed");
     HIPCHECK(runs_carry_tails(X, n, nb, scal0, s->seg.as<int64_t>(), bkey, s->rc_b.as<int64_t>(), s->r_endof.as<int32_t>(),
                               reinterpret_cast<unsigned long long*>(s->rc_a.as<int64_t>()), s->rc_c.as<int64_t>(),
                               s->rc_d.as<int64_t>(), scal0 + 6, s->scan_tmp.as<int64_t>(), s->rtop.as<int64_t>(),
-                              s->rpool.as<int64_t>(), s->rtab.as<int64_t>(), st));
+                              s->rpool.as<int64_t>(), s->rtab.as<int64_t>(), st, A.n_dev, scal0 + 1));
   }
   // the batch's one host synchronisation: completed runs, entries, first exception, segment overflow (one
   // small kernel writes them into pinned host memory: no copy commands, which cost ~25 us of gaps)
   if (!s->h_res) HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&s->h_res), 128, hipHostMallocMapped | hipHostMallocCoherent));
   int64_t* h_res_dev = nullptr;
   HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_res_dev), s->h_res, 0));
-  HIPCHECK(runs_results_launch(ctl, scal0 + 3, rcarry ? s->rtop.as<int64_t>() : nullptr, h_res_dev, st));
+  HIPCHECK(runs_results_launch(ctl, scal0 + 3, rcarry ? s->rtop.as<int64_t>() : nullptr, h_res_dev, st,
+                               rcarry ? scal0 : nullptr));
   HIPCHECK(hipStreamSynchronize(st));
+  if (nosync) {                                    // the key checks and the extended batch's size, now
+    if (s->h_res[7] & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    if (s->h_res[7] & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+    n = nb + s->h_res[8];
+    A.n = n;
+    A.n_dev = nullptr;
+  }
   unsigned long long res[6];
   for (int q = 0; q < 6; q++) res[q] = (unsigned long long)s->h_res[q];
   const int64_t top = s->h_res[6];
@@ -734,7 +761,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     // every run shorter than a chunk: the CSR in one pass over the end chunks (runs_emit)
     HIPCHECK(runs_emit_launch(A, s->r_endof.as<int32_t>(), s->idx.as<int64_t>(), int(res[4]), s->o_record.as<int64_t>(),
                               s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(), s->o_name.as<int32_t>(),
-                              s->o_entrec.as<int64_t>(), st));
+                              s->o_entrec.as<int64_t>(), st, n_grid));
     HIPCHECK(hipEventRecord(s->eb1, st));
     s->g_matches = nm;
     s->g_entries = ne;
@@ -743,7 +770,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
   if (emit_scan)                                   // (the start-ordered list the paths below read)
     HIPCHECK(runs_compact_launch(s->flag.as<int64_t>(), s->r_endof.as<int32_t>(), n, A.chunk, s->idx.as<int64_t>(),
                                  s->rk.as<unsigned long long>(), scal0 + 3, reinterpret_cast<int64_t*>(ctl + 2),
-                                 s->scan_tmp.as<int64_t>(), st));
+                                 s->scan_tmp.as<int64_t>(), st, n_grid));
   // (completing record, start) order: a windowed rank when every run spans <= 1024 records
   // (runs_order), else rocPRIM's radix sort over the completing record's bits
   // the entry offsets are scanned straight into the output's ent_off (runs_expand reads them there);

@@ -411,7 +411,7 @@ std::string jit_source_runs(const Program& P, std::string& why) {
   o += R"(#include "runs_dev.h"
 extern "C" __global__ __launch_bounds__(kcep::RT) void kcep_runs_sim(kcep::RunsArgs A, int64_t* __restrict__ flag,
                                                                      int32_t* __restrict__ end_of) {
-  kcep::runs_sim_body(kcep::JitTab{}, A, flag, end_of);
+  kcep::runs_sim_body(kcep::JitTab{}, kcep::runs_args_dev(A), flag, end_of);
 }
 extern "C" __global__ __launch_bounds__(kcep::RT) void kcep_runs_write(kcep::WriteArgs W) {
   kcep::runs_write_body(kcep::JitTab{}, W);

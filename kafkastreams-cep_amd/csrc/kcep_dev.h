@@ -173,7 +173,8 @@ struct RunsArgs {
   const int64_t* offset;
   const int64_t* ts;
   const void* cols[16];
-  int64_t n;
+  int64_t n;                      // records (the grid and the chunk statistics' layout follow it) ...
+  const int64_t* n_dev;           // ... or, when set, an upper bound, the count itself on the device
   int64_t base;
   unsigned long long* nmatch;     // match counter (append position)
   unsigned long long* match_key;  // appended (end << 31 | start), sorted afterwards

@@ -37,7 +37,7 @@ namespace kcep {
 namespace {
 
 __global__ __launch_bounds__(RT) void runs_sim(RunsArgs A, int64_t* __restrict__ flag, int32_t* __restrict__ end_of) {
-  runs_sim_body(InterpTab{A.P}, A, flag, end_of);
+  runs_sim_body(InterpTab{A.P}, runs_args_dev(A), flag, end_of);
 }
 
 __global__ __launch_bounds__(RT) void runs_write(WriteArgs W) { runs_write_body(InterpTab{W.R.P}, W); }
@@ -87,12 +87,15 @@ __device__ __forceinline__ int64_t chunk_stat(const int64_t* __restrict__ stat, 
   if (!by_end) return stat[q * W + w];
   return stat[(2 + q) * W + w] + (w > 0 ? stat[(4 + q) * W + w - 1] : 0);
 }
+// n_dev (optional): the records on the device (the chunks past them hold no statistics)
 template <bool by_end>
 __global__ __launch_bounds__(1024) void runs_chunk_scan(const int64_t* __restrict__ stat, int64_t nw, int64_t W,
                                                         int64_t* __restrict__ pre, int64_t* __restrict__ tot_cnt,
-                                                        int64_t* __restrict__ tot_len) {
+                                                        int64_t* __restrict__ tot_len, const int64_t* __restrict__ n_dev,
+                                                        int chunk) {
   __shared__ int64_t s_c[16], s_l[16];
   constexpr int REG = 16;                          // up to 16 K chunks: each thread's sums stay in registers
+  if (n_dev && (*n_dev + chunk - 1) / chunk < nw) nw = (*n_dev + chunk - 1) / chunk;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t per = (nw + 1023) / 1024, w0 = int64_t(threadIdx.x) * per, w1 = w0 + per < nw ? w0 + per : nw;
   int64_t c = 0, l = 0;
@@ -435,12 +438,14 @@ __device__ __forceinline__ void col_put(void* c, int type, int64_t i, int64_t v)
 }
 
 // per batch segment: its key's carried tail length (0 beyond the segment count)
+// (a key id outside [0, max_keys) gets none: carry_keycheck flags the batch, which then fails)
 __global__ void rc_tail_len(const int64_t* __restrict__ nseg, const int64_t* __restrict__ seg_start,
                             const int32_t* __restrict__ key, const int64_t* __restrict__ rtab, int64_t nmax,
-                            int64_t* __restrict__ tlen) {
+                            int64_t* __restrict__ tlen, int32_t max_keys) {
   const int64_t sg = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (sg >= nmax) return;
-  tlen[sg] = sg < *nseg ? rtab[2 * int64_t(key[seg_start[sg]]) + 1] : 0;
+  const int32_t k = sg < *nseg ? key[seg_start[sg]] : -1;
+  tlen[sg] = k >= 0 && k < max_keys ? rtab[2 * int64_t(k) + 1] : 0;
 }
 
 // the batch's records into the extended batch, after their key's tail
@@ -489,9 +494,9 @@ __global__ void rc_build_tail(RcExt X, int64_t nmax, const int64_t* __restrict__
 
 // per segment: the first start whose run is still open (runs_sim's end_of == -2)
 __global__ void rc_open_min(const int32_t* __restrict__ end_of, const int32_t* __restrict__ seg, int64_t n,
-                            unsigned long long* __restrict__ tstart) {
+                            unsigned long long* __restrict__ tstart, const int64_t* __restrict__ n_dev) {
   const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (j < n && end_of[j] == -2) atomicMin(&tstart[seg[j]], (unsigned long long)j);
+  if (j < n && (!n_dev || j < *n_dev) && end_of[j] == -2) atomicMin(&tstart[seg[j]], (unsigned long long)j);
 }
 
 __global__ void rc_new_len(int64_t nmax, const int64_t* __restrict__ nseg, const int64_t* __restrict__ seg_start,
@@ -510,12 +515,13 @@ __global__ void rc_new_len(int64_t nmax, const int64_t* __restrict__ nseg, const
 
 // the new tails appended to the pool (at *top + noff): the key table per segment, then the records one
 // thread each (a thread walking its segment's whole tail took 97 us per 1 M-record C3 batch)
+// bad: the batch's key-check flags -- a failing batch leaves the tail pool and table as they were
 __global__ void rc_tail_table(int64_t nmax, const int64_t* __restrict__ nseg, const int64_t* __restrict__ seg_start,
                               const int32_t* __restrict__ key, const int64_t* __restrict__ newlen,
                               const int64_t* __restrict__ noff, const int64_t* __restrict__ top,
-                              int64_t* __restrict__ rtab) {
+                              int64_t* __restrict__ rtab, const int64_t* __restrict__ bad) {
   const int64_t sg = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (sg >= nmax || sg >= *nseg) return;
+  if (sg >= nmax || sg >= *nseg || *bad) return;
   const int64_t k = key[seg_start[sg]];
   const int64_t L = newlen[sg];
   if (L) rtab[2 * k] = *top + noff[sg];
@@ -524,9 +530,9 @@ __global__ void rc_tail_table(int64_t nmax, const int64_t* __restrict__ nseg, co
 __global__ void rc_tail_write(RcExt X, int64_t nrec, const int64_t* __restrict__ nseg,
                               const unsigned long long* __restrict__ tstart, const int64_t* __restrict__ noff,
                               const int64_t* __restrict__ new_total, const int64_t* __restrict__ top,
-                              int64_t* __restrict__ rpool) {
+                              int64_t* __restrict__ rpool, const int64_t* __restrict__ bad) {
   const int64_t x = int64_t(blockIdx.x) * 256 + threadIdx.x;   // the x-th new tail record of the batch
-  if (x >= nrec || x >= *new_total) return;
+  if (x >= nrec || x >= *new_total || *bad) return;
   int64_t lo = 0, hi = *nseg - 1;                  // its segment: the last whose tail starts at or before x
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) >> 1;
@@ -543,7 +549,11 @@ __global__ void rc_tail_write(RcExt X, int64_t nrec, const int64_t* __restrict__
   for (int c = 0; c < X.ncols; c++) d[5 + c] = col_bits(X.cols[c], X.coltype[c], e);
 }
 
-__global__ void rc_top_add(int64_t* __restrict__ top, const int64_t* __restrict__ add) { *top += *add; }
+__global__ void rc_top_add(int64_t* __restrict__ top, const int64_t* __restrict__ add, const int64_t* __restrict__ bad) {
+  if (!*bad) *top += *add;
+}
+// *out = a + *b (the extended batch's record count on the device)
+__global__ void rc_count(int64_t* __restrict__ out, int64_t a, const int64_t* __restrict__ b) { *out = a + *b; }
 
 // compaction of the tail pool: every key's tail copied to `dst` at the exclusive prefix of the lengths
 __global__ void rc_gc_len(const int64_t* __restrict__ rtab, int64_t nkeys, int64_t* __restrict__ len) {
@@ -585,14 +595,16 @@ hipError_t runs_sim_launch(const RunsArgs& A, int64_t* flag, int32_t* end_of, hi
 
 // stat: runs_sim's per-chunk counts / lengths (W = the sim launch's waves); pre: 2 W entries of scratch;
 // the completed runs into out in start order, their count into *tot_cnt, their total length *tot_len
+// n_grid: the record count runs_sim's grid was sized by (its statistics' layout), >= n
 hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64_t n, int32_t chunk, int64_t* pre,
                                unsigned long long* out, int64_t* tot_cnt, int64_t* tot_len, int64_t* scan_tmp,
-                               hipStream_t st) {
+                               hipStream_t st, int64_t n_grid) {
   if (n <= 0) return hipSuccess;
-  const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
+  const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n_grid, chunk)) * (RT / 64);
   if (chunk > RUNS_CHUNK || chunk < 64 || (chunk & (chunk - 1))) return hipErrorInvalidValue;
   if (nw <= (int64_t(1) << 16)) {
-    hipLaunchKernelGGL(runs_chunk_scan<false>, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
+    hipLaunchKernelGGL(runs_chunk_scan<false>, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len, nullptr,
+                       chunk);
   } else {
     hipError_t e = exclusive_scan(stat, nw, pre, tot_cnt, scan_tmp, st);
     if (e == hipSuccess) e = exclusive_scan(stat + W, nw, pre + W, tot_len, scan_tmp, st);
@@ -604,14 +616,17 @@ hipError_t runs_compact_launch(const int64_t* stat, const int32_t* end_of, int64
 
 // the host's view of a runs batch, into pinned host memory h: {completed runs, first exception, entries,
 // segment overflow, longest span, failing runs, tail pool top}
+// ... and, for a carry batch, h[7] its key-check flags and h[8] its carried tail records (x: scal)
 __global__ void runs_results(const unsigned long long* __restrict__ ctl, const int64_t* __restrict__ nm,
-                             const int64_t* __restrict__ top, int64_t* __restrict__ h) {
+                             const int64_t* __restrict__ top, int64_t* __restrict__ h, const int64_t* __restrict__ x) {
   const int t = threadIdx.x;
   if (t < 7) h[t] = t == 0 ? *nm : t == 6 ? (top ? *top : 0) : int64_t(ctl[t]);
+  else if (t == 7) h[t] = x ? x[1] : 0;
+  else if (t == 8) h[t] = x ? x[5] : 0;
 }
 hipError_t runs_results_launch(const unsigned long long* ctl, const int64_t* nm, const int64_t* top, int64_t* h,
-                               hipStream_t st) {
-  hipLaunchKernelGGL(runs_results, dim3(1), dim3(64), 0, st, ctl, nm, top, h);
+                               hipStream_t st, const int64_t* x) {
+  hipLaunchKernelGGL(runs_results, dim3(1), dim3(64), 0, st, ctl, nm, top, h, x);
   return hipGetLastError();
 }
 
@@ -647,16 +662,18 @@ hipError_t runs_expand_launch(const RunsArgs& R, const unsigned long long* sorte
 // with the batch's totals into *tot_cnt / *tot_len.  False when the chunks are too many for one
 // scanning workgroup (then the batch takes runs_compact + runs_order / the sort instead).
 bool runs_emit_scan(const int64_t* stat, int64_t n, int32_t chunk, int64_t* pre, int64_t* tot_cnt, int64_t* tot_len,
-                    hipStream_t st) {
+                    hipStream_t st, const int64_t* n_dev) {
   const int64_t nw = (n + chunk - 1) / chunk, W = int64_t(runs_blocks(n, chunk)) * (RT / 64);
   if (n <= 0 || nw > (int64_t(1) << 16) || chunk > RUNS_CHUNK) return false;
-  hipLaunchKernelGGL(runs_chunk_scan<true>, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len);
+  hipLaunchKernelGGL(runs_chunk_scan<true>, dim3(1), dim3(1024), 0, st, stat, nw, W, pre, tot_cnt, tot_len, n_dev, chunk);
   return true;
 }
 // the CSR from runs_sim's results (runs_emit_scan's pre); span: the longest completed span (< chunk)
+// n_grid: the record count runs_sim's grid was sized by (its statistics' layout), >= R.n
 hipError_t runs_emit_launch(const RunsArgs& R, const int32_t* end_of, const int64_t* pre, int span, int64_t* match_record,
-                            int32_t* match_key, int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st) {
-  const int64_t nw = (R.n + R.chunk - 1) / R.chunk, W = int64_t(runs_blocks(R.n, R.chunk)) * (RT / 64);
+                            int32_t* match_key, int64_t* ent_off, int32_t* ent_name, int64_t* ent_record, hipStream_t st,
+                            int64_t n_grid) {
+  const int64_t nw = (R.n + R.chunk - 1) / R.chunk, W = int64_t(runs_blocks(n_grid, R.chunk)) * (RT / 64);
   if (R.n <= 0) return hipSuccess;
   if (span < 0 || span >= R.chunk || R.chunk > RUNS_CHUNK || !R.segs) return hipErrorInvalidValue;
   const size_t lds = size_t(R.chunk + span + 1) * 16 + size_t(R.chunk + 1) * 4 + 4;
@@ -673,9 +690,10 @@ static unsigned blocks256(int64_t n) { return unsigned((std::max<int64_t>(n, 1) 
 hipError_t runs_carry_build(const RcIn& B, int64_t n, int64_t base, const int64_t* seg_flag, const int64_t* seg_idx,
                             const int64_t* seg_start, const int64_t* nseg, const int64_t* rtab, const int64_t* rpool,
                             int64_t* tlen, int64_t* toff, int64_t* total, int64_t* scan_tmp, const RcExt& X,
-                            hipStream_t st, bool lens_only) {
+                            hipStream_t st, bool lens_only, int32_t max_keys) {
   if (lens_only) {
-    hipLaunchKernelGGL(rc_tail_len, dim3(blocks256(n + 1)), dim3(256), 0, st, nseg, seg_start, B.key, rtab, n + 1, tlen);
+    hipLaunchKernelGGL(rc_tail_len, dim3(blocks256(n + 1)), dim3(256), 0, st, nseg, seg_start, B.key, rtab, n + 1, tlen,
+                       max_keys);
     return exclusive_scan(tlen, n + 1, toff, total, scan_tmp, st);
   }
   hipLaunchKernelGGL(rc_build_new, dim3(blocks256(n)), dim3(256), 0, st, X, n, seg_flag, seg_idx, toff, tlen, base, B);
@@ -688,16 +706,23 @@ hipError_t runs_carry_build(const RcIn& B, int64_t n, int64_t base, const int64_
 hipError_t runs_carry_tails(const RcExt& X, int64_t ext_n, int64_t n, const int64_t* nseg, const int64_t* seg_start,
                             const int32_t* key, const int64_t* toff, const int32_t* end_of, unsigned long long* tstart,
                             int64_t* newlen, int64_t* noff, int64_t* new_total, int64_t* scan_tmp, int64_t* top,
-                            int64_t* rpool, int64_t* rtab, hipStream_t st) {
+                            int64_t* rpool, int64_t* rtab, hipStream_t st, const int64_t* ext_n_dev, const int64_t* bad) {
   hipError_t e = hipMemsetAsync(tstart, 0x7F, size_t(n + 1) * 8, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(rc_open_min, dim3(blocks256(ext_n)), dim3(256), 0, st, end_of, X.seg, ext_n, tstart);
+  hipLaunchKernelGGL(rc_open_min, dim3(blocks256(ext_n)), dim3(256), 0, st, end_of, X.seg, ext_n, tstart, ext_n_dev);
   hipLaunchKernelGGL(rc_new_len, dim3(blocks256(n + 1)), dim3(256), 0, st, n + 1, nseg, seg_start, toff, tstart, newlen);
   if ((e = exclusive_scan(newlen, n + 1, noff, new_total, scan_tmp, st)) != hipSuccess) return e;
-  hipLaunchKernelGGL(rc_tail_table, dim3(blocks256(n)), dim3(256), 0, st, n, nseg, seg_start, key, newlen, noff, top, rtab);
+  hipLaunchKernelGGL(rc_tail_table, dim3(blocks256(n)), dim3(256), 0, st, n, nseg, seg_start, key, newlen, noff, top, rtab,
+                     bad);
   hipLaunchKernelGGL(rc_tail_write, dim3(blocks256(ext_n)), dim3(256), 0, st, X, ext_n, nseg, tstart, noff, new_total, top,
-                     rpool);
-  hipLaunchKernelGGL(rc_top_add, dim3(1), dim3(1), 0, st, top, new_total);
+                     rpool, bad);
+  hipLaunchKernelGGL(rc_top_add, dim3(1), dim3(1), 0, st, top, new_total, bad);
+  return hipGetLastError();
+}
+
+// *out = nb + *tails: the extended batch's records, for the launches sized by a bound
+hipError_t runs_carry_count(int64_t* out, int64_t nb, const int64_t* tails, hipStream_t st) {
+  hipLaunchKernelGGL(rc_count, dim3(1), dim3(1), 0, st, out, nb, tails);
   return hipGetLastError();
 }
 

@@ -90,6 +90,13 @@ __device__ __forceinline__ bool wave_any(bool x) { return __builtin_amdgcn_ballo
 // 1024 vs 2.59 at 128 on C3); a batch too small to give every SIMD three waves
 // that way takes smaller chunks (runs_chunk).
 
+// the args a runs_sim launch runs on: the record count from the device when the host passed a bound
+__device__ __forceinline__ RunsArgs runs_args_dev(const RunsArgs& A) {
+  RunsArgs a = A;
+  if (A.n_dev) a.n = *A.n_dev < A.n ? *A.n_dev : A.n;
+  return a;
+}
+
 struct RunResult {
   int64_t end;        // record where the run consumed its last stage, -1 none
   int64_t fail_at;    // record whose evaluation raised, -1 none

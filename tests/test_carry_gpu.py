@@ -406,6 +406,37 @@ def test_runs_carry_long_open_run_and_export_import():
     assert len(want) > 0 and got + got2 == want
 
 
+@pytest.mark.parametrize("bad", ["key_out_of_range", "key_in_two_segments"])
+def test_runs_carry_rejected_batch_leaves_tails(bad):
+    """A runs-path carry batch is launched before the host has read its key checks (the extended
+    batch's size stays on the device: one synchronisation per batch).  A batch with a key id outside
+    [0, max_keys) or a key in two segments still fails with CEP_E_ARG, its tail kernels leave the
+    carried tails and the key table as they were, and the stream continues exactly as the oracle's
+    without that batch (open runs carried across it)."""
+    ir = PL.c3_stock().to_ir(PL.I32)
+    key, val = c3_stream(3, 40, 12)
+    bounds, order = batches_of(key, list(range(20, len(key), 20)))
+    key, val = key[order], val[order]
+    want, _, oerr = oracle_run(ir, key, [val], [1], O.MODE_PROCESSOR)
+    s = N.Session(N.CompiledPattern(ir), len(key) + 8, carry=True, max_keys=64)
+    assert s.path == N.PATH_RUNS
+    got = []
+    for i, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+        if i == len(bounds) // 2:
+            if bad == "key_out_of_range":
+                bk, bv = np.array([1, 1, 1 << 20, 1 << 20], np.int32), np.array([5, 6, 7, 8], np.int32)
+            else:
+                bk, bv = np.array([1, 2, 1], np.int32), np.array([5, 6, 7], np.int32)
+            with pytest.raises(N.CepError) as e:
+                s.push(len(bk), bk, [bv], flags=N.BATCH_OFFSETS_MONOTONE)
+            assert e.value.code == 11
+        s.push(b - a, key[a:b], [val[a:b]], flags=N.BATCH_OFFSETS_MONOTONE)
+        out = s.collect()
+        got += [(int(out["match_record"][m]), int(out["match_key"][m])) for m in range(len(out["match_record"]))]
+    assert oerr is None and len(want) > 0
+    assert got == [(m[0], m[1]) for m in want]
+
+
 def test_runs_carry_rejects_unclean_batches():
     """Like the stencil carry: null records or unflagged offsets cannot be taken by the runs kernels
     (the host applies CEPProcessor's filters first)."""
