@@ -299,6 +299,7 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   int32_t* const s_cnt = s_at + WN + 1;            // end slot counts, then their prefix (chunk + 1)
   __shared__ int32_t s_w[4];
   __shared__ int32_t s_name[16];
+  __shared__ unsigned long long s_mask[4];         // per wave: the run starts of its entry window
   const int tid = threadIdx.x;
   const int64_t c = blockIdx.x, c0 = c * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
   if (tid < 16) s_name[tid] = tid < P->nstages ? P->st[tid].name : 0;
@@ -396,23 +397,47 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
     ent_off[mb + i] = eb + s_at[i];
   }
   __syncthreads();
-  // the entries, thread-strided (coalesced stores): each finds its run by a binary search over the
-  // runs' entry offsets and its stage in the run's segments, both in LDS.  (A per-run layout loop --
-  // one thread walking each of its runs' entries -- diverged on the long runs: 714 vs 282 us.)
-  for (int x = tid; x < NE; x += 256) {
-    int a = 0, b = M - 1;                          // the last run whose range starts at or before x
-    while (a < b) {
-      const int mid = (a + b + 1) >> 1;
-      if (s_at[mid] <= x) a = mid; else b = mid - 1;
+  // the entries: each wave a quarter of the chunk's range, 64 consecutive entries per step (coalesced
+  // stores).  A lane finds its run from the window's run starts: the runs after the window's first one
+  // set their start's bit in a per-wave LDS mask, and a lane's run is the first one plus the starts at or
+  // before it (a popcount) -- one binary search per wave instead of one per entry.  (A binary search per
+  // entry: 222 us on C3; a per-run layout loop, one thread walking each of its runs' entries, diverged on
+  // the long runs: 714 us.)
+  const int wv = tid >> 6, lane = tid & 63;
+  const int per = ((NE + 3) / 4 + 63) & ~63;
+  const int x0 = wv * per, x1 = x0 + per < NE ? x0 + per : NE;
+  if (x0 < x1) {
+    int q0 = 0, b = M - 1;                         // the run holding entry x0
+    while (q0 < b) {
+      const int mid = (q0 + b + 1) >> 1;
+      if (s_at[mid] <= x0) q0 = mid; else b = mid - 1;
     }
-    const int32_t r = s_run[a];
-    const int jo = r & 2047;                       // the start, from lo
-    const int o = int(c0 - lo) + (r >> 11) - jo - (x - s_at[a]);   // the entry's record, from the start
-    const uint4 sg = segn == 4 ? make_uint4(s_seg[a].x, s_seg[a].y, 0xFFFFFFFFu, 0xFFFFFFFFu)
-                               : seg_load(segs, segn, lo + jo);
-    const int64_t rec = lo + jo + o;
-    ent_name[eb + x] = s_name[seg_stage(sg, segn, o)];
-    ent_record[eb + x] = pos ? pos[rec] : base + rec;
+    for (int wb = x0; wb < x1; wb += 64) {
+      const int qi = q0 + 1 + lane;                // s_at[M] = NE: a start past every entry
+      const int d = qi <= M ? s_at[qi] - wb : 64;
+      if (lane == 0) s_mask[wv] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (d >= 0 && d < 64) atomicOr(&s_mask[wv], 1ull << d);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long msk = s_mask[wv];
+      const int x = wb + lane;
+      if (x < x1) {
+        const int a = q0 + __popcll(msk & (lane == 63 ? ~0ull : (2ull << lane) - 1));
+        const int32_t r = s_run[a];
+        const int jo = r & 2047;                   // the start, from lo
+        const int o = int(c0 - lo) + (r >> 11) - jo - (x - s_at[a]);   // the entry's record, from the start
+        const uint4 sg = segn == 4 ? make_uint4(s_seg[a].x, s_seg[a].y, 0xFFFFFFFFu, 0xFFFFFFFFu)
+                                   : seg_load(segs, segn, lo + jo);
+        const int64_t rec = lo + jo + o;
+        ent_name[eb + x] = s_name[seg_stage(sg, segn, o)];
+        ent_record[eb + x] = pos ? pos[rec] : base + rec;
+      }
+      q0 += __popcll(msk);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();             // (the mask is read before the next window resets it)
+    }
   }
 }
 
