@@ -156,8 +156,10 @@ __device__ __forceinline__ int32_t* wave_regrow(Lane& l, WaveShared<GL>& w, int3
       // bytes per launch at 2x / 4x / 8x / 16x: 232 / 210 / 176 / 171 MB (profiles/r05_c4_arena.txt)
       const int64_t n4 = int64_t(cap) * 16 > need ? int64_t(cap) * 16 : need;
       w.grown = nullptr;
+      // Not under a per-key cap (cep_opts.max_key_words counts reserved words: the headroom would hand
+      // keys back early -- C4's capped hand-off leg: 832 keys at 16x against 126 at 2x)
       if (lds_ok && w.ka.scr && int64_t(w.ka.scr_top) + ((n4 + 3) & ~int64_t(3)) <= w.ka.scr_cap &&
-          n4 <= (int64_t(1) << 30)) {
+          n4 <= (int64_t(1) << 30) && l.A->max_key_words <= 0) {
         w.grown = pool_alloc(l, n4, kind);
         if (w.grown) nc = n4;
       }
