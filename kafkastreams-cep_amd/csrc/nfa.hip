@@ -301,17 +301,18 @@ hipError_t gather_words_launch(const int64_t* a, int na, const int64_t* b, int n
 }
 
 // Two exclusive scans of one length n (or *n_dev <= n, read on the device) in one set of launches;
-// tmp: 2 x ceil(n / 1024) words.  Up to 16 M elements.
+// tmp: 2 x ceil(n / 1024) words.
 hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
                                int64_t* out1, int64_t* total0, int64_t* total1, int64_t* tmp, hipStream_t st) {
   const int64_t nb = (std::max<int64_t>(n, 1) + 1023) / 1024;
-  if (nb > int64_t(SCAN_REG) * 1024) {
-    hipError_t e = exclusive_scan(in0, n, out0, total0, tmp, st);
-    return e != hipSuccess ? e : exclusive_scan(in1, n, out1, total1, tmp, st);
-  }
   const ScanPair S{{in0, in1}, {out0, out1}, {total0, total1}, std::max<int64_t>(n, 0), n_dev, nb};
   hipLaunchKernelGGL(scan_blocks, dim3(unsigned(nb), 2), dim3(256), 0, st, S, tmp);
-  hipLaunchKernelGGL(scan_sums_pair, dim3(2), dim3(1024), 0, st, S, tmp);
+  if (nb <= int64_t(SCAN_REG) * 1024) {
+    hipLaunchKernelGGL(scan_sums_pair, dim3(2), dim3(1024), 0, st, S, tmp);
+  } else {                                         // (blocks past *n_dev summed to 0 in scan_blocks)
+    hipLaunchKernelGGL(scan_sums, dim3(1), dim3(256), 0, st, tmp, nb, total0);
+    hipLaunchKernelGGL(scan_sums, dim3(1), dim3(256), 0, st, tmp + nb, nb, total1);
+  }
   hipLaunchKernelGGL(scan_final, dim3(unsigned(nb), 2), dim3(256), 0, st, S, tmp);
   return hipGetLastError();
 }
