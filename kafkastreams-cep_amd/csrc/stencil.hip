@@ -23,6 +23,35 @@ struct SlotFormat {
   int k, plain, chain, carry, dense, kdense;
   int64_t nsuper;
   int sub;
+  // match m of super-tile t (c matches): its slot word and aux byte, then stage s of its row from them
+  __device__ __forceinline__ void load(const int32_t* slots, int64_t t, int64_t c, int64_t m, int32_t& v,
+                                       uint32_t& a) const {
+    a = 0;
+    if (dense) {
+      v = m < ST_DENSE ? slots[t * ST_DENSE + m] : slots[nsuper * ST_DENSE + t * int64_t(sub) * ST_TILE + m];
+      return;
+    }
+    if (kdense && c <= ST_DENSE_KEYED) {
+      const int64_t i = t * ST_DENSE_KEYED + m;
+      v = slots[i];
+      a = reinterpret_cast<const uint8_t*>(slots + nsuper * ST_DENSE_KEYED)[i];
+      return;
+    }
+    const int32_t* src = slots + (kdense ? nsuper * (ST_DENSE_KEYED + ST_DENSE_KEYED / 4) : 0) +
+                         t * int64_t(sub) * ST_TILE * k;
+    const uint8_t* aux = reinterpret_cast<const uint8_t*>(src + int64_t(sub) * ST_TILE);
+    v = src[m];
+    if (plain ? (carry && v < 0) : k > 1) a = aux[m];
+  }
+  __device__ __forceinline__ int32_t value(int32_t v, uint32_t a, int s) const {
+    if (dense) return v + s;
+    if (plain) {                                 // first record; carry boundary: -(1 + completing record)
+      if (!carry || v >= 0) return v + s;
+      const int need = int(a);
+      return s < need ? -(1 + (need - s)) : -(1 + v) - (k - 1) + s;
+    }
+    return stencil_row(v, a, s, k, chain, carry);
+  }
   // match m of super-tile t (c matches), stage s
   __device__ __forceinline__ int32_t entry(const int32_t* slots, int64_t t, int64_t c, int64_t m, int s) const {
     if (dense)                                   // the plain kernel without carry (kcep_internal.h ST_DENSE)
@@ -44,16 +73,22 @@ struct SlotFormat {
     return stencil_row(v, k > 1 ? aux[m] : 0u, s, k, chain, carry);
   }
 };
+// One thread per match: its slot word (and aux byte) loaded once, its k row entries stored (a wave's
+// stores of one stage k ints apart, the k stores together filling the wave's rows).  (Was one thread
+// per output word: a divide by k and the slot loads repeated k times per match.)
 __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
                                                       const int64_t* __restrict__ pre, int32_t* __restrict__ out,
                                                       int64_t out_cap, int sub, SlotFormat F) {
   const int64_t t = blockIdx.x;                  // super-tile
   const int k = F.k;
-  const int64_t words = cnt[t] * k, dst = pre[t] * k;
-  if (pre[t] + cnt[t] > out_cap) return;
-  for (int64_t w = threadIdx.x; w < words; w += blockDim.x) {
-    const int64_t m = w / k;
-    out[dst + w] = F.entry(slots, t, cnt[t], m, int(w - m * k));
+  const int64_t c = cnt[t], p = pre[t];
+  if (p + c > out_cap) return;
+  int32_t* const dst = out + p * k;
+  for (int64_t m = threadIdx.x; m < c; m += blockDim.x) {
+    int32_t v;
+    uint32_t a;
+    F.load(slots, t, c, m, v, a);
+    for (int s = 0; s < k; s++) dst[m * k + s] = F.value(v, a, s);
   }
 }
 
