@@ -28,7 +28,9 @@ struct RunState {
 
 constexpr int RUNS_COLCACHE = 4;   // columns of the current record held in registers
 
-__device__ __forceinline__ int64_t load_col(const RunsArgs& A, int col, int type, int64_t g) {
+// Record indices are 32-bit in the engine (a runs batch holds < 2^31 records, abi.cpp push_runs): half
+// the VALU work of 64-bit index arithmetic and comparisons in the per-record loop.
+__device__ __forceinline__ int64_t load_col(const RunsArgs& A, int col, int type, int32_t g) {
   const void* c = A.cols[col];
   if (type == T_I32) return static_cast<const int32_t*>(c)[g];
   return static_cast<const int64_t*>(c)[g];
@@ -36,7 +38,7 @@ __device__ __forceinline__ int64_t load_col(const RunsArgs& A, int col, int type
 
 struct RunEnv {
   const RunsArgs& A;
-  int64_t g;
+  int32_t g;
   const RunState& rs;
   int err;
   bool in_fold;
@@ -98,8 +100,8 @@ __device__ __forceinline__ RunsArgs runs_args_dev(const RunsArgs& A) {
 }
 
 struct RunResult {
-  int64_t end;        // record where the run consumed its last stage, -1 none
-  int64_t fail_at;    // record whose evaluation raised, -1 none
+  int32_t end;        // record where the run consumed its last stage, -1 none
+  int32_t fail_at;    // record whose evaluation raised, -1 none
   int err;
   bool open;          // the run consumed its key's last record of the batch and waits for the next
 };
@@ -107,7 +109,7 @@ struct RunResult {
 // item(i, &j, &stop): start record and last record to walk of item i (false: skip)
 // done(i, RunResult); on_consume(i, record, stage)
 template <class Tab, class Item, class Done, class Consume>
-__device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int64_t i0, int64_t i1, Item&& item, Done&& done,
+__device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int32_t i0, int32_t i1, Item&& item, Done&& done,
                                            Consume&& on_consume) {
   const auto& P = T.prog();                               // stage ids are wave-uniform: scalar reads
   RunState rs;
@@ -115,17 +117,18 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
   for (int q = 0; q < RUNS_MAX_STATES; q++) { rs.tag[q] = 0; rs.val[q] = 0; }
   RunResult res{-1, -1, 0, false};
   bool alive = false;
-  int64_t idx = -1, r = 0, stop = 0;
+  int32_t idx = -1, r = 0, stop = 0;
+  const int32_t n = int32_t(A.n);
   int ps = -1, cur = -1;
   int32_t k = 0;
-  int64_t next = i0;                                          // wave-uniform: next unassigned item
+  int32_t next = i0;                                          // wave-uniform: next unassigned item
   const int nst = P.nstages;
   const int ncc = P.ncols < RUNS_COLCACHE ? P.ncols : RUNS_COLCACHE;
   int64_t cv[RUNS_COLCACHE];
 #pragma unroll
   for (int q = 0; q < RUNS_COLCACHE; q++) cv[q] = 0;
   // the record's key and cached columns, issued together (one memory latency per step)
-  auto load_record = [&](int64_t g, int32_t* kk) {
+  auto load_record = [&](int32_t g, int32_t* kk) {
     *kk = A.key[g];
 #pragma unroll
     for (int q = 0; q < RUNS_COLCACHE; q++)
@@ -137,8 +140,8 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
     if (idle && next < i1) {
       const int rank = __builtin_amdgcn_mbcnt_hi(uint32_t(idle >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(idle), 0));
       if (!alive) {
-        const int64_t it = next + rank;
-        int64_t j = 0;
+        const int32_t it = next + rank;
+        int32_t j = 0;
         if (it < i1 && item(it, &j, &stop)) {
           idx = it;
           alive = true;
@@ -157,7 +160,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
       if (next >= i1) break;
       continue;
     }
-    const int64_t gs = alive ? r : i0;                          // a loadable record for idle lanes (JitTab)
+    const int32_t gs = alive ? r : i0;                          // a loadable record for idle lanes (JitTab)
     KCEP_UNROLL
     for (int s = nst - 1; s >= 1; s--) {
       const bool here = alive && ps == s;
@@ -227,7 +230,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int6
       if (ps == -1) {                                              // consumed: on to the next record
         r++;
         int32_t kr = k + 1;
-        if (r < A.n && r <= stop) load_record(r, &kr);
+        if (r < n && r <= stop) load_record(r, &kr);
         ps = kr == k ? cur : -2;
         if (ps == -2 && r <= stop) res.open = true;                // out of the key's records, not dead
       } else if (ps != -2) {
@@ -259,26 +262,27 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
   __shared__ int32_t s_end[RT / 64][RUNS_CHUNK];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
-  const int64_t i0 = wave * A.chunk, i1 = i0 + A.chunk < A.n ? i0 + A.chunk : A.n;
+  const int64_t i0l = wave * A.chunk;
+  const int32_t i0 = int32_t(i0l < A.n ? i0l : A.n), i1 = int32_t(i0l + A.chunk < A.n ? i0l + A.chunk : A.n);
   uint16_t* const myseg = s_seg[threadIdx.x];
   if (i0 < A.n) {
-    int64_t seg_item = -1;                                      // the lane's current start record
+    int32_t seg_item = -1;                                      // the lane's current start record
     int seg_last = -1, seg_n = 0;
     run_engine(
-        T, A, i0, i1, [&](int64_t i, int64_t* j, int64_t* stop) { *j = i; *stop = INT64_MAX; return true; },
-        [&](int64_t i, const RunResult& res) {
+        T, A, i0, i1, [&](int32_t i, int32_t* j, int32_t* stop) { *j = i; *stop = INT32_MAX; return true; },
+        [&](int32_t i, const RunResult& res) {
           // carry: a run that ended in the carried records was emitted by an earlier batch; -2 marks a
           // run still open at its key's last record (its start begins the key's next carried tail)
           const bool old_end = A.pos && res.end >= 0 && A.pos[res.end] < A.emit_from;
           s_end[wv][i - i0] = old_end ? -1 : res.open ? -2 : int32_t(res.end);
           if (res.fail_at >= 0 && !(A.pos && A.pos[res.fail_at] < A.emit_from)) {
             A.err_code[i] = res.err;
-            atomicMin(A.err_min, (unsigned long long)(res.fail_at << 31 | i));
+            atomicMin(A.err_min, (unsigned long long)(int64_t(res.fail_at) << 31 | i));
             if (A.err_list) {
               const unsigned long long q = atomicAdd(A.err_n, 1ull);
               if (int64_t(q) < A.err_cap) {
                 unsigned long long* e = A.err_list + 3 * q;
-                e[0] = (unsigned long long)(res.fail_at << 31 | i);
+                e[0] = (unsigned long long)(int64_t(res.fail_at) << 31 | i);
                 e[1] = (unsigned long long)(A.pos ? A.pos[res.fail_at] : res.fail_at);
                 e[2] = (unsigned long long)(uint32_t(A.key[i])) << 32 | uint32_t(res.err);
               }
@@ -292,14 +296,14 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
             else *reinterpret_cast<uint4*>(A.segs + i * 8) = *reinterpret_cast<const uint4*>(myseg);
           }
         },
-        [&](int64_t i, int64_t r, int stage) {
+        [&](int32_t i, int32_t r, int stage) {
           if (!A.segs) return;
           if (i != seg_item) { seg_item = i; seg_last = -1; seg_n = 0; }
           if (stage == seg_last) return;
           seg_last = stage;
-          const int64_t off = r - i;
+          const int32_t off = r - i;
           if (seg_n >= A.segn || off >= 4096 || stage >= 16) { atomicOr(A.seg_over, 1ull); return; }
-          myseg[seg_n++] = uint16_t(stage << 12 | int(off));
+          myseg[seg_n++] = uint16_t(stage << 12 | off);
         });
   }
   __syncthreads();                                              // (every wave reaches it)
@@ -362,21 +366,21 @@ __device__ __forceinline__ void put_entry(const Tab& T, const WriteArgs& W, int6
 template <class Tab>
 __device__ __forceinline__ void runs_write_body(const Tab& T, const WriteArgs& W) {
   const int64_t wave = (int64_t(blockIdx.x) * RT + threadIdx.x) >> 6;
-  const int64_t i0 = wave * W.R.chunk, i1 = i0 + W.R.chunk < W.nm ? i0 + W.R.chunk : W.nm;
-  if (i0 >= W.nm) return;
+  if (wave * W.R.chunk >= W.nm) return;
+  const int32_t i0 = int32_t(wave * W.R.chunk), i1 = int32_t(i0 + W.R.chunk < W.nm ? i0 + W.R.chunk : W.nm);
   run_engine(
       T, W.R, i0, i1,
-      [&](int64_t m, int64_t* j, int64_t* stop) {
+      [&](int32_t m, int32_t* j, int32_t* stop) {
         const unsigned long long kv = W.sorted[m];
-        *j = int64_t(kv & 0x7FFFFFFFull);
-        *stop = int64_t(kv >> 31);
+        *j = int32_t(kv & 0x7FFFFFFFull);
+        *stop = int32_t(kv >> 31);
         W.match_record[m] = W.R.pos ? W.R.pos[*stop] : W.R.base + *stop;
         W.match_key[m] = W.R.key[*j];
         W.ent_off_out[m] = W.ent_off[m];
         return true;
       },
-      [](int64_t, const RunResult&) {},
-      [&](int64_t m, int64_t r, int stage) {
+      [](int32_t, const RunResult&) {},
+      [&](int32_t m, int32_t r, int stage) {
         const int64_t end = int64_t(W.sorted[m] >> 31);
         put_entry(T, W, W.ent_off[m] + (end - r), stage, r);
       });
