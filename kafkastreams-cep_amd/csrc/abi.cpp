@@ -46,6 +46,8 @@ hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* i
                         int64_t* tmp, hipStream_t st);
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
 hipError_t set_words_launch(int64_t* w, int n, int at, int64_t v, hipStream_t st);
+hipError_t nfa_order_launch(const NfaArgs& A, int64_t nseg, uint8_t* bits, unsigned* bcnt, int32_t* order,
+                            hipStream_t st, const JitModule* j);
 hipError_t gather_words_launch(const int64_t* a, int na, const int64_t* b, int nb, int64_t* h, hipStream_t st);
 hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
                                int64_t* out1, int64_t* total0, int64_t* total1, int64_t* tmp, hipStream_t st);
@@ -188,7 +190,7 @@ struct cep_session {
   int zc_slot = -1;               // the push's kernels read ring slot zc_slot in place (zero copy)
   // ---- general workspace ----
   DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_ent, r_err, r_errrec, r_carry,
-      moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec;
+      moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec, ord, ord_bucket, ord_cnt;
   int64_t pool_words = 0;       // pool capacity to use (grows after an overflow)
   int64_t nseg = 0, g_matches = 0, g_entries = 0;
   int64_t nseg_hint = 0;        // the last general batch's segment count (pool estimate of the next)
@@ -918,6 +920,19 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       A.scratch = s->wscratch.as<int32_t>();
     }
   }
+  // the wave kernel's schedule: segments by estimated cost, heaviest first (nfa_dev.h stage_may_take;
+  // KCEP_NFA_ORDER=0: as they come, the tests' hook onto that order)
+  if (s->wave && !getenv_flag_off("KCEP_NFA_ORDER")) {
+    // ord_bucket: a byte per segment, then a byte per record (the per-record estimate bits)
+    // ord_cnt: 16 bucket sizes per 256 segments
+    if (s->ord.ensure(size_t(nseg) * 4) || s->ord_bucket.ensure(size_t(nseg) + size_t(n)) ||
+        s->ord_cnt.ensure(size_t((nseg + 255) / 256) * 64))
+      return fail(CEP_E_HIP, "allocation failed");
+    A.seg_bucket = s->ord_bucket.as<uint8_t>();
+    HIPCHECK(nfa_order_launch(A, nseg, s->ord_bucket.as<uint8_t>() + nseg, s->ord_cnt.as<unsigned>(), s->ord.as<int32_t>(),
+                              st, s->jitg.get()));
+    A.seg_order = s->ord.as<int32_t>();
+  }
   bool timed = false;
   bool grew = false;                               // the pool was regrown for this batch: given back after it
   bool pool_at_limit = false;                      // the pool cannot grow further: overflowing keys are handed back
@@ -1240,7 +1255,7 @@ void cep_session_close(cep_session* s) {
   for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->wscratch, &s->dstage, &s->dl_ticket,
                   &s->h_topic, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
-                  &s->r_carry, &s->r_ent, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
+                  &s->r_carry, &s->r_ent, &s->ord, &s->ord_bucket, &s->ord_cnt, &s->moff, &s->eoff, &s->o_record, &s->o_key, &s->o_entoff, &s->o_name,
                   &s->o_entrec, &s->ctab, &s->cpool, &s->kstamp, &s->halo, &s->hpos, &s->hflags, &s->opos, &s->rk, &s->rk_sorted, &s->rk_tmp, &s->r_segs, &s->r_blk, &s->r_len, &s->r_entoff,
                   &s->r_errcode, &s->r_errlist, &s->r_endof, &s->r_prof, &s->rtab, &s->rpool, &s->rpool2, &s->rtop, &s->e_key,
                   &s->e_topic, &s->e_part, &s->e_seg, &s->e_off, &s->e_ts, &s->e_pos, &s->rc_a, &s->rc_b, &s->rc_c,

@@ -447,6 +447,9 @@ std::string jit_source_general(const Program& P, std::string& why, bool phases) 
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()" + std::to_string(wave_occ) + R"())) void kcep_nfa_wave(kcep::NfaArgs A) {
   kcep::nfa_wave_body<)" + agg + R"(>(A);
 }
+extern "C" __global__ __launch_bounds__(256) void kcep_nfa_order(kcep::NfaArgs A, uint8_t* bits) {
+  kcep::nfa_order_bits_body(A, bits);
+}
 )";
   return o;
 }
@@ -454,9 +457,9 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu()
 std::shared_ptr<const JitModule> jit_general(const Program& P, std::string& why, bool phases) {
   const std::string src = jit_source_general(P, why, phases);
   if (src.empty()) return nullptr;
-  static const char* const names[] = {"kcep_nfa_kernel", "kcep_nfa_wave"};
-  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa, &JitModule::nfa_wave};
-  return build(src, names, slots, 2, why);
+  static const char* const names[] = {"kcep_nfa_kernel", "kcep_nfa_wave", "kcep_nfa_order"};
+  static hipFunction_t JitModule::* const slots[] = {&JitModule::nfa, &JitModule::nfa_wave, &JitModule::nfa_order};
+  return build(src, names, slots, 3, why);
 }
 
 bool jit_check_general(const Program& P, std::string& why) {

@@ -17,6 +17,7 @@ struct JitModule {
   hipFunction_t runs_write = nullptr;   // runs_dev.h runs_write_body<JitTab>
   hipFunction_t nfa = nullptr;          // nfa_dev.h nfa_kernel_body (general path)
   hipFunction_t nfa_wave = nullptr;     // nfa_wave.h nfa_wave_body, one key per wave (general path)
+  hipFunction_t nfa_order = nullptr;    // nfa_dev.h nfa_order_bits_body, the wave kernel's schedule estimate
   ~JitModule();
 };
 

@@ -158,6 +158,9 @@ struct NfaArgs {
                                   // check for runs sharing a sequence), bit 1 it has SequenceMatchers
   int32_t last_attempt;           // 1: no pool regrowth follows -- an overflowing key reports CEP_E_RUN_CAPACITY
   int32_t* seg_next;              // wave kernel: the next key segment a persistent wave takes (zeroed before)
+  const int32_t* seg_order;       // wave kernel: the segments in the order the waves take them (null: as they
+                                  // come), heaviest estimated first (nfa_order_*)
+  uint8_t* seg_bucket;            // nfa_order_count's estimate per segment (the placement reads it)
   int32_t* scratch;               // wave kernel: one recycled workspace region per workgroup (nfa_wave.h) ...
   int64_t scratch_words;          // ... of this many words (0: none)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY

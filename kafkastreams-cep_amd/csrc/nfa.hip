@@ -237,6 +237,118 @@ hipError_t nfa_launch(const NfaArgs& A, hipStream_t st, hipFunction_t jf) {
   return hipGetLastError();
 }
 
+// ---- the wave kernel's schedule (nfa_dev.h stage_may_take): heaviest estimated segments first ----
+__global__ __launch_bounds__(256) void nfa_order_bits(NfaArgs A, uint8_t* bits) { nfa_order_bits_body(A, bits); }
+// The per-wave bucket sizes of a 256-thread block into s_w[4][16] (no atomics: each wave its own row);
+// returns the lane's rank among its wave's lanes of its bucket
+__device__ __forceinline__ unsigned order_wave_counts(int b, unsigned (*s_w)[16]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned rank = 0;
+  for (int q = 0; q < 16; q++) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(b == q);
+    if (lane == 0) s_w[wv][q] = unsigned(__popcll(m));
+    if (b == q) rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0));
+  }
+  return rank;
+}
+// one thread per segment: its weight from its records' bits (walked backwards: sum over begin-matching
+// records of 2^(later matching records)), log2-bucketed; each block's bucket sizes into bcnt[block][16]
+__global__ __launch_bounds__(256) void nfa_order_count(const int64_t* __restrict__ seg_start,
+                                                       const int64_t* __restrict__ nseg_dev, int64_t nseg_host,
+                                                       const uint8_t* __restrict__ bits, uint8_t* __restrict__ bucket,
+                                                       unsigned* __restrict__ bcnt) {
+  __shared__ unsigned s_w[4][16];
+  const int64_t nseg = nseg_dev ? *nseg_dev : nseg_host;
+  if (int64_t(blockIdx.x) * blockDim.x >= nseg) return;   // (the grid is sized by a bound)
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  int b = -1;
+  if (t < nseg) {
+    float w = 0.f;
+    int after = 0;
+    for (int64_t g = seg_start[t + 1] - 1; g >= seg_start[t]; g--) {
+      const uint32_t x = bits[g];
+      if (x & 1) w += exp2f(float(after < 100 ? after : 100));
+      after += (x >> 1) & 1;
+    }
+    const int lb = w < 2.f ? 0 : int(log2f(w));
+    b = lb < 15 ? lb : 15;
+    bucket[t] = uint8_t(b);
+  }
+  order_wave_counts(b, s_w);
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int q = threadIdx.x;
+    bcnt[size_t(blockIdx.x) * 16 + q] = s_w[0][q] + s_w[1][q] + s_w[2][q] + s_w[3][q];
+  }
+}
+// each segment's place: the buckets from the heaviest down, within a bucket by segment index (a
+// deterministic schedule; the schedule only: every key's results land in its own segment's slots)
+__global__ __launch_bounds__(256) void nfa_order_place(const int64_t* __restrict__ nseg_dev, int64_t nseg_host,
+                                                       const uint8_t* __restrict__ bucket,
+                                                       const unsigned* __restrict__ bcnt, int32_t* __restrict__ order) {
+  __shared__ unsigned s_tot[16][17], s_bef[16][17], s_base[16], s_w[4][16];
+  const int64_t nseg = nseg_dev ? *nseg_dev : nseg_host;
+  if (int64_t(blockIdx.x) * blockDim.x >= nseg) return;
+  const int64_t nblk = (nseg + 255) / 256;
+  {                                                // bucket q over all blocks / the blocks before this one
+    const int q = threadIdx.x & 15, part = threadIdx.x >> 4;
+    unsigned tot = 0, bef = 0;
+    for (int64_t k = part; k < nblk; k += 16) {
+      const unsigned c = bcnt[size_t(k) * 16 + q];
+      tot += c;
+      bef += k < int64_t(blockIdx.x) ? c : 0u;
+    }
+    s_tot[q][part] = tot;
+    s_bef[q][part] = bef;
+  }
+  const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int b = t < nseg ? int(bucket[t]) : -1;
+  const unsigned rank = order_wave_counts(b, s_w);
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int q = threadIdx.x;
+    unsigned tot = 0, bef = 0;
+    for (int k = 0; k < 16; k++) {
+      tot += s_tot[q][k];
+      bef += s_bef[q][k];
+    }
+    s_tot[q][16] = tot;
+    s_bef[q][16] = bef;
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {                          // heavier buckets first, then this bucket's earlier blocks
+    const int q = threadIdx.x;
+    unsigned base = s_bef[q][16];
+    for (int r = q + 1; r < 16; r++) base += s_tot[r][16];
+    s_base[q] = base;
+  }
+  __syncthreads();
+  if (b < 0) return;
+  const int wv = threadIdx.x >> 6;
+  unsigned at = s_base[b] + rank;
+  for (int k = 0; k < wv; k++) at += s_w[k][b];
+  order[at] = int32_t(t);
+}
+// bits: A.n bytes; bcnt: 16 words per 256 segments; the segment grids over nseg (an upper bound with
+// A.nseg_dev: their blocks past the real count return at once)
+hipError_t nfa_order_launch(const NfaArgs& A, int64_t nseg, uint8_t* bits, unsigned* bcnt, int32_t* order,
+                            hipStream_t st, const JitModule* j) {
+  if (nseg <= 0 || A.n <= 0) return hipSuccess;
+  const unsigned rblocks = unsigned((A.n + 255) / 256), sblocks = unsigned((nseg + 255) / 256);
+  if (j && j->nfa_order) {
+    NfaArgs a = A;
+    void* args[] = {&a, &bits};
+    hipError_t e = hipModuleLaunchKernel(j->nfa_order, rblocks, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+    if (e != hipSuccess) return e;
+  } else {
+    hipLaunchKernelGGL(nfa_order_bits, dim3(rblocks), dim3(256), 0, st, A, bits);
+  }
+  hipLaunchKernelGGL(nfa_order_count, dim3(sblocks), dim3(256), 0, st, A.seg_start, A.nseg_dev, nseg, bits, A.seg_bucket,
+                     bcnt);
+  hipLaunchKernelGGL(nfa_order_place, dim3(sblocks), dim3(256), 0, st, A.nseg_dev, nseg, A.seg_bucket, bcnt, order);
+  return hipGetLastError();
+}
+
 // The workgroups (one wave each) the wave kernel's persistent grid should have: as many as the chip
 // holds at once (occupancy x compute units), at most one per segment.
 int64_t nfa_wave_grid(int64_t nseg, bool agg, const JitModule* j) {

@@ -735,6 +735,41 @@ __device__ __forceinline__ void eval_event_only(Lane& l) {
   }
 }
 
+// ---- the wave kernel's schedule: heaviest keys first ----
+// A key's cost is unknown until it runs (C4: a key's live runs multiply with every matching record),
+// and keys that happen to be heavy and come last leave the chip idle behind them (C4, one batch:
+// 81 % of wave slots busy on average, the last 0.9 ms of 5.4 at < 90 %).  An estimate from the
+// event-only edge predicates: each record that a begin-stage consuming edge may take opens runs that
+// every later record a consuming edge of another stage may take can double, so a segment weighs
+// sum over its begin-matching records of 2^(later matching records) -- bucketed by log2 (16 buckets).
+// On C4's per-key times this order gives a list-schedule makespan within 1 % of the true-cost order
+// (4479 / 4452 us against 5275 us as the keys come; tools/c4_profile.py --save).
+__device__ __forceinline__ bool stage_may_take(const Lane& l, int s) {
+  const int ne = ST_NEDGES(l, s);
+  for (int e = 0; e < ne; e++) {
+    const int op = ST_OP(l, s, e);
+    if (op != E_BEGIN && op != E_TAKE) continue;
+    const int sl = ST_SL(l, s, e);
+    if (ST_PRED(l, s, e) < 0 || sl < 0 || ((l.slm | l.sle) >> sl) & 1) return true;   // (not event-only: may)
+  }
+  return false;
+}
+// one thread per batch record: bit 0 a begin-stage consuming edge may take it, bit 1 one of another stage
+__device__ __forceinline__ void nfa_order_bits_body(const NfaArgs& A, uint8_t* bits) {
+  const int64_t g = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= A.n) return;
+  Lane l{};
+  l.A = &A;
+  l.P = A.P;
+  l.g = g;
+  eval_event_only(l);
+  const int ns = KCEP_PROG(l).nstages, b = KCEP_PROG(l).begin;
+  bool other = false;
+  for (int s = 1; s < ns; s++)
+    if (s != b && stage_may_take(l, s)) { other = true; break; }
+  bits[g] = uint8_t((stage_may_take(l, b) ? 1 : 0) | (other ? 2 : 0));
+}
+
 // NFA.runs++ (NFA.java:297, :331).  Wave mode: a placeholder -(2 + k) for the lane's k-th increment;
 // the wave numbers them in queue order after the round (nfa_wave.h wave_fix_seq)
 template <bool W = false>

@@ -803,6 +803,7 @@ __device__ __forceinline__ void nfa_wave_body(const NfaArgs& A) {
     if (gp.gl == 0) seg = atomicAdd(A.seg_next, 1);
     seg = gp.bcast(seg);
     if (seg >= nseg) break;                        // every wave of the grid reaches this
+    if (A.seg_order) seg = A.seg_order[seg];
     wave_key<AGG, WAVE>(A, seg, gp, ws, s_arena, ARENA, s_priv, scr);
     wave_sync();
   }

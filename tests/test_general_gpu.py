@@ -255,10 +255,14 @@ def test_key_over_capacity_at_first_allocation(lane_nfa):
     assert got == [m for m in want if m[1] != 7]
 
 
+@pytest.mark.parametrize("order", ["cost", "arrival"])
 @pytest.mark.parametrize("lane_nfa", [False, True], ids=["wave", "lane"])
-def test_c4_heavy_keys(lane_nfa):
+def test_c4_heavy_keys(lane_nfa, order, monkeypatch):
     """C4 (skip-till-any times(3) + zeroOrMore) keys long enough that one record's run queue holds
-    several rounds of 64 runs on the wave kernel; every match, in order, as the oracle's."""
+    several rounds of 64 runs on the wave kernel; every match, in order, as the oracle's.  The wave
+    kernel takes the keys heaviest-estimated first (nfa_dev.h seg_bucket) or as they come
+    (KCEP_NFA_ORDER=0): the schedule changes nothing in the output."""
+    monkeypatch.setenv("KCEP_NFA_ORDER", "1" if order == "cost" else "0")
     from kcep import synth
     key, val, _ = synth.c4_stream_np(400, L=16)
     ir = synth.c4_pattern().to_ir(PL.I32)

@@ -24,6 +24,9 @@ for i in range(3):
     s.push(n, key.data_ptr(), [val.data_ptr()], ts=ts.data_ptr(), mem=N.MEM_DEVICE, stream=st)
     kms = s.last_kernel_ms()
 prof = s.key_profile()
+if "--save" in sys.argv:                              # per-key rows for offline analysis
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(ROOT, "gpurun_out", "c4_key_profile.npy"), prof)
 cyc = prof[:, 3].astype(np.float64) / 100.0   # wall clock 100 MHz -> us
 live, ev = prof[:, 1], prof[:, 2]
 print(f"jit={s.jit} kernel {kms:.2f} ms  keys {len(prof)}  live-run hwm {s.live_run_hwm()}")
