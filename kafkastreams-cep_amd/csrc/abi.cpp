@@ -47,7 +47,13 @@ hipError_t nfa_segments(const int32_t* key, int64_t n, int64_t* flag, int64_t* i
 hipError_t exclusive_scan(const int64_t* in, int64_t n, int64_t* out, int64_t* total, int64_t* tmp, hipStream_t st);
 hipError_t set_words_launch(int64_t* w, int n, int at, int64_t v, hipStream_t st);
 hipError_t nfa_order_launch(const NfaArgs& A, int64_t nseg, uint8_t* bits, unsigned* bcnt, int32_t* order,
-                            hipStream_t st, const JitModule* j);
+                            hipStream_t st, const JitModule* j, int lo);
+// The schedule's estimate buckets (log2 of the segment weight) below this one keep arrival order
+// behind the heavier ones: only a key that could end the grid late needs to start early, and every
+// key moved forward adds scratch lines in flight beside the other heavy keys (C4, lowest ordered
+// bucket 0 / 4 / 6 / 8 / 10: kernel 4.240 / 4.255 / 4.282 / 4.273 / 4.573 ms, kcep_nfa_wave
+// 201.2 / 201.3 / 200.9 / 197.6 / 183.0 MB per launch; profiles/r05_c4_order_lo.txt)
+constexpr int NFA_ORDER_LO = 8;
 hipError_t gather_words_launch(const int64_t* a, int na, const int64_t* b, int nb, int64_t* h, hipStream_t st);
 hipError_t exclusive_scan_pair(const int64_t* in0, const int64_t* in1, int64_t n, const int64_t* n_dev, int64_t* out0,
                                int64_t* out1, int64_t* total0, int64_t* total1, int64_t* tmp, hipStream_t st);
@@ -930,7 +936,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       return fail(CEP_E_HIP, "allocation failed");
     A.seg_bucket = s->ord_bucket.as<uint8_t>();
     HIPCHECK(nfa_order_launch(A, nseg, s->ord_bucket.as<uint8_t>() + nseg, s->ord_cnt.as<unsigned>(), s->ord.as<int32_t>(),
-                              st, s->jitg.get()));
+                              st, s->jitg.get(), NFA_ORDER_LO));
     A.seg_order = s->ord.as<int32_t>();
   }
   bool timed = false;

@@ -252,11 +252,12 @@ __device__ __forceinline__ unsigned order_wave_counts(int b, unsigned (*s_w)[16]
   return rank;
 }
 // one thread per segment: its weight from its records' bits (walked backwards: sum over begin-matching
-// records of 2^(later matching records)), log2-bucketed; each block's bucket sizes into bcnt[block][16]
+// records of 2^(later matching records)), log2-bucketed, buckets below lo merged into bucket 0 (their
+// segments keep arrival order); each block's bucket sizes into bcnt[block][16]
 __global__ __launch_bounds__(256) void nfa_order_count(const int64_t* __restrict__ seg_start,
                                                        const int64_t* __restrict__ nseg_dev, int64_t nseg_host,
                                                        const uint8_t* __restrict__ bits, uint8_t* __restrict__ bucket,
-                                                       unsigned* __restrict__ bcnt) {
+                                                       unsigned* __restrict__ bcnt, int lo) {
   __shared__ unsigned s_w[4][16];
   const int64_t nseg = nseg_dev ? *nseg_dev : nseg_host;
   if (int64_t(blockIdx.x) * blockDim.x >= nseg) return;   // (the grid is sized by a bound)
@@ -272,6 +273,7 @@ __global__ __launch_bounds__(256) void nfa_order_count(const int64_t* __restrict
     }
     const int lb = w < 2.f ? 0 : int(log2f(w));
     b = lb < 15 ? lb : 15;
+    b = b < lo ? 0 : b;
     bucket[t] = uint8_t(b);
   }
   order_wave_counts(b, s_w);
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(256) void nfa_order_place(const int64_t* __restrict
 // bits: A.n bytes; bcnt: 16 words per 256 segments; the segment grids over nseg (an upper bound with
 // A.nseg_dev: their blocks past the real count return at once)
 hipError_t nfa_order_launch(const NfaArgs& A, int64_t nseg, uint8_t* bits, unsigned* bcnt, int32_t* order,
-                            hipStream_t st, const JitModule* j) {
+                            hipStream_t st, const JitModule* j, int lo) {
   if (nseg <= 0 || A.n <= 0) return hipSuccess;
   const unsigned rblocks = unsigned((A.n + 255) / 256), sblocks = unsigned((nseg + 255) / 256);
   if (j && j->nfa_order) {
@@ -344,7 +346,7 @@ hipError_t nfa_order_launch(const NfaArgs& A, int64_t nseg, uint8_t* bits, unsig
     hipLaunchKernelGGL(nfa_order_bits, dim3(rblocks), dim3(256), 0, st, A, bits);
   }
   hipLaunchKernelGGL(nfa_order_count, dim3(sblocks), dim3(256), 0, st, A.seg_start, A.nseg_dev, nseg, bits, A.seg_bucket,
-                     bcnt);
+                     bcnt, lo);
   hipLaunchKernelGGL(nfa_order_place, dim3(sblocks), dim3(256), 0, st, A.nseg_dev, nseg, A.seg_bucket, bcnt, order);
   return hipGetLastError();
 }
