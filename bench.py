@@ -20,6 +20,14 @@ next step.
 ``--config c3|c4|c5`` measures the other BASELINE configs (not the headline
 line; DESIGN.md reports them).
 
+Launch.  ``python3 bench.py --gpus N`` with N > 1 and no ``WORLD_SIZE`` in the
+environment starts the N ranks itself (``launch``: N child processes with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, rank 0's
+line relayed, a failing rank fails the run); the parent never touches the GPU.
+Under ``torch.distributed.run`` (WORLD_SIZE set) each process is one rank.
+Without a visible GPU the ranks run a dry run on CPU (gloo): the launch, the
+partitioner and the per-rank totals, nothing matched, ``value`` null.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -49,6 +57,9 @@ CONFIGS = {
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal (gloo): launch, partitioner and per-rank totals, nothing matched; "
+                         "automatic when no GPU is visible")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
@@ -133,15 +144,110 @@ def workload(cfg: str, rank: int, world: int, K: int, n: int | None, dev, stream
     return sh.key, sh.cols, sh.extra["ts"], ir, (sh, info)
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, argv) -> int:
+    """``--gpus n`` without a launcher: one child process per rank (this script again, never an exec),
+    each with RANK / LOCAL_RANK / WORLD_SIZE and a 127.0.0.1 rendezvous.  Rank 0's stdout (the JSON line)
+    is relayed; the other ranks' stdout goes to stderr.  The first rank to fail ends the run: the others
+    are killed by PID and its exit status is returned.  This process imports neither torch nor the
+    library, so it never touches a GPU; each rank checks ``n`` against the devices it sees."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.kill()
+            if live:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
+def dry_run(args, world: int, rank: int):
+    """No GPU visible: the multi-rank path up to the device, on CPU.  Every rank builds the node-wide
+    stream, takes its shard with the product partitioner (kcep/shard.py on CPU tensors: cep_shard_plan +
+    the host cep_partition / cep_gather) and the ranks all-gather their event counts over gloo.  Nothing is
+    matched (the kernels need a GPU), so ``value`` is null.  Sizes default to 1/100 of the config's."""
     import torch
     import torch.distributed as dist
-    from kcep import native as N
+    if world > 1:
+        dist.init_process_group("gloo")
+    C = CONFIGS[args.config]
+    K = args.keys or max(1, C["keys"] // 100)
+    n_req = args.events or (C["events"] // 100 if C.get("events") else None)
+    key, cols, ts, ir, shard_info = workload(args.config, rank, world, K, n_req, torch.device("cpu"), None)
+    n = int(key.numel())
+    mine = torch.tensor([float(n), float(torch.unique(key).numel())], dtype=torch.float64)
+    per = [torch.zeros_like(mine) for _ in range(world)] if world > 1 else [mine]
+    if world > 1:
+        dist.all_gather(per, mine)
+    if rank == 0:
+        line = {"metric": METRIC if args.config == "c2" else f"events/sec (whole node), {C['desc']}",
+                "value": None, "unit": "events/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": None, "higher_is_better": True,
+                "scaling": "strong" if C.get("node_wide") and world > 1 else "weak", "vs_baseline": None,
+                "dtype": "int32", "data": "synthetic (splitmix64 counter RNG, BASELINE.md §3)",
+                "config": {"workload": C["desc"], "keys_per_gpu": K,
+                           "parallelism": f"key-hash sharded x{world}" if world > 1 else "1 GPU",
+                           "events_per_rank": [int(p[0]) for p in per], "keys_per_rank": [int(p[1]) for p in per]},
+                "roofline": None, "cpu_baseline": None,
+                "dry_run": "no GPU visible: launch, partitioner and per-rank totals on CPU (gloo); nothing matched"}
+        if shard_info is not None:
+            line["config"]["shard"] = shard_info[1]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus, argv))
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: running {world} ranks", file=sys.stderr)
+    if os.environ.get("KCEP_BENCH_FAIL_RANK") == str(rank):      # tests/test_bench_launch.py: a failing rank
+        sys.exit(3)
+    if args.dry_run or not torch.cuda.is_available():
+        return dry_run(args, world, rank)
+    if world > torch.cuda.device_count():
+        raise SystemExit(f"bench.py: {world} ranks but only {torch.cuda.device_count()} GPUs visible")
+    from kcep import native as N
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
