@@ -91,11 +91,13 @@ typedef struct {
                               session keeps its state as of the batch start, and every other key of the
                               batch completes normally.  The host routes that key to the reference CPU path
                               (a key over capacity falls back per key). */
-  int64_t max_pool_bytes;  /* general path: device memory the session's NFA workspace pool may grow to when a
-                              batch overflows it (0 = a quarter of the device's HBM).  Past it the overflowing
-                              keys are handed back per key as above.  A pool grown for one batch is given back
-                              after that batch, so one heavy batch does not hold the device for the session's
-                              lifetime (several sessions share one GPU: one GpuCEPProcessor per stream task) */
+  int64_t max_pool_bytes;  /* general path: device memory the session's NFA workspace may grow to when a batch
+                              overflows its pool (0 = a quarter of the device's HBM): the pool plus the wave
+                              kernel's per-workgroup scratch regions.  Past it the overflowing keys are handed
+                              back per key as above.  The next batches start from the grown size (no re-run
+                              per batch); after 4 batches in a row that fit the estimated pool it is given
+                              back, so one heavy stretch does not hold the device for the session's lifetime
+                              (several sessions share one GPU: one GpuCEPProcessor per stream task) */
 } cep_opts;
 
 /* Session flags */
@@ -210,6 +212,9 @@ int cep_session_jit(const cep_session* s);
 /* General path: 1 if the session runs one key per wave (kcep_nfa_wave, CEP_SESSION_WAVE_NFA), 0 if one
    key per lane (kcep_nfa_kernel) or another path */
 int cep_session_wave(const cep_session* s);
+/* General path: kernel attempts the last batch took (1, plus one per pool regrowth re-run); 0 if the last
+   batch ran on another path.  cep_last_kernel_ms times the first attempt only. */
+int cep_batch_attempts(const cep_session* s);
 /* General path: the most live runs (NFA run queue length, NFAStates.java:33-37) any key held during the
    last batch -- C4's run-explosion high-water mark.  -1 if the last batch ran on another path. */
 int cep_live_run_hwm(const cep_session* s, int64_t* hwm);
@@ -256,6 +261,14 @@ const int64_t* cep_device_match_count(const cep_session* s);
 /* Waits for the last batch and materialises the host CSR.  A second call before the next push
  * returns the same CSR without touching the device. */
 int cep_collect(cep_session* s, cep_matches* out);
+
+/* Host-only consistency check of a CSR before it is walked: ent_off starts at 0, never decreases and ends
+ * at n_entries; every match_record and ent_record lies in [0, n_records); every ent_name in [0, n_names).
+ * cep_collect applies it to the device-written CSR of the general and runs paths (n_records = the batch,
+ * or everything pushed so far on a carry session), so a device fault surfaces as CEP_E_HIP instead of a
+ * host crash in the walk (the reference fails the task with an exception,
+ * SharedVersionedBufferStoreImpl.java:113-115). */
+int cep_csr_check(const cep_matches* m, int64_t n_records, int32_t n_names);
 
 /* Order-independent 64-bit checksum of the last batch's matches, computed on
  * the device (matches the oracle's orc_baseline checksum); waits. */

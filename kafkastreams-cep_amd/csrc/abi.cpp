@@ -154,6 +154,7 @@ uint64_t mix64(uint64_t x) {
 // first allocation of a key's workspace on the general path (grown on demand from the pool)
 constexpr NfaCaps kCaps{16, 64, 32, 32, 8, 16};
 constexpr int kMaxRetry = 24;                      // pool regrowths (each toward free HBM) before CEP_E_RUN_CAPACITY
+constexpr int kPoolQuiet = 4;                      // batches within the estimate before a grown pool is given back
 constexpr int64_t kRunsErrCap = int64_t(1) << 20;  // runs path: failing runs listed per batch (cep_batch_errors)
 }  // namespace
 
@@ -197,7 +198,12 @@ struct cep_session {
   // ---- general workspace ----
   DBuf dprog, flag, idx, seg, scan_tmp, scal, ctl, pool, r_matches, r_words, r_out, r_ent, r_err, r_errrec, r_carry,
       moff, eoff, o_record, o_key, o_entoff, o_name, o_entrec, ord, ord_bucket, ord_cnt;
-  int64_t pool_words = 0;       // pool capacity to use (grows after an overflow)
+  int64_t pool_words = 0;       // pool capacity this batch uses
+  int64_t pool_est = 0;         // the batches' estimated pool (largest so far)
+  int64_t pool_learned = 0;     // what the last overflowing batch grew the pool to (0: none): later batches start
+                                // there, without re-running, until kPoolQuiet batches in a row fit the estimate
+  int pool_quiet = 0;
+  int last_attempts = 0;        // general path: kernel attempts of the last batch (1 + pool regrowths)
   int64_t nseg = 0, g_matches = 0, g_entries = 0;
   int64_t nseg_hint = 0;        // the last general batch's segment count (pool estimate of the next)
   // ---- carried per-key state (CEP_SESSION_CARRY): NFAStore equivalent ----
@@ -609,7 +615,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     if (nosync) {
       n = nmax;
       if ((rc = tail_reserve(s, n, st))) return rc;  // room for the new tails (at most every record)
-      HIPCHECK(runs_carry_count(scal + 7, nb, scal + 5, st));
+      HIPCHECK(runs_carry_count(scal + 7, nb, scal + 5, nmax, st));
     } else {
       int64_t h[6];
       HIPCHECK(hipMemcpyAsync(h, scal, sizeof h, hipMemcpyDeviceToHost, st));
@@ -626,6 +632,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     X.key = s->e_key.as<int32_t>(); X.topic = s->e_topic.as<int32_t>(); X.partition = s->e_part.as<int32_t>();
     X.seg = s->e_seg.as<int32_t>(); X.offset = s->e_off.as<int64_t>(); X.ts = s->e_ts.as<int64_t>();
     X.pos = s->e_pos.as<int64_t>();
+    X.cap = n;
     X.ncols = int32_t(PP.coltypes.size());
     for (int c = 0; c < X.ncols; c++) {
       X.coltype[c] = PP.coltypes[c];
@@ -888,8 +895,10 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   const int64_t per_key = 48 + 16 * cap.q0 + 3 * D.nstates * (cap.seq_base + 1) + cap.heap_base + cap.out_base + 16;
   const int64_t per_ev = 4 * D.nslots + cap.heap_mult + cap.out_mult + 4 + 3 * D.nstates;
   int64_t est = nseg_est * per_key + (n + (s->carry ? s->cpool_used / 4 : 0)) * per_ev;
-  s->pool_words = std::max<int64_t>(s->pool_words, est + est / 2 + (int64_t(1) << 20));
-  const int64_t pool_base = s->pool_words;         // what the batch starts with (kept for the next batch)
+  s->pool_est = std::max<int64_t>(s->pool_est, est + est / 2 + (int64_t(1) << 20));
+  // a workload that needed a regrown pool starts from that size (no re-run per batch), until kPoolQuiet
+  // batches in a row fit the estimate again
+  s->pool_words = std::max(s->pool_est, s->pool_learned);
   A.cap = cap;
   A.carry = s->carry ? 1 : 0;
   A.max_keys = int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX));
@@ -951,7 +960,13 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   int attempts = 0;
   for (int attempt = 0;; attempt++) {
     attempts = attempt + 1;
-    if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
+    if (s->pool.ensure(size_t(s->pool_words) * 4)) {
+      if (s->pool_words <= s->pool_est) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
+      (void)hipGetLastError();                     // the learned size no longer fits: back to the estimate
+      s->pool_learned = 0;
+      s->pool_words = s->pool_est;
+      if (s->pool.ensure(size_t(s->pool_words) * 4)) return fail(CEP_E_RUN_CAPACITY, "cannot allocate the NFA pool");
+    }
     if (s->carry && s->cpool_used + nseg * 64 > s->cpool_words) {
       if ((rc = carry_gc(s, 2 * (s->cpool_used + nseg * 64), st))) return rc;
     }
@@ -1017,7 +1032,9 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
       s->pool.release();                           // within the session's budget (cep_opts.max_pool_bytes,
       size_t free_b = 0, total_b = 0;              // default a quarter of the HBM) and the free HBM (keeping
       HIPCHECK(hipMemGetInfo(&free_b, &total_b));  // 1/16 of it): past that a key is handed back per key
-      const int64_t budget = (s->opts.max_pool_bytes > 0 ? s->opts.max_pool_bytes : int64_t(total_b / 4)) / 4;
+      // (the wave kernel's scratch regions count against the budget too)
+      const int64_t budget = ((s->opts.max_pool_bytes > 0 ? s->opts.max_pool_bytes : int64_t(total_b / 4)) -
+                              int64_t(s->wscratch.cap)) / 4;
       const int64_t room = std::min<int64_t>(int64_t(free_b / 4) - int64_t(free_b / 64), budget);
       const int64_t want = std::min<int64_t>(s->pool_words * 2, room);
       if (want <= s->pool_words) pool_at_limit = true;
@@ -1030,6 +1047,8 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   }
   // compaction into the CSR (counts scanned with the last attempt)
   s->nseg_hint = nseg;
+  s->last_attempts = attempts;
+  const int64_t pool_used = s->h_res[0];           // the successful attempt's pool top
   s->g_matches = tots[0];
   s->g_entries = tots[1];
   if (!(spec && attempts == 1 && tots[0] <= cap_m && tots[1] <= cap_e)) {
@@ -1051,10 +1070,20 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
     s->base += n;
   }
   HIPCHECK(hipEventRecord(s->eb1, st));
-  if (grew) {                                      // one heavy batch does not keep the device's memory: the
-    HIPCHECK(hipStreamSynchronize(st));            // compaction has read the matches out of the pool
-    s->pool.release();
-    s->pool_words = pool_base;
+  if (grew) {                                      // the next batches start from the grown size
+    s->pool_learned = s->pool_words;
+    s->pool_quiet = 0;
+  } else if (s->pool_learned > 0) {
+    s->pool_quiet = pool_used > s->pool_est ? 0 : s->pool_quiet + 1;
+    if (s->pool_quiet >= kPoolQuiet) {
+      // kPoolQuiet batches in a row within the estimate: the grown pool is given back, so one heavy stretch
+      // does not hold the device for the session's lifetime (the compaction has read the matches out of it)
+      HIPCHECK(hipStreamSynchronize(st));
+      s->pool.release();
+      s->wscratch.release();
+      s->pool_learned = 0;
+      s->pool_quiet = 0;
+    }
   }
   // the reference fails the task at its first exception: report the earliest failing record
   if (!s->g_any_err) {                             // no key raised: nothing to read back
@@ -1333,6 +1362,8 @@ int cep_session_jit(const cep_session* s) {
 
 int cep_session_wave(const cep_session* s) { return s && s->path == CEP_PATH_GENERAL && s->wave ? 1 : 0; }
 
+int cep_batch_attempts(const cep_session* s) { return s && s->last_path == CEP_PATH_GENERAL ? s->last_attempts : 0; }
+
 int cep_pattern_kernel_source(const cep_pattern* p, int path, char* buf, size_t cap, size_t* needed) {
   if (!p || !needed) return fail(CEP_E_ARG, "null argument");
   const bool runs = path == CEP_PATH_RUNS && p->prog.runs_ok, general = path == CEP_PATH_GENERAL && p->prog.general_ok;
@@ -1458,6 +1489,28 @@ int cep_last_batch_ms(cep_session* s, float* ms) {
   return CEP_OK;
 }
 
+// A device-written CSR is checked before any host code walks it: a device bug then fails the call with
+// CEP_E_HIP instead of crashing the JVM or Python process (the reference fails the task with an exception,
+// SharedVersionedBufferStoreImpl.java:113-115, never with a crash).
+int cep_csr_check(const cep_matches* m, int64_t n_records, int32_t n_names) {
+  if (!m) return fail(CEP_E_ARG, "null argument");
+  const int64_t nm = m->n_matches, ne = m->n_entries;
+  if (nm < 0 || ne < 0) return fail(CEP_E_HIP, "device CSR inconsistent: negative counts");
+  if (nm == 0) return ne == 0 && (!m->ent_off || m->ent_off[0] == 0) ? CEP_OK
+                                                                   : fail(CEP_E_HIP, "device CSR inconsistent: entries without matches");
+  if (!m->match_record || !m->ent_off || (ne > 0 && (!m->ent_name || !m->ent_record)))
+    return fail(CEP_E_HIP, "device CSR inconsistent: missing arrays");
+  if (m->ent_off[0] != 0 || m->ent_off[nm] != ne) return fail(CEP_E_HIP, "device CSR inconsistent: entry offsets' ends");
+  bool bad = false;
+  for (int64_t i = 0; i < nm; i++)
+    bad |= m->ent_off[i + 1] < m->ent_off[i] || uint64_t(m->match_record[i]) >= uint64_t(n_records);
+  if (bad) return fail(CEP_E_HIP, "device CSR inconsistent: entry offsets or match records out of range");
+  for (int64_t e = 0; e < ne; e++)
+    bad |= uint64_t(m->ent_record[e]) >= uint64_t(n_records) || uint32_t(m->ent_name[e]) >= uint32_t(n_names);
+  if (bad) return fail(CEP_E_HIP, "device CSR inconsistent: entry records or stage names out of range");
+  return CEP_OK;
+}
+
 int cep_collect(cep_session* s, cep_matches* o) {
   if (!s || !o) return fail(CEP_E_ARG, "null argument");
   RoctxRange range("cep_collect");
@@ -1491,6 +1544,13 @@ int cep_collect(cep_session* s, cep_matches* o) {
     o->path = s->last_path;
     o->err = s->g_err;
     o->err_record = s->g_err_rec;
+    o->match_record = s->match_record.data();
+    o->ent_off = s->ent_off.data();
+    o->ent_name = s->ent_name.data();
+    o->ent_record = s->ent_record.data();
+    // records: the batch's (stream positions on carry sessions: everything pushed so far)
+    int rc = cep_csr_check(o, s->carry ? s->base : s->n, int32_t(s->pat->prog.names.size()));
+    if (rc) return rc;
     if (s->g_err) g_err = "the reference NFA raises an exception on this batch";
   } else if (s->delivered) {                       // CEP_BATCH_DELIVER: the device wrote the CSR's inputs
     const StencilProgram& SP = s->pat->prog.stencil;

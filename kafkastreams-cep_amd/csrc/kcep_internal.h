@@ -222,12 +222,14 @@ struct RcExt {
   void* cols[16];
   int32_t coltype[16];
   int32_t ncols;
+  int64_t cap;                       // records the arrays hold: writes past it are dropped (a batch with a key
+                                     // in two segments gives that key's tail to both; it is rejected anyway)
 };
 hipError_t runs_carry_build(const RcIn& B, int64_t n, int64_t base, const int64_t* seg_flag, const int64_t* seg_idx,
                             const int64_t* seg_start, const int64_t* nseg, const int64_t* rtab, const int64_t* rpool,
                             int64_t* tlen, int64_t* toff, int64_t* total, int64_t* scan_tmp, const RcExt& X,
                             hipStream_t st, bool lens_only, int32_t max_keys);
-hipError_t runs_carry_count(int64_t* out, int64_t nb, const int64_t* tails, hipStream_t st);
+hipError_t runs_carry_count(int64_t* out, int64_t nb, const int64_t* tails, int64_t cap, hipStream_t st);
 hipError_t runs_carry_tails(const RcExt& X, int64_t ext_n, int64_t n, const int64_t* nseg, const int64_t* seg_start,
                             const int32_t* key, const int64_t* toff, const int32_t* end_of, unsigned long long* tstart,
                             int64_t* newlen, int64_t* noff, int64_t* new_total, int64_t* scan_tmp, int64_t* top,

@@ -481,6 +481,7 @@ __global__ void rc_build_new(RcExt X, int64_t n, const int64_t* __restrict__ seg
   if (i >= n) return;
   const int64_t sg = seg_idx[i] + seg_flag[i] - 1;
   const int64_t e = i + toff[sg] + tlen[sg];
+  if (e >= X.cap) return;                          // (only a batch the key check rejects gets here)
   X.key[e] = B.key[i];
   X.topic[e] = B.topic ? B.topic[i] : 0;
   X.partition[e] = B.partition ? B.partition[i] : 0;
@@ -504,7 +505,7 @@ __global__ void rc_build_tail(RcExt X, int64_t nmax, const int64_t* __restrict__
   const int32_t k = key[seg_start[sg]];
   const int64_t* src = rpool + rtab[2 * int64_t(k)] * RW;
   const int64_t e0 = seg_start[sg] + toff[sg];
-  for (int64_t t = 0; t < T; t++, src += RW) {
+  for (int64_t t = 0; t < T && e0 + t < X.cap; t++, src += RW) {
     const int64_t e = e0 + t;
     X.pos[e] = src[0];
     X.offset[e] = src[1];
@@ -577,8 +578,11 @@ __global__ void rc_tail_write(RcExt X, int64_t nrec, const int64_t* __restrict__
 __global__ void rc_top_add(int64_t* __restrict__ top, const int64_t* __restrict__ add, const int64_t* __restrict__ bad) {
   if (!*bad) *top += *add;
 }
-// *out = a + *b (the extended batch's record count on the device)
-__global__ void rc_count(int64_t* __restrict__ out, int64_t a, const int64_t* __restrict__ b) { *out = a + *b; }
+// *out = min(a + *b, cap) (the extended batch's record count on the device; over cap only for a batch
+// with a key in two segments, which the key check rejects)
+__global__ void rc_count(int64_t* __restrict__ out, int64_t a, const int64_t* __restrict__ b, int64_t cap) {
+  *out = a + *b < cap ? a + *b : cap;
+}
 
 // compaction of the tail pool: every key's tail copied to `dst` at the exclusive prefix of the lengths
 __global__ void rc_gc_len(const int64_t* __restrict__ rtab, int64_t nkeys, int64_t* __restrict__ len) {
@@ -745,9 +749,9 @@ hipError_t runs_carry_tails(const RcExt& X, int64_t ext_n, int64_t n, const int6
   return hipGetLastError();
 }
 
-// *out = nb + *tails: the extended batch's records, for the launches sized by a bound
-hipError_t runs_carry_count(int64_t* out, int64_t nb, const int64_t* tails, hipStream_t st) {
-  hipLaunchKernelGGL(rc_count, dim3(1), dim3(1), 0, st, out, nb, tails);
+// *out = min(nb + *tails, cap): the extended batch's records, for the launches sized by a bound (cap)
+hipError_t runs_carry_count(int64_t* out, int64_t nb, const int64_t* tails, int64_t cap, hipStream_t st) {
+  hipLaunchKernelGGL(rc_count, dim3(1), dim3(1), 0, st, out, nb, tails, cap);
   return hipGetLastError();
 }
 

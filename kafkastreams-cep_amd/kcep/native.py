@@ -76,7 +76,8 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_batch_errors", "cep_session_set_timing",
            "cep_key_profile", "cep_key_hash", "cep_key_shard", "cep_shard_plan", "cep_partition", "cep_gather",
            "cep_match_count_to", "cep_state_evict", "cep_state_import_keys", "cep_state_positions",
-           "cep_session_set_max_key_words", "cep_state_to_reference", "cep_pattern_check"]
+           "cep_session_set_max_key_words", "cep_state_to_reference", "cep_pattern_check", "cep_batch_attempts",
+           "cep_csr_check"]
 
 _lib = None
 
@@ -125,6 +126,8 @@ def lib():
     L.cep_stream_position.restype = C.c_int64
     L.cep_session_jit.argtypes = [P]
     L.cep_session_wave.argtypes = [P]
+    L.cep_batch_attempts.argtypes = [P]
+    L.cep_csr_check.argtypes = [C.POINTER(Matches), C.c_int64, C.c_int32]
     L.cep_live_run_hwm.argtypes = [P, C.POINTER(C.c_int64)]
     L.cep_session_set_timing.argtypes = [P, C.c_int32]
     L.cep_batch_errors.argtypes = [P, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
@@ -311,6 +314,10 @@ class Session:
         v = C.c_int64()
         check(lib().cep_live_run_hwm(self.h, C.byref(v)))
         return v.value
+
+    def attempts(self) -> int:
+        """General path: kernel attempts of the last batch (1 + pool regrowth re-runs; 0: other path)."""
+        return int(lib().cep_batch_attempts(self.h))
 
     def set_timing(self, on: bool):
         """cep_session_set_timing: per-batch HIP event timing on/off."""

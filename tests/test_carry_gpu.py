@@ -437,6 +437,45 @@ def test_runs_carry_rejected_batch_leaves_tails(bad):
     assert got == [(m[0], m[1]) for m in want]
 
 
+def test_runs_carry_duplicate_key_with_a_long_tail_is_bounded():
+    """a runs carry batch is launched on a bound of its extended size (the batch plus
+    every tail record the pool holds) before its key check is read.  A batch holding key 0 in two
+    segments gives key 0's tail to both, which can exceed that bound when key 0's tail is more than half
+    of the live tails -- here right after the first batch (no garbage in the pool yet: the bound is the
+    live tails exactly) with key 0 holding almost all of them.  The writes past the bound are dropped on
+    the device, the batch fails with CEP_E_ARG, and the stream then continues as the oracle's without it."""
+    ir = PL.c3_stock().to_ir(PL.I32)
+    n0 = 600
+    key = np.concatenate([np.zeros(n0, np.int32), np.ones(4, np.int32)])
+    val = np.concatenate([100 + np.arange(n0), [100, 101, 102, 103]]).astype(np.int32)   # key 0: one long open run
+    tail_k = np.concatenate([np.zeros(3, np.int32), np.ones(2, np.int32)])
+    tail_v = np.array([90, 80, 70, 200, 50], np.int32)                                  # closes / continues the runs
+    want, _, oerr = oracle_run(ir, np.concatenate([key, tail_k]), [np.concatenate([val, tail_v])], [1],
+                               O.MODE_PROCESSOR)
+    s = N.Session(N.CompiledPattern(ir), 2 * n0, carry=True, max_keys=4)
+    assert s.path == N.PATH_RUNS
+    s.push(len(key), key, [val], flags=N.BATCH_OFFSETS_MONOTONE)
+    got = s.collect()
+    got = [(int(got["match_record"][m]), int(got["match_key"][m])) for m in range(len(got["match_record"]))]
+    blob = s.state_export()
+    assert len(NN_state_positions(blob)) >= n0 - 1          # key 0 carries (nearly) its whole segment
+    for _ in range(3):
+        with pytest.raises(N.CepError) as e:
+            s.push(5, np.array([0, 0, 1, 0, 0], np.int32), [np.array([5, 6, 7, 8, 9], np.int32)],
+                   flags=N.BATCH_OFFSETS_MONOTONE)
+        assert e.value.code == 11
+    s.push(len(tail_k), tail_k, [tail_v], flags=N.BATCH_OFFSETS_MONOTONE)
+    out = s.collect()
+    got += [(int(out["match_record"][m]), int(out["match_key"][m])) for m in range(len(out["match_record"]))]
+    assert oerr is None and len(want) > 0
+    assert got == [(m[0], m[1]) for m in want]
+
+
+def NN_state_positions(blob):
+    from kcep import native as NN
+    return NN.state_positions(blob)
+
+
 def test_runs_carry_rejects_unclean_batches():
     """Like the stencil carry: null records or unflagged offsets cannot be taken by the runs kernels
     (the host applies CEPProcessor's filters first)."""

@@ -300,9 +300,10 @@ def test_wave_scratch_regions(name, mk, vmax, gen, scratch, monkeypatch):
 
 
 def test_pool_regrowth_is_bounded_and_given_back(monkeypatch):
-    """The general path's workspace pool (ADVICE r4): a batch that overflows it is re-run on a larger
-    pool, and the pool goes back to its usual size after the batch, so one heavy batch does not hold
-    the device for the session's lifetime; with a budget (cep_opts.max_pool_bytes) the pool stops
+    """The general path's workspace pool (ADVICE r4, r5): a batch that overflows it is re-run on a larger
+    pool; the next batches start from the grown size (one attempt each, no re-run per batch), and after
+    4 batches in a row that fit the estimate the grown pool is given back, so one heavy stretch does not
+    hold the device for the session's lifetime; with a budget (cep_opts.max_pool_bytes) the pool stops
     growing there and the keys still out of room are handed back per key (CEP_E_RUN_CAPACITY) while
     every other key completes as the oracle's."""
     import torch
@@ -312,18 +313,32 @@ def test_pool_regrowth_is_bounded_and_given_back(monkeypatch):
     ir = synth.c4_pattern().to_ir(PL.I32)
     want = oracle_matches(ir, key, [val], [1], O.MODE_PROCESSOR)
     s = N.Session(N.CompiledPattern(ir), 2 * len(key), force_path=N.PATH_GENERAL, lane_nfa=False)
-    s.push(len(key), key, [val])                           # ~2.1 M pool words: over the first estimate
-    assert product_matches(s, s.collect()) == want
+    light_k, light_v = key[key < 8], val[key < 8]
+    light_want = oracle_matches(ir, light_k, [light_v], [1], O.MODE_PROCESSOR)
+    s.push(len(light_k), light_k, [light_v])
+    assert s.attempts() == 1 and product_matches(s, s.collect()) == light_want
     torch.cuda.synchronize()
     free0 = torch.cuda.mem_get_info()[0]
-    heavy = np.concatenate([key, key + 400])               # twice the keys: the pool overflows
+    s.push(len(key), key, [val])                           # ~2.1 M pool words: over the first estimate
+    assert s.attempts() > 1
+    assert product_matches(s, s.collect()) == want
+    heavy = np.concatenate([key, key + 400])               # twice the keys: the pool overflows again
     hval = np.concatenate([val, val])
     s.push(len(heavy), heavy, [hval])
+    assert s.attempts() > 1
     got = product_matches(s, s.collect())
-    torch.cuda.synchronize()
-    free1 = torch.cuda.mem_get_info()[0]
     assert len(got) == 2 * len(want)
-    assert free1 >= free0 - (64 << 20)                     # the regrown pool was given back
+    for _ in range(2):                                     # the same workload again: the learned size, one attempt
+        s.push(len(heavy), heavy, [hval])
+        assert s.attempts() == 1
+        assert product_matches(s, s.collect()) == got
+    for i in range(4):                                     # light batches: the grown pool goes back after the 4th
+        s.push(len(light_k), light_k, [light_v])
+        assert s.attempts() == 1 and product_matches(s, s.collect()) == light_want
+        torch.cuda.synchronize()
+        if i < 3:
+            assert torch.cuda.mem_get_info()[0] < free0 - (8 << 20)   # still held
+    assert torch.cuda.mem_get_info()[0] >= free0 - (64 << 20)          # given back
     # a second session on the same device, with a pool budget the batch cannot fit in (longer keys:
     # their workspace outgrows the first pool estimate, which is linear in the records)
     heavy, hval, _ = synth.c4_stream_np(800, L=19)

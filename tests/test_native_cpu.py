@@ -203,3 +203,31 @@ def test_state_to_reference_host_only():
         bad[-6] = t
         with pytest.raises(N.CepError):
             cs.state_to_reference(_kcst(bad))
+
+
+def test_csr_check_rejects_corrupt_csr():
+    """cep_csr_check: the host walk of a device-written CSR is guarded -- a CSR with
+    decreasing offsets, offsets not ending at n_entries, or a record / stage name out of range fails
+    with CEP_E_HIP (the reference fails the task with an exception, never a crash)."""
+    import ctypes as C
+    import numpy as np
+
+    def check(mrec, eoff, ename, erec, n_records=10, n_names=4):
+        mrec, eoff = np.asarray(mrec, np.int64), np.asarray(eoff, np.int64)
+        ename, erec = np.asarray(ename, np.int32), np.asarray(erec, np.int64)
+        key = np.zeros(len(mrec), np.int32)
+        m = N.Matches(len(mrec), len(erec), mrec.ctypes.data_as(C.POINTER(C.c_int64)),
+                      key.ctypes.data_as(C.POINTER(C.c_int32)), eoff.ctypes.data_as(C.POINTER(C.c_int64)),
+                      ename.ctypes.data_as(C.POINTER(C.c_int32)), erec.ctypes.data_as(C.POINTER(C.c_int64)),
+                      2, 0, -1)
+        return N.lib().cep_csr_check(C.byref(m), n_records, n_names)
+
+    assert check([2, 5], [0, 2, 3], [1, 2, 1], [2, 1, 5]) == 0
+    assert check([], [0], [], []) == 0
+    assert check([2, 5], [0, 3, 2], [1, 2, 1], [2, 1, 5]) == 10        # offsets decrease
+    assert check([2, 5], [1, 2, 3], [1, 2, 1], [2, 1, 5]) == 10        # does not start at 0
+    assert check([2, 5], [0, 2, 2], [1, 2, 1], [2, 1, 5]) == 10        # does not end at n_entries
+    assert check([2, 11], [0, 2, 3], [1, 2, 1], [2, 1, 5]) == 10       # match record past the batch
+    assert check([2, 5], [0, 2, 3], [1, 2, 1], [2, -7, 5]) == 10       # entry record negative
+    assert check([2, 5], [0, 2, 3], [1, 4, 1], [2, 1, 5]) == 10        # stage name id past the names
+    assert "inconsistent" in N.lib().cep_last_error().decode()
