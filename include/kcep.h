@@ -140,9 +140,17 @@ typedef struct {
 #define CEP_BATCH_DELIVER 2           /* the caller collects this batch (a processor flush): on stencil / chain
                                          carry sessions the device hands the matches to pinned host memory as
                                          part of the push, so cep_collect only waits (one host round trip) */
+#define CEP_BATCH_ARRIVAL_ORDER 4     /* CEP_SESSION_CARRY sessions: the records are in arrival order, as
+                                         CEPProcessor.process sees them one by one (CEPProcessor.java:134-150),
+                                         not grouped by key.  The library groups them by key on the device (a
+                                         stable sort), record positions are arrival positions (stream position =
+                                         records pushed before + arrival index), and cep_collect returns the
+                                         matches in arrival order of their completing record -- per record in
+                                         matchPattern's emission order: the order context.forward sends them
+                                         (:148) -- with cep_batch_errors in ascending position.  No host sort */
 
 /* One batch of records, struct-of-arrays, grouped by key (each key's records
- * contiguous and in arrival order).  Replaces a sequence of
+ * contiguous and in arrival order; or in plain arrival order with CEP_BATCH_ARRIVAL_ORDER).  Replaces a sequence of
  * CEPProcessor.process(key, value) calls; the per-record Event fields of
  * Event.java:27-123 map to key_id/topic/partition/offset/ts, the value's typed
  * fields to cols.  Optional arrays may be NULL: valid -> all records valid,

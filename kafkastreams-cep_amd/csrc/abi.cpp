@@ -243,6 +243,13 @@ struct cep_session {
   int64_t rpool_cap = 0, rpool_used = 0;   // tail records (5 + ncols int64 words each)
   int64_t* h_res = nullptr;                // runs / general paths: the batch's counts, written by the device into
                                            // pinned memory (16 words)
+  // ---- CEP_BATCH_ARRIVAL_ORDER (group.hip): the batch grouped by key on the device ----
+  DBuf g_key, g_arr, g_pos, g_valid, g_topic, g_part, g_off, g_ts, g_head, g_top, g_nodes, g_lt, g_start, g_tmp, a_cnt,
+      a_ecnt, a_head, a_moff, a_moffe, a_tmp, a_record, a_key, a_entoff, a_name, a_entrec;
+  uint32_t group_stamp = 0;                // the groupings so far (epoch of the per-key list heads)
+  DBuf g_cols[16];
+  const int64_t* cur_pos = nullptr;        // the batch being pushed: stream position per grouped record (else null)
+  const int64_t* last_gpos = nullptr;      // ... of the last stencil / chain batch (carry_args)
   bool collected = false;                  // the CSR above is the last batch's: a second collect re-uses it
   cep_matches last{};
   std::vector<uint8_t> evict_buf;          // cep_state_evict's blobs
@@ -291,7 +298,7 @@ bool getenv_flag_off(const char* name) {
 StencilCarry carry_args(const cep_session* s) {
   return StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), s->pat->prog.stencil.k - 1, s->halo_stamp,
                       int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->halo_base,
-                      s->hflags.as<unsigned long long>() + (s->halo_stamp & 1)};
+                      s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), s->last_gpos};
 }
 
 // Host-resident batch columns -> one packed device image (s->dstage), 256-B aligned per column.  The
@@ -440,7 +447,8 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     L.clear_flag = s->hflags.as<unsigned long long>() + (s->halo_stamp & 1);
     L.carry = StencilCarry{s->halo.as<HaloHdr>(), s->hpos.as<int64_t>(), SP.k - 1, ++s->halo_stamp,
                            int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)), s->base,
-                           s->hflags.as<unsigned long long>() + (s->halo_stamp & 1)};
+                           s->hflags.as<unsigned long long>() + (s->halo_stamp & 1), s->cur_pos};
+    s->last_gpos = s->cur_pos;
     s->halo_base = s->base;
     s->base += b->n;
   }
@@ -464,6 +472,16 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     L.deliver.host_cap = s->dl_cap;
     L.deliver.ticket = s->dl_ticket.as<unsigned>();
     L.deliver.stamp = ++s->dl_stamp;
+    if (s->cur_pos && b->n > 0) {                  // arrival order: rows delivered by their completing record's arrival
+      if (s->a_moff.ensure(size_t(b->n) * 8) || s->a_tmp.ensure(size_t(b->n / 1024 + 4) * 8) || s->scal.ensure(64))
+        return fail(CEP_E_HIP, "allocation failed");
+      L.deliver.a_cnt = s->a_cnt.as<int64_t>();
+      L.deliver.a_head = s->a_head.as<int32_t>();
+      L.deliver.a_moff = s->a_moff.as<int64_t>();
+      L.deliver.a_tot = s->scal.as<int64_t>() + 6;
+      L.deliver.a_tmp = s->a_tmp.as<int64_t>();
+      L.deliver.a_n = b->n;
+    }
     s->delivered = true;
   }
   HIPCHECK(stencil_launch(L, s->timing ? s->ev0 : nullptr, s->timing ? s->ev1 : nullptr, st));
@@ -598,6 +616,7 @@ int push_runs(cep_session* s, const cep_batch* b, hipStream_t st) {
     HIPCHECK(carry_keycheck_launch(nb, scal, in.key, s->seg.as<int64_t>(), int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX)),
                                    s->kstamp.as<int32_t>(), ++s->batch_no, reinterpret_cast<unsigned long long*>(scal + 1), st));
     RcIn B{};
+    B.pos = s->cur_pos;
     B.key = in.key; B.topic = in.topic; B.partition = in.partition; B.offset = in.offset; B.ts = in.ts;
     for (int c = 0; c < 16; c++) B.cols[c] = in.cols[c];
     const int32_t mk = int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX));
@@ -843,6 +862,7 @@ int push_general(cep_session* s, const cep_batch* b, hipStream_t st) {
   s->g_matches = s->g_entries = 0;
   s->nseg = 0;
   A.base = s->carry ? s->base : 0;
+  A.pos = s->cur_pos;
   if (n == 0) {                                   // cep_device_match_count reads scal[3]: zero it
     if (s->scal.ensure(64)) return fail(CEP_E_HIP, "allocation failed");
     HIPCHECK(hipMemsetAsync(s->scal.as<int64_t>() + 3, 0, 16, st));
@@ -1287,6 +1307,11 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 
 void cep_session_close(cep_session* s) {
   if (!s) return;
+  for (DBuf* b : {&s->g_key, &s->g_arr, &s->g_pos, &s->g_valid, &s->g_topic, &s->g_part, &s->g_off, &s->g_ts, &s->g_head,
+                  &s->g_top, &s->g_nodes, &s->g_lt, &s->g_start, &s->g_tmp, &s->a_cnt, &s->a_ecnt, &s->a_head, &s->a_moff,
+                  &s->a_moffe, &s->a_tmp, &s->a_record, &s->a_key, &s->a_entoff, &s->a_name, &s->a_entrec})
+    b->release();
+  for (auto& c : s->g_cols) c.release();
   for (DBuf* b : {&s->prog, &s->out, &s->status, &s->counter, &s->total, &s->sum, &s->mkey, &s->slots, &s->wscratch, &s->dstage, &s->dl_ticket,
                   &s->h_topic, &s->dprog, &s->flag, &s->idx, &s->seg, &s->scan_tmp,
                   &s->scal, &s->ctl, &s->pool, &s->r_matches, &s->r_words, &s->r_out, &s->r_err, &s->r_errrec,
@@ -1390,6 +1415,119 @@ int cep_pattern_build_kernels(const cep_pattern* p, int path) {
 
 static int push_dispatch(cep_session* s, const cep_batch* b, hipStream_t st, bool stencil_batch);
 
+// CEP_BATCH_ARRIVAL_ORDER: the batch (records in arrival order, host or device) grouped by key on the device
+// (group.hip) into the session's grouped columns; gb describes them (device memory, flags without
+// CEP_BATCH_ARRIVAL_ORDER, CEP_BATCH_DELIVER added for the stencil / chain paths, whose rows the delivery
+// then writes in arrival order); s->cur_pos = every grouped record's stream position (base + arrival index)
+static int group_batch(cep_session* s, const cep_batch* b, hipStream_t st, cep_batch& gb, const void** gcols) {
+  const Program& P = s->pat->prog;
+  const int64_t n = b->n;
+  NfaArgs in{};                                    // the batch's columns on the device (host ones staged)
+  in.key = b->key_id; in.valid = b->valid; in.topic = b->topic; in.partition = b->partition;
+  in.offset = b->offset; in.ts = b->ts;
+  for (int c = 0; c < b->n_cols; c++) in.cols[c] = b->cols[c];
+  if (b->mem == CEP_MEM_HOST) {
+    HostArr arrs[6 + 16] = {{in.key, size_t(n) * 4, reinterpret_cast<const void**>(&in.key)},
+                            {in.valid, size_t(n), reinterpret_cast<const void**>(&in.valid)},
+                            {in.topic, size_t(n) * 4, reinterpret_cast<const void**>(&in.topic)},
+                            {in.partition, size_t(n) * 4, reinterpret_cast<const void**>(&in.partition)},
+                            {in.offset, size_t(n) * 8, reinterpret_cast<const void**>(&in.offset)},
+                            {in.ts, size_t(n) * 8, reinterpret_cast<const void**>(&in.ts)}};
+    for (int c = 0; c < b->n_cols; c++)
+      arrs[6 + c] = HostArr{in.cols[c], size_t(n) * type_size(P.coltypes[c]), &in.cols[c]};
+    // small batches are read over the link in place (one pass: the sort's keys, then the gather)
+    int rc = stage_host(s, arrs, 6 + b->n_cols, st, true);
+    if (rc) return rc;
+  }
+  const size_t n4 = size_t(n) * 4, n8 = size_t(n) * 8;
+  const size_t heads = size_t(s->opts.max_keys + 1) * 8;
+  if (!s->g_head.p || !s->g_top.p) {               // epoch-tagged list heads and the node counter: zeroed once
+    if (s->g_head.ensure(heads) || s->g_top.ensure(16) || hipMemsetAsync(s->g_head.p, 0, heads, st) ||
+        hipMemsetAsync(s->g_top.p, 0, 16, st))
+      return fail(CEP_E_HIP, "allocation failed");
+  }
+  if (s->g_key.ensure(n4) || s->g_arr.ensure(n4) || s->g_pos.ensure(n8) || s->g_nodes.ensure(8 * n4) ||
+      s->g_lt.ensure(n8) || s->g_start.ensure(n8) || s->g_tmp.ensure(size_t(n / 1024 + 4) * 8) || s->scal.ensure(64) ||
+      s->a_cnt.ensure(n8) || s->a_ecnt.ensure(n8) || s->a_head.ensure(n4) || (in.valid && s->g_valid.ensure(size_t(n))) ||
+      (in.topic && s->g_topic.ensure(n4)) || (in.partition && s->g_part.ensure(n4)) || (in.offset && s->g_off.ensure(n8)) ||
+      (in.ts && s->g_ts.ensure(n8)))
+    return fail(CEP_E_HIP, "allocation failed");
+  GroupArgs G{};
+  G.max_keys = int32_t(std::min<int64_t>(s->opts.max_keys, INT32_MAX - 1));
+  G.stamp = ++s->group_stamp;
+  G.head = s->g_head.as<unsigned long long>();
+  G.node_top = s->g_top.as<int32_t>();
+  int32_t* nodes = s->g_nodes.as<int32_t>();
+  G.node_key = nodes; G.node_chunk = nodes + n; G.node_cnt = nodes + 2 * n; G.node_next = nodes + 3 * n;
+  G.node_prefix = nodes + 4 * n; G.node_leader = nodes + 5 * n; G.rec_node = nodes + 6 * n; G.rec_rank = nodes + 7 * n;
+  G.lt = s->g_lt.as<int64_t>(); G.start = s->g_start.as<int64_t>(); G.start_tot = s->g_top.as<int64_t>() + 1;
+  G.scan_tmp = s->g_tmp.as<int64_t>();
+  G.key = in.key; G.g_key = s->g_key.as<int32_t>(); G.arr = s->g_arr.as<int32_t>(); G.pos = s->g_pos.as<int64_t>();
+  G.base = s->base;
+  G.valid = in.valid; G.g_valid = in.valid ? s->g_valid.as<uint8_t>() : nullptr;
+  G.topic = in.topic; G.g_topic = in.topic ? s->g_topic.as<int32_t>() : nullptr;
+  G.partition = in.partition; G.g_partition = in.partition ? s->g_part.as<int32_t>() : nullptr;
+  G.offset = in.offset; G.g_offset = in.offset ? s->g_off.as<int64_t>() : nullptr;
+  G.ts = in.ts; G.g_ts = in.ts ? s->g_ts.as<int64_t>() : nullptr;
+  G.ncols = b->n_cols;
+  for (int c = 0; c < b->n_cols; c++) {
+    if (s->g_cols[c].ensure(size_t(n) * type_size(P.coltypes[c]))) return fail(CEP_E_HIP, "allocation failed");
+    G.cols[c] = in.cols[c];
+    G.g_cols[c] = s->g_cols[c].p;
+    G.coltype[c] = P.coltypes[c];
+    gcols[c] = s->g_cols[c].p;
+  }
+  G.cnt = s->a_cnt.as<int64_t>();
+  G.ecnt = s->a_ecnt.as<int64_t>();
+  HIPCHECK(group_launch(G, n, st));
+  gb = *b;
+  gb.key_id = G.g_key; gb.valid = G.g_valid; gb.topic = G.g_topic; gb.partition = G.g_partition;
+  gb.offset = G.g_offset; gb.ts = G.g_ts;
+  gb.cols = gcols;
+  gb.mem = CEP_MEM_DEVICE;
+  gb.flags = (b->flags & ~uint32_t(CEP_BATCH_ARRIVAL_ORDER)) | CEP_BATCH_DELIVER;
+  s->cur_pos = G.pos;
+  return CEP_OK;
+}
+
+// the general / runs CSR of an arrival-order batch into arrival order of the completing record (group.hip);
+// base: the batch's first stream position
+static int arrival_csr(cep_session* s, int64_t base, int64_t n, hipStream_t st) {
+  if (!s->e_rec.empty()) {                         // exceptions: ascending position, the first one reported
+    std::vector<std::pair<int64_t, int32_t>> e;
+    for (size_t i = 0; i < s->e_rec.size(); i++) e.emplace_back(s->e_rec[i], s->e_code[i]);
+    std::sort(e.begin(), e.end());
+    for (size_t i = 0; i < e.size(); i++) {
+      s->e_rec[i] = e[i].first;
+      s->e_code[i] = e[i].second;
+    }
+    s->g_err_rec = e[0].first;
+    s->g_err = e[0].second;
+  }
+  const int64_t nm = s->g_matches, ne = s->g_entries;
+  if (nm <= 0) return CEP_OK;
+  const size_t hm = size_t(nm + nm / 4 + 256), he = size_t(ne + ne / 4 + 256);
+  if ((s->a_record.cap < size_t(nm) * 8 && s->a_record.ensure(hm * 8)) ||
+      (s->a_key.cap < size_t(nm) * 4 && s->a_key.ensure(hm * 4)) ||
+      (s->a_entoff.cap < size_t(nm) * 8 && s->a_entoff.ensure(hm * 8)) ||
+      (s->a_name.cap < size_t(ne) * 4 && s->a_name.ensure(he * 4)) ||
+      (s->a_entrec.cap < size_t(ne) * 8 && s->a_entrec.ensure(he * 8)) || s->a_moff.ensure(size_t(n) * 8) ||
+      s->a_moffe.ensure(size_t(n) * 8) || s->a_tmp.ensure(size_t(n / 1024 + 4) * 16) || s->scal.ensure(64))
+    return fail(CEP_E_HIP, "allocation failed");
+  HIPCHECK(arrival_reorder(s->o_record.as<int64_t>(), s->o_key.as<int32_t>(), s->o_entoff.as<int64_t>(),
+                           s->o_name.as<int32_t>(), s->o_entrec.as<int64_t>(), nm, ne, base, n, s->a_cnt.as<int64_t>(),
+                           s->a_ecnt.as<int64_t>(), s->a_head.as<int32_t>(), s->a_moff.as<int64_t>(),
+                           s->a_moffe.as<int64_t>(), s->scal.as<int64_t>() + 6, s->a_tmp.as<int64_t>(),
+                           s->a_record.as<int64_t>(), s->a_key.as<int32_t>(), s->a_entoff.as<int64_t>(),
+                           s->a_name.as<int32_t>(), s->a_entrec.as<int64_t>(), st));
+  std::swap(s->o_record, s->a_record);
+  std::swap(s->o_key, s->a_key);
+  std::swap(s->o_entoff, s->a_entoff);
+  std::swap(s->o_name, s->a_name);
+  std::swap(s->o_entrec, s->a_entrec);
+  return CEP_OK;
+}
+
 int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   if (!s || !b) return fail(CEP_E_ARG, "null argument");
   static const char* const kRange[] = {"cep_push_batch", "cep_push_batch:stencil", "cep_push_batch:general",
@@ -1417,7 +1555,23 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   s->h2d_wait = false;
   s->delivered = false;
   s->zc_slot = -1;
-  int rc = push_dispatch(s, b, st, stencil_batch);
+  s->cur_pos = nullptr;
+  s->last_gpos = nullptr;
+  int rc = CEP_OK;
+  const bool arrival = (b->flags & CEP_BATCH_ARRIVAL_ORDER) && b->n > 0;
+  if ((b->flags & CEP_BATCH_ARRIVAL_ORDER) && !s->carry)
+    return fail(CEP_E_UNSUPPORTED, "CEP_BATCH_ARRIVAL_ORDER needs a CEP_SESSION_CARRY session");
+  cep_batch gb;
+  const void* gcols[16] = {};
+  const int64_t base0 = s->base;
+  if (arrival) {
+    rc = group_batch(s, b, st, gb, gcols);
+    if (!rc) rc = push_dispatch(s, &gb, st, stencil_batch);
+    if (!rc && (s->last_path == CEP_PATH_GENERAL || s->last_path == CEP_PATH_RUNS)) rc = arrival_csr(s, base0, b->n, st);
+    s->cur_pos = nullptr;
+  } else {
+    rc = push_dispatch(s, b, st, stencil_batch);
+  }
   if (s->zc_slot >= 0) {                           // the ring slot is free again once the kernels are done
     HIPCHECK(hipEventRecord(s->ring_ev[s->zc_slot], st));
     s->zc_slot = -1;

@@ -165,7 +165,11 @@ struct NfaArgs {
   int64_t scratch_words;          // ... of this many words (0: none)
   int64_t max_key_words;          // per-key workspace cap in words (0 = none): over it, CEP_E_RUN_CAPACITY
   unsigned long long* err_any;    // set when any key reports an exception (the host reads res_err only then)
+  const int64_t* pos;             // stream position of each batch record (CEP_BATCH_ARRIVAL_ORDER: base + its
+                                  // arrival index); null: base + record index
 };
+// a batch record's stream position (emitted entries, carried events, exception records)
+__device__ __forceinline__ int64_t a_pos(const NfaArgs& A, int64_t g) { return A.pos ? A.pos[g] : A.base + g; }
 
 // deterministic-runs path (runs.hip)
 struct RunsArgs {

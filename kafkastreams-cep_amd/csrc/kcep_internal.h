@@ -145,7 +145,10 @@ struct StencilCarry {
   int64_t base;                      // stream position of batch record 0
   unsigned long long* flags;         // bit 0: key id out of range, bit 1: a key in two segments,
                                      // bit 2: chain carry batch beyond a tile's match space
+  const int64_t* gpos;               // stream position of each batch record (CEP_BATCH_ARRIVAL_ORDER: base + its
+                                     // arrival index); null: base + record index
 };
+KCEP_HD inline int64_t halo_gpos(const StencilCarry& C, int64_t r) { return C.gpos ? C.gpos[r] : C.base + r; }
 KCEP_HD inline int halo_old(const HaloHdr& h, int32_t stamp) {
   // the newer slot written before batch `stamp` (or an empty one)
   const int32_t a = h.stamp[0] < stamp ? h.stamp[0] : -1, b = h.stamp[1] < stamp ? h.stamp[1] : -1;
@@ -163,7 +166,49 @@ struct DeliverArgs {
   int64_t host_cap = 0;
   unsigned* ticket = nullptr;     // device: workgroups done (the last one stamps hdr[2] = stamp; reset to 0)
   int64_t stamp = 0;              // this delivery's number: cep_collect spins until hdr[2] holds it
+  // CEP_BATCH_ARRIVAL_ORDER (group.hip): the rows delivered in arrival order of their completing record --
+  // per arrival record its matches (a_cnt, zeroed by group_gather), their prefix (a_moff), its first match
+  int64_t* a_cnt = nullptr;       // null: grouped order
+  int32_t* a_head = nullptr;
+  int64_t* a_moff = nullptr;
+  int64_t* a_tot = nullptr;
+  int64_t* a_tmp = nullptr;       // the scan's scratch
+  int64_t a_n = 0;                // the batch's records
 };
+// CEP_BATCH_ARRIVAL_ORDER: an arrival-order batch grouped by key (group.hip)
+struct GroupArgs {
+  const int32_t* key;             // in: arrival order
+  int32_t* g_key;                 // out: grouped (stable by key id)
+  int32_t* arr;                   // out: arrival index of each grouped record
+  int64_t* pos;                   // out: its stream position, base + arrival index
+  int64_t base;
+  const uint8_t* valid; uint8_t* g_valid;
+  const int32_t* topic; int32_t* g_topic;
+  const int32_t* partition; int32_t* g_partition;
+  const int64_t* offset; int64_t* g_offset;
+  const int64_t* ts; int64_t* g_ts;
+  const void* cols[16]; void* g_cols[16];
+  int32_t coltype[16];
+  int32_t ncols;
+  int64_t* cnt;                   // zeroed (n): the reorder's per-record match / entry counts
+  int64_t* ecnt;
+  // the grouping's state and scratch (group.hip)
+  int32_t max_keys;
+  uint32_t stamp;                 // this grouping's number (>= 1)
+  unsigned long long* head;       // max_keys + 1 epoch-tagged list heads
+  int32_t* node_top;
+  int32_t *node_key, *node_chunk, *node_cnt, *node_next, *node_prefix, *node_leader, *rec_node, *rec_rank;
+  int64_t *lt, *start, *start_tot, *scan_tmp;
+};
+hipError_t group_launch(const GroupArgs& G, int64_t n, hipStream_t st);
+hipError_t arrival_reorder(const int64_t* mrec, const int32_t* mkey, const int64_t* eoff, const int32_t* ename,
+                           const int64_t* erec, int64_t nm, int64_t ne, int64_t base, int64_t n, int64_t* cnt,
+                           int64_t* ecnt, int32_t* head, int64_t* moff, int64_t* moff_e, int64_t* tot, int64_t* tmp,
+                           int64_t* o_rec, int32_t* o_key, int64_t* o_eoff, int32_t* o_name, int64_t* o_erec,
+                           hipStream_t st);
+hipError_t stencil_arrival_ranks(const int32_t* out, int k, const int64_t* total, int64_t out_cap, const int64_t* gpos,
+                                 int64_t base, int64_t n, int64_t* cnt, int32_t* head, int64_t* moff, int64_t* tot,
+                                 int64_t* tmp, hipStream_t st);
 // The plain stencil kernel without carry stores a super-tile's first ST_DENSE matches (one int each)
 // in a dense region at the head of the slot buffer (super-tile t at t * ST_DENSE) and the rest in
 // the super-tile's own region after it (nsuper * ST_DENSE + t * sub * 4096 + m): the dense runs sit
@@ -208,6 +253,7 @@ int compile_ir(const uint8_t* ir, size_t len, Program& out, std::string& err);
 // ---- carried tails of the runs path (CEP_SESSION_CARRY, runs.hip) ----
 // the batch's columns as runs_carry_build reads them (device pointers; optional ones may be null)
 struct RcIn {
+  const int64_t* pos;                // stream positions of the batch's records (null: base + index)
   const int32_t* key;
   const int32_t* topic;
   const int32_t* partition;

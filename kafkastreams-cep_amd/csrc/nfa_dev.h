@@ -482,12 +482,12 @@ __device__ __forceinline__ int64_t cw64(const int32_t* p) { return int64_t(uint3
 __device__ __forceinline__ const int32_t* cev_of(const Lane& l, int e) { return l.cev + int64_t(e) * l.evw; }
 __device__ __forceinline__ int64_t gidx(const Lane& l, int e) { return l.seg0 + (e - l.C); }
 __device__ __forceinline__ int64_t ev_pos(const Lane& l, int e) {
-  return e < l.C ? cw64(cev_of(l, e)) : l.A->base + gidx(l, e);
+  return e < l.C ? cw64(cev_of(l, e)) : a_pos(*l.A, gidx(l, e));
 }
 __device__ __forceinline__ int32_t b_topic(const Lane& l, int64_t g) { return l.A->topic ? l.A->topic[g] : 0; }
 __device__ __forceinline__ int32_t b_part(const Lane& l, int64_t g) { return l.A->partition ? l.A->partition[g] : 0; }
-__device__ __forceinline__ int64_t b_off(const Lane& l, int64_t g) { return l.A->offset ? l.A->offset[g] : l.A->base + g; }
-__device__ __forceinline__ int64_t b_ts(const Lane& l, int64_t g) { return l.A->ts ? l.A->ts[g] : l.A->base + g; }
+__device__ __forceinline__ int64_t b_off(const Lane& l, int64_t g) { return l.A->offset ? l.A->offset[g] : a_pos(*l.A, g); }
+__device__ __forceinline__ int64_t b_ts(const Lane& l, int64_t g) { return l.A->ts ? l.A->ts[g] : a_pos(*l.A, g); }
 __device__ __forceinline__ int64_t b_field(const Lane& l, int col, int t, int64_t g) {
   const void* c = l.A->cols[col];
   if (t == T_I32) return static_cast<const int32_t*>(c)[g];
@@ -1005,7 +1005,7 @@ __device__ __forceinline__ bool emit_match(Lane& l, const Run& y) {
   const int cnt = buf_peek(l, r_sid(y), y.ev, y.ver, true, tmp, l.nev + 1);
   if (cnt < 0) return false;
   int32_t* o = l.out + l.out_top;
-  const int64_t pos = l.A->base + l.g;
+  const int64_t pos = a_pos(*l.A, l.g);
   o[0] = int32_t(uint32_t(uint64_t(pos)));
   o[1] = int32_t(uint32_t(uint64_t(pos) >> 32));
   o[2] = cnt;
@@ -1349,7 +1349,7 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
   if (!p || !out_at) {
     if (A.last_attempt || l.cap_hit) {                                 // handed back per key
       A.res_err[seg] = CEP_E_RUN_CAPACITY;
-      A.res_err_rec[seg] = A.base + l.seg0;
+      A.res_err_rec[seg] = a_pos(A, l.seg0);
       atomicOr(A.err_any, 1ull);                                       // the host reads res_err only then
     } else {
       atomicAdd(&A.flags[0], 1);
@@ -1372,14 +1372,14 @@ __device__ __forceinline__ bool key_begin(Lane& l, const NfaArgs& A, int seg, in
     if (!import_state(l, blob)) {
       if (l.overflow && (A.last_attempt || l.cap_hit)) {
         A.res_err[seg] = CEP_E_RUN_CAPACITY;
-        A.res_err_rec[seg] = A.base + l.seg0;
+        A.res_err_rec[seg] = a_pos(A, l.seg0);
         atomicOr(A.err_any, 1ull);
         return false;
       }
       if (l.overflow) atomicAdd(&A.flags[0], 1);
       A.res_err[seg] = l.err;
       if (l.err) {
-        A.res_err_rec[seg] = A.base + l.seg0;
+        A.res_err_rec[seg] = a_pos(A, l.seg0);
         atomicOr(A.err_any, 1ull);
       }
       return false;
@@ -1451,7 +1451,7 @@ __device__ __forceinline__ void key_end(Lane& l, const NfaArgs& A, int seg, int6
     // over capacity: the key stops at this record and is handed back (CEP_E_RUN_CAPACITY); the
     // matches of its earlier records stand, like the records before a reference exception
     A.res_err[seg] = CEP_E_RUN_CAPACITY;
-    A.res_err_rec[seg] = A.base + l.g;
+    A.res_err_rec[seg] = a_pos(A, l.g);
     l.overflow = 0;
     if (l.nmatch > l.rec_nmatch) {                                     // none of the failing record's
       l.nmatch = l.rec_nmatch;                                         // matches is emitted
@@ -1503,7 +1503,7 @@ __device__ __forceinline__ void nfa_kernel_body(const NfaArgs& A) {
     l.rec_etop = l.etop;
     l.rec_nmatch = l.nmatch;
     if (!step(l, fr)) {
-      if (l.err) err_rec = A.base + g;
+      if (l.err) err_rec = a_pos(A, g);
       break;
     }
     live_max = l.qlen > live_max ? l.qlen : live_max;

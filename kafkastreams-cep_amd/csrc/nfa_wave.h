@@ -303,7 +303,7 @@ __device__ __forceinline__ int wave_commit_parallel(Lane& l, WaveShared<GL>& w, 
 template <int GL>
 __device__ __forceinline__ bool wave_emit_matches(Lane& l, WaveShared<GL>& w, const Grp<GL>& g, int flen) {
   const int lane = g.gl;
-  const int64_t pos = l.A->base + l.g;
+  const int64_t pos = a_pos(*l.A, l.g);
   const int maxp = l.nev + 1;                                  // one node per event at most
   for (int base = 0; base < flen; base += GL) {
     const int nact = flen - base < GL ? flen - base : GL;
@@ -750,7 +750,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
       wave_sync();
       KWP_ADD(10, t_pl2);
     }
-    if (w.err) { err_rec = A.base + g; break; }
+    if (w.err) { err_rec = a_pos(A, g); break; }
     if (w.overflow) break;
     KWP_MARK(t_end);
     // swap the queues; matchConstruction (:151-158); the high-water mark on lane 0
@@ -773,7 +773,7 @@ __device__ __forceinline__ void wave_key(const NfaArgs& A, int seg, const Grp<GL
     }
     wave_sync();
     KWP_ADD(8, t_end);
-    if (w.err) { err_rec = A.base + g; break; }
+    if (w.err) { err_rec = a_pos(A, g); break; }
     live_max = w.qlen > live_max ? w.qlen : live_max;
   }
   wave_sync();

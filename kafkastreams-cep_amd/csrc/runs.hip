@@ -485,9 +485,10 @@ __global__ void rc_build_new(RcExt X, int64_t n, const int64_t* __restrict__ seg
   X.key[e] = B.key[i];
   X.topic[e] = B.topic ? B.topic[i] : 0;
   X.partition[e] = B.partition ? B.partition[i] : 0;
-  X.pos[e] = base + i;
-  X.offset[e] = B.offset ? B.offset[i] : base + i;
-  X.ts[e] = B.ts ? B.ts[i] : base + i;
+  const int64_t p = B.pos ? B.pos[i] : base + i;
+  X.pos[e] = p;
+  X.offset[e] = B.offset ? B.offset[i] : p;
+  X.ts[e] = B.ts ? B.ts[i] : p;
   X.seg[e] = int32_t(sg);
   for (int c = 0; c < X.ncols; c++) col_put(X.cols[c], X.coltype[c], e, col_bits(B.cols[c], X.coltype[c], i));
 }

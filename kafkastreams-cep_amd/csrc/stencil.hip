@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __r
       for (int s = 0; s < STENCIL_MAX_K; s++)
         if (s < k) {
           const int32_t r = row[s];
-          p[s] = r >= 0 ? C.base + r : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
+          p[s] = r >= 0 ? halo_gpos(C, r) : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
         }
       if (host) hkey[i] = kk;
       else dkey[i] = kk;
@@ -319,7 +319,7 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   const bool plain = L.plain && !L.chain && L.k <= 7;
   const SlotFormat F{L.k, plain, L.chain, L.carry.hdr != nullptr, plain && !L.carry.hdr && ST_PLAIN_STAGE,
                      !plain && !L.carry.hdr && ST_KEYED_DENSE, nsuper, sub};
-  if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr) {   // a small carry flush: scan, rows and delivery at once
+  if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr && !D.a_moff) {   // a small carry flush: scan, rows and delivery at once
     hipLaunchKernelGGL(stencil_finish_deliver, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, nsuper,
                        L.k, L.out, L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey,
                        D.hpos, D.dkey, D.dpos, D.ticket, D.stamp);
@@ -393,7 +393,7 @@ __global__ void stencil_resolve(const int32_t* __restrict__ key, const int32_t* 
   const int64_t* hp = C.pos + (2 * int64_t(kk) + old) * C.km1;
   for (int s = 0; s < k; s++) {
     const int32_t r = out[i * k + s];
-    pos[i * k + s] = r >= 0 ? C.base + r : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
+    pos[i * k + s] = r >= 0 ? halo_gpos(C, r) : (r == -1 ? -1 : hp[h.cnt[old] - (-r - 1)]);
   }
 }
 // CEP_BATCH_DELIVER (a carry session's flush, GpuCEPProcessor): the batch's matches handed to pinned host
@@ -402,12 +402,15 @@ __global__ void stencil_resolve(const int32_t* __restrict__ key, const int32_t* 
 // so that cep_collect is one wait instead of one host round trip per post-processing step.  Matches
 // past host_cap go to the device arrays (dkey / dpos), which cep_collect copies.  The match count is
 // read on the device: the grid strides over the session's capacity.
+// CEP_BATCH_ARRIVAL_ORDER (moff != null): match i goes to moff[a] + (i - head[a]), a = the arrival index of its
+// completing record (group.hip stencil_arrival_ranks)
 __global__ __launch_bounds__(256) void stencil_deliver(const int32_t* __restrict__ key, const int32_t* __restrict__ out,
                                                        int k, const int64_t* __restrict__ total, int64_t out_cap,
                                                        StencilCarry C, int64_t host_cap, int64_t* __restrict__ hdr,
                                                        int32_t* __restrict__ hkey, int64_t* __restrict__ hpos,
                                                        int32_t* __restrict__ dkey, int64_t* __restrict__ dpos,
-                                                       unsigned* ticket, int64_t stamp) {
+                                                       unsigned* ticket, int64_t stamp, const int64_t* __restrict__ moff,
+                                                       const int32_t* __restrict__ head) {
   const int64_t t = *total, nm = t < out_cap ? t : out_cap;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     hdr[0] = t;
@@ -420,22 +423,32 @@ __global__ __launch_bounds__(256) void stencil_deliver(const int32_t* __restrict
     const HaloHdr* h = kok ? C.hdr + kk : nullptr;
     const int old = kok ? halo_old(*h, C.stamp) : 0;
     const int64_t* hp = kok ? C.pos + (2 * int64_t(kk) + old) * C.km1 : nullptr;
-    const bool host = i < host_cap;
-    int64_t* p = host ? hpos + i * k : dpos + i * k;
+    int64_t j = i;
+    if (moff) {
+      const int64_t a = C.gpos[last] - C.base;
+      j = moff[a] + (i - head[a]);
+    }
+    const bool host = j < host_cap;
+    int64_t* p = host ? hpos + j * k : dpos + j * k;
     for (int s = 0; s < k; s++) {
       const int32_t r = out[i * k + s];
-      p[s] = r >= 0 ? C.base + r : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
+      p[s] = r >= 0 ? halo_gpos(C, r) : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
     }
-    if (host) hkey[i] = kk;
-    else dkey[i] = kk;
+    if (host) hkey[j] = kk;
+    else dkey[j] = kk;
   }
   deliver_done(ticket, unsigned(gridDim.x), hdr, stamp);
 }
 hipError_t stencil_deliver_launch(const int32_t* key, const int32_t* out, int k, const int64_t* total, int64_t out_cap,
                                   const StencilCarry& C, const DeliverArgs& D, hipStream_t st) {
   const int64_t blocks = std::min<int64_t>((out_cap + 255) / 256, 1024);
+  if (D.a_moff) {                                  // arrival order: the matches' ranks first
+    hipError_t e = stencil_arrival_ranks(out, k, total, out_cap, C.gpos, C.base, D.a_n, D.a_cnt, D.a_head, D.a_moff,
+                                         D.a_tot, D.a_tmp, st);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(stencil_deliver, dim3(unsigned(std::max<int64_t>(blocks, 1))), dim3(256), 0, st, key, out, k, total,
-                     out_cap, C, D.host_cap, D.hdr, D.hkey, D.hpos, D.dkey, D.dpos, D.ticket, D.stamp);
+                     out_cap, C, D.host_cap, D.hdr, D.hkey, D.hpos, D.dkey, D.dpos, D.ticket, D.stamp, D.a_moff, D.a_head);
   return hipGetLastError();
 }
 

@@ -356,7 +356,7 @@ __device__ __forceinline__ void halo_write(const StencilCarry& C, const HaloHead
   }
   for (int t = 0; t < seg; t++, c++) {
     masks |= ((wmk >> (8 * t)) & 0xFFull) << (8 * c);
-    np[c] = C.base + gj - (seg - 1) + t;
+    np[c] = halo_gpos(C, gj - (seg - 1) + t);
   }
   h->masks[nw] = masks;
   h->cnt[nw] = uint8_t(c);

@@ -27,6 +27,7 @@ PATH_STENCIL, PATH_GENERAL, PATH_CHAIN, PATH_RUNS = 1, 2, 3, 4
 MEM_HOST, MEM_DEVICE = 0, 1
 BATCH_OFFSETS_MONOTONE = 1
 BATCH_DELIVER = 2          # the push is collected at once: matches handed to pinned host memory by the device
+BATCH_ARRIVAL_ORDER = 4    # records in arrival order: grouped by key on the device, matches back in arrival order
 SESSION_CARRY = 1
 SESSION_INTERPRET = 2
 SESSION_PROFILE = 4

@@ -447,9 +447,10 @@ def test_runs_carry_duplicate_key_with_a_long_tail_is_bounded():
     ir = PL.c3_stock().to_ir(PL.I32)
     n0 = 600
     key = np.concatenate([np.zeros(n0, np.int32), np.ones(4, np.int32)])
-    val = np.concatenate([100 + np.arange(n0), [100, 101, 102, 103]]).astype(np.int32)   # key 0: one long open run
+    # key 0: a constant price keeps every run open (avg >= v, never avg < v): its tail is its whole segment
+    val = np.concatenate([np.full(n0, 100), [100, 99, 98, 97]]).astype(np.int32)
     tail_k = np.concatenate([np.zeros(3, np.int32), np.ones(2, np.int32)])
-    tail_v = np.array([90, 80, 70, 200, 50], np.int32)                                  # closes / continues the runs
+    tail_v = np.array([200, 90, 80, 200, 50], np.int32)                                 # closes / continues the runs
     want, _, oerr = oracle_run(ir, np.concatenate([key, tail_k]), [np.concatenate([val, tail_v])], [1],
                                O.MODE_PROCESSOR)
     s = N.Session(N.CompiledPattern(ir), 2 * n0, carry=True, max_keys=4)
