@@ -414,6 +414,12 @@ def main(argv=None):
                 _carry_stream(pat, n, K, key, cols, stream, 0, n_matches, csum, value / world, reps=1, per=b,
                               host=pageable, collect=True) for b in args.processor_batch]
             del pageable
+            # the records as a Kafka partition delivers them: keys interleaved, in generation order (the C2
+            # stream's ts column is each record's arrival position); the library groups each batch on the
+            # device (CEP_BATCH_ARRIVAL_ORDER) and hands the matches back in arrival order
+            line["processor_batches"] += [
+                _arrival_batches(pat, n, K, key, cols, ts, stream, n_matches, csum, value / world, per=b, pipelined=p)
+                for b in args.processor_batch[:1] for p in (False, True)]
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS) and args.carry_batches > 1:
             line["carry_stream"] = _carry_stream(pat, n, K, key, cols, stream, args.carry_batches, n_matches, csum,
                                                  value / world)
@@ -513,6 +519,106 @@ def _carry_stream(pat, n, K, key, cols, stream, nb, n_matches, csum, resident, r
                     "overhead_us_per_batch": (dt - n / resident) * 1e6 / nbat})
     cs.close()
     return out
+
+
+def _mix64(x):
+    import numpy as np
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(33))
+        x = x * np.uint64(0xff51afd7ed558ccd)
+        x = x ^ (x >> np.uint64(33))
+        x = x * np.uint64(0xc4ceb9fe1a85ec53)
+        return x ^ (x >> np.uint64(33))
+
+
+def _csr_checksum(mrec, ent_off, ent_name, ent_rec, pos_map):
+    """cep_checksum's order-independent sum (per match: mix64 over its record and traversal entries) of a
+    host CSR, its record positions first mapped through pos_map (numpy, vectorised over matches)."""
+    import numpy as np
+    if len(mrec) == 0:
+        return 0
+    lens = np.diff(ent_off)
+    with np.errstate(over="ignore"):
+        h = _mix64(pos_map[mrec].astype(np.uint64) * np.uint64(0x9e3779b97f4a7c15))
+        for t in range(int(lens.max())):
+            sel = lens > t
+            e = ent_off[:-1][sel] + t
+            v = (pos_map[ent_rec[e]].astype(np.uint64) << np.uint64(8)) ^ ent_name[e].astype(np.uint64)
+            h[sel] = _mix64(h[sel] ^ v)
+        return int(h.sum(dtype=np.uint64))
+
+
+def _arrival_batches(pat, n, K, key, cols, ts, stream, n_matches, csum, resident, per, pipelined=False):
+    """The processor's flushes as a Kafka partition delivers the records: the C2 stream in its generation
+    (arrival) order -- keys interleaved -- in pinned host batches of `per` records through a carry session,
+    CEP_BATCH_ARRIVAL_ORDER | CEP_BATCH_DELIVER, each collected: the library groups every batch by key on
+    the device and returns its matches in arrival order of the completing record, so no host sorts.
+    Parity: the batches' matches, their stream (arrival) positions mapped back to the resident batch's
+    positions, give the resident run's match count and checksum; and every batch's matches come in
+    non-decreasing arrival order of their completing record (the reference's forward order).
+    pipelined: batch i + 1 is pushed before batch i is collected (cep_collect_batch: double-buffered
+    delivery), so the host's copy-in of the next batch overlaps the device's work on this one."""
+    import numpy as np
+    import torch
+    from kcep import native as N
+    ka = torch.empty_like(key)
+    ka[ts] = key
+    ca = []
+    for c in cols:
+        x = torch.empty_like(c)
+        x[ts] = c
+        ca.append(x)
+    hk, hc = ka.cpu().pin_memory(), [c.cpu().pin_memory() for c in ca]
+    del ka, ca
+    pos_map = ts.cpu().numpy().copy()                      # arrival position -> resident batch position
+    pos_map[pos_map.copy()] = np.arange(n)
+    cs = N.Session(pat, per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K)
+    cs.set_timing(False)
+    flags = N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER | N.BATCH_ARRIVAL_ORDER
+    bounds = list(range(0, n, per)) + [n]
+
+    def one_pass(check):
+        parts, ordered = [], True
+
+        def take(out):
+            nonlocal ordered
+            if check:
+                mr = out["match_record"]
+                ordered = ordered and bool(np.all(mr[1:] >= mr[:-1]))
+                parts.append(out)
+        prev = None
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            cs.push(b - a, hk.data_ptr() + 4 * a, [c.data_ptr() + c.element_size() * a for c in hc], mem=N.MEM_HOST,
+                    stream=stream.cuda_stream, flags=flags)
+            if not pipelined:
+                take(cs.collect())
+                continue
+            if prev is not None:
+                take(cs.collect(batch_id=prev))
+            prev = cs.batch_id()
+        if pipelined and prev is not None:
+            take(cs.collect(batch_id=prev))
+        return parts, ordered
+
+    parts, ordered = one_pass(True)
+    m = sum(len(p["match_record"]) for p in parts)
+    c = 0
+    for p in parts:
+        c = (c + _csr_checksum(p["match_record"], p["ent_off"], p["ent_name"], p["ent_record"], pos_map)) & ((1 << 64) - 1)
+    del parts
+    cs.state_clear()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    one_pass(False)
+    stream.synchronize()
+    dt = time.perf_counter() - t0
+    cs.close()
+    nbat = len(bounds) - 1
+    return {"value": n / dt, "unit": "events/s", "batches": nbat, "events_per_batch": per, "ms_per_pass": dt * 1e3,
+            "vs_resident": n / dt / resident, "path": "stencil" if cs.path == N.PATH_STENCIL else "chain",
+            "parity": bool(m == n_matches and c == csum), "forward_order": ordered, "matches": int(m),
+            "host_memory": "pinned", "collect_per_batch": True, "arrival_order": True, "pipelined": pipelined,
+            "us_per_batch": dt * 1e6 / nbat, "overhead_us_per_batch": (dt - n / resident) * 1e6 / nbat}
 
 
 def _kcrf_events(blob):

@@ -278,6 +278,16 @@ int cep_collect(cep_session* s, cep_matches* out);
  * SharedVersionedBufferStoreImpl.java:113-115). */
 int cep_csr_check(const cep_matches* m, int64_t n_records, int32_t n_names);
 
+/* Pipelined flushes.  cep_batch_id: the number of the last pushed batch (1, 2, ...).  On stencil / chain carry
+ * sessions a CEP_BATCH_DELIVER batch's matches go to one of two host buffers, so a host can push batch i + 1
+ * before it collects batch i: cep_collect_batch(id) collects the last batch (as cep_collect) or the delivered
+ * batch before it (CEP_E_UNSUPPORTED if that one had more matches than the host buffer holds, 2^20 rows, which
+ * are collected only before the next push); cep_batch_ready(id) tells without waiting whether batch id's
+ * matches are complete (1) or not yet (0).  The host CSR of cep_collect_batch is valid until the next collect. */
+int64_t cep_batch_id(const cep_session* s);
+int cep_batch_ready(cep_session* s, int64_t id);
+int cep_collect_batch(cep_session* s, int64_t id, cep_matches* out);
+
 /* Order-independent 64-bit checksum of the last batch's matches, computed on
  * the device (matches the oracle's orc_baseline checksum); waits. */
 int cep_checksum(cep_session* s, uint64_t* sum, int64_t* n_matches);

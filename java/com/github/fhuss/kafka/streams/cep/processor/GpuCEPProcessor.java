@@ -81,7 +81,8 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     private static native long cepCompile(byte[] ir);                                   // cep_compile
     private static native String[] cepStageNames(long pattern);                          // cep_pattern_name
     private static native long cepSessionOpen(long pattern, int device, int mode, long maxEvents,
-                                              int flags, long maxKeys, long maxKeyWords); // cep_session_open
+                                              int flags, long maxKeys, long maxKeyWords,
+                                              long maxPoolBytes);                 // cep_session_open
     private static native int cepSessionPath(long session);                              // cep_session_path
     /** cep_push_batch + cep_collect (the host arrays are borrowed until the batch is done). */
     private static native int cepPushBatch(long session, int n, int[] keyId, int[] topic, int[] partition,
@@ -108,6 +109,7 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     private static final int CEP_MODE_PROCESSOR = 1, CEP_SESSION_CARRY = 1, CEP_E_RUN_CAPACITY = 9;
     private static final int CEP_PATH_STENCIL = 1, CEP_PATH_CHAIN = 3, CEP_PATH_RUNS = 4, CEP_BATCH_OFFSETS_MONOTONE = 1;
     private static final int CEP_BATCH_DELIVER = 2;                // collected at once: matches delivered to host memory
+    private static final int CEP_BATCH_ARRIVAL_ORDER = 4;          // records in arrival order: grouped on the device
 
     private final String queryName;
     private final String rawQueryName;
@@ -117,6 +119,7 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
     private final int batchSize;
     private final int maxKeys;
     private final long maxKeyWords;
+    private final long maxPoolBytes;           // the session's device workspace budget (0: a quarter of the HBM)
     private ProcessorContext context;
     private long pattern, session;
     private int path;
@@ -151,6 +154,13 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
      *  get the next free ids as they arrive. */
     public GpuCEPProcessor(String queryName, Pattern<K, V> pattern, byte[] ir, List<String> topics,
                            ValueDecoder<V> decoder, int batchSize, int maxKeys, long maxKeyWords) {
+        this(queryName, pattern, ir, topics, decoder, batchSize, maxKeys, maxKeyWords, 0L);
+    }
+
+    /** maxPoolBytes: cep_opts.max_pool_bytes -- with one processor per stream task sharing a GPU, each
+     *  session's device workspace budget (e.g. the HBM share of one task). */
+    public GpuCEPProcessor(String queryName, Pattern<K, V> pattern, byte[] ir, List<String> topics,
+                           ValueDecoder<V> decoder, int batchSize, int maxKeys, long maxKeyWords, long maxPoolBytes) {
         this.queryName = queryName.toLowerCase().replace("\\s+", "");   // CEPProcessor.java:83, literal replace
         this.rawQueryName = queryName;
         this.referencePattern = pattern;
@@ -160,6 +170,7 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         this.batchSize = batchSize;
         this.maxKeys = maxKeys;
         this.maxKeyWords = maxKeyWords;
+        this.maxPoolBytes = maxPoolBytes;
         this.pruneAt = Math.max(1 << 20, 2 * batchSize);
     }
 
@@ -169,7 +180,7 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         this.pattern = check(cepCompile(ir));
         this.names = cepStageNames(pattern);
         this.session = check(cepSessionOpen(pattern, 0, CEP_MODE_PROCESSOR, batchSize, CEP_SESSION_CARRY,
-                                            maxKeys, maxKeyWords));
+                                            maxKeys, maxKeyWords, maxPoolBytes));
         this.path = cepSessionPath(session);
         // the reference processor for keys that outgrow the device, over the reference's own stores
         this.stages = new StagesFactory<K, V>().make(referencePattern);
@@ -217,13 +228,13 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
         }
     }
 
-    /** One cep_push_batch of the records at arrival indices idx (ascending), grouped by key id (stable);
-     *  fills matches (emission order) and errors (arrival index, code) pairs. */
+    /** One cep_push_batch of the records at arrival indices idx (ascending), in arrival order: the library
+     *  groups them by key on the device (CEP_BATCH_ARRIVAL_ORDER) and returns the matches in arrival order of
+     *  their completing record, so nothing is sorted here; fills matches (forward order) and errors
+     *  (arrival index, code) pairs. */
     private void run(List<Event<K, V>> recs, int[] kid, int[] idx, int flags, List<Match> matches, List<long[]> errors) {
         final int n = idx.length;
-        Integer[] order = new Integer[n];
-        for (int i = 0; i < n; i++) order[i] = idx[i];
-        Arrays.sort(order, (a, b) -> Integer.compare(kid[a], kid[b]));   // stable: arrival order per key
+        final int[] order = idx;                                        // batch position -> arrival index
         int[] keyId = new int[n], topic = new int[n], part = new int[n];
         long[] off = new long[n], ts = new long[n];
         int nc = decoder.columns();
@@ -248,7 +259,8 @@ public class GpuCEPProcessor<K, V> implements Processor<K, V> {
             }
             log.put(base + j, e);
         }
-        int rc = cepPushBatch(session, n, keyId, topic, part, off, ts, types, cols, flags | CEP_BATCH_DELIVER);
+        int rc = cepPushBatch(session, n, keyId, topic, part, off, ts, types, cols,
+                              flags | CEP_BATCH_DELIVER | CEP_BATCH_ARRIVAL_ORDER);
         if (rc != 0) throw new IllegalStateException(queryName + ": " + cepLastError());
         long[] sizes = new long[2];
         cepCollect(session, sizes, null, null, null, null, null);         // sizes only (no device work)

@@ -46,7 +46,8 @@ JNIEXPORT jobjectArray JNICALL CLS(cepStageNames)(JNIEnv* env, jclass c, jlong p
 }
 
 JNIEXPORT jlong JNICALL CLS(cepSessionOpen)(JNIEnv* env, jclass c, jlong pattern, jint device, jint mode,
-                                            jlong max_events, jint flags, jlong max_keys, jlong max_key_words) {
+                                            jlong max_events, jint flags, jlong max_keys, jlong max_key_words,
+                                            jlong max_pool_bytes) {
   cep_opts o;
   memset(&o, 0, sizeof o);
   o.device = device;
@@ -55,6 +56,7 @@ JNIEXPORT jlong JNICALL CLS(cepSessionOpen)(JNIEnv* env, jclass c, jlong pattern
   o.max_events = max_events;
   o.max_keys = max_keys;
   o.max_key_words = max_key_words;
+  o.max_pool_bytes = max_pool_bytes;
   cep_session* s = NULL;
   int rc = cep_session_open((const cep_pattern*)(intptr_t)pattern, &o, &s);
   return rc ? -(jlong)rc : (jlong)(intptr_t)s;

@@ -188,7 +188,10 @@ struct cep_session {
   hipEvent_t h2d_ev = nullptr;
   // ---- CEP_BATCH_DELIVER (carry stencil / chain sessions): the matches handed to pinned host memory by
   // the device during the push; cep_collect then only waits ----
-  void* dl = nullptr;             // dl_layout: header, host_cap keys, host_cap * k positions
+  void* dl[2] = {nullptr, nullptr};   // dl_layout: header, host_cap keys, host_cap * k positions; by stamp parity
+  int64_t dl_pid[2] = {-1, -1};       // the batch (push number) each holds: a host pushes batch i + 1 before it
+                                      // collects batch i (cep_collect_batch)
+  int64_t push_id = 0;                // cep_push_batch calls so far (cep_batch_id)
   int64_t dl_cap = 0;
   DBuf dl_ticket;                 // device: workgroups of the delivery kernel done
   int64_t dl_stamp = 0;           // the last delivery's number
@@ -244,7 +247,7 @@ struct cep_session {
   int64_t* h_res = nullptr;                // runs / general paths: the batch's counts, written by the device into
                                            // pinned memory (16 words)
   // ---- CEP_BATCH_ARRIVAL_ORDER (group.hip): the batch grouped by key on the device ----
-  DBuf g_key, g_arr, g_pos, g_valid, g_topic, g_part, g_off, g_ts, g_head, g_top, g_nodes, g_lt, g_start, g_tmp, a_cnt,
+  DBuf g_key, g_arr, g_pos, g_valid, g_topic, g_part, g_off, g_ts, g_head, g_top, g_nodes, g_start, a_cnt,
       a_ecnt, a_head, a_moff, a_moffe, a_tmp, a_record, a_key, a_entoff, a_name, a_entrec;
   uint32_t group_stamp = 0;                // the groupings so far (epoch of the per-key list heads)
   DBuf g_cols[16];
@@ -409,8 +412,8 @@ int stage_host(cep_session* s, HostArr* arrs, int na, hipStream_t st, bool zero_
 
 // CEP_BATCH_DELIVER host buffer: {match count, error flags, completion stamp, 0}, host_cap keys (int32,
 // padded to 8 bytes), then host_cap x k stream positions
-void dl_layout(const cep_session* s, int64_t*& hdr, int32_t*& hkey, int64_t*& hpos) {
-  hdr = static_cast<int64_t*>(s->dl);
+void dl_layout(const cep_session* s, int slot, int64_t*& hdr, int32_t*& hkey, int64_t*& hpos) {
+  hdr = static_cast<int64_t*>(s->dl[slot]);
   hkey = reinterpret_cast<int32_t*>(hdr + 4);
   hpos = hdr + 4 + (s->dl_cap + 1) / 2 + 1;
 }
@@ -455,10 +458,12 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
   if (s->carry && (b->flags & CEP_BATCH_DELIVER)) {   // the matches to pinned host memory, by the device
     const int k = SP.k;
     const int64_t host_cap = std::min<int64_t>(s->out_cap, int64_t(1) << 20);
-    if (!s->dl) {
+    if (!s->dl[0]) {
       const size_t bytes = 8 * (4 + size_t(host_cap + 1) / 2 + 1) + size_t(host_cap) * size_t(k) * 8;   // see dl_layout
-      HIPCHECK(hipHostMalloc(&s->dl, bytes, hipHostMallocMapped | hipHostMallocCoherent));
-      memset(s->dl, 0, 32);
+      for (int j = 0; j < 2; j++) {
+        HIPCHECK(hipHostMalloc(&s->dl[j], bytes, hipHostMallocMapped | hipHostMallocCoherent));
+        memset(s->dl[j], 0, 32);
+      }
       s->dl_cap = host_cap;
       if (s->dl_ticket.ensure(16)) return fail(CEP_E_HIP, "allocation failed");
       HIPCHECK(hipMemsetAsync(s->dl_ticket.p, 0, 16, st));
@@ -466,7 +471,9 @@ int push_stencil(cep_session* s, const cep_batch* b, hipStream_t st) {
     if (s->out_cap > host_cap &&
         (s->mkey.ensure(size_t(s->out_cap) * 4) || s->opos.ensure(size_t(s->out_cap) * size_t(k) * 8)))
       return fail(CEP_E_HIP, "allocation failed");
-    dl_layout(s, L.deliver.hdr, L.deliver.hkey, L.deliver.hpos);
+    const int slot = int((s->dl_stamp + 1) & 1);   // the next stamp's buffer (the other holds the batch before)
+    dl_layout(s, slot, L.deliver.hdr, L.deliver.hkey, L.deliver.hpos);
+    s->dl_pid[slot] = s->push_id;
     L.deliver.dkey = s->mkey.as<int32_t>();
     L.deliver.dpos = s->opos.as<int64_t>();
     L.deliver.host_cap = s->dl_cap;
@@ -1308,7 +1315,7 @@ int cep_session_open(const cep_pattern* p, const cep_opts* opts, cep_session** o
 void cep_session_close(cep_session* s) {
   if (!s) return;
   for (DBuf* b : {&s->g_key, &s->g_arr, &s->g_pos, &s->g_valid, &s->g_topic, &s->g_part, &s->g_off, &s->g_ts, &s->g_head,
-                  &s->g_top, &s->g_nodes, &s->g_lt, &s->g_start, &s->g_tmp, &s->a_cnt, &s->a_ecnt, &s->a_head, &s->a_moff,
+                  &s->g_top, &s->g_nodes, &s->g_start, &s->a_cnt, &s->a_ecnt, &s->a_head, &s->a_moff,
                   &s->a_moffe, &s->a_tmp, &s->a_record, &s->a_key, &s->a_entoff, &s->a_name, &s->a_entrec})
     b->release();
   for (auto& c : s->g_cols) c.release();
@@ -1329,10 +1336,9 @@ void cep_session_close(cep_session* s) {
   }
   if (s->h2d_ev) (void)hipEventDestroy(s->h2d_ev);
   if (s->h_res) (void)hipHostFree(s->h_res);
-  if (s->dl) {
-    (void)hipDeviceSynchronize();                   // a delivery may still be writing into it
-    (void)hipHostFree(s->dl);
-  }
+  if (s->dl[0] || s->dl[1]) (void)hipDeviceSynchronize();   // a delivery may still be writing into them
+  for (int j = 0; j < 2; j++)
+    if (s->dl[j]) (void)hipHostFree(s->dl[j]);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->eb0) (void)hipEventDestroy(s->eb0);
@@ -1447,7 +1453,7 @@ static int group_batch(cep_session* s, const cep_batch* b, hipStream_t st, cep_b
       return fail(CEP_E_HIP, "allocation failed");
   }
   if (s->g_key.ensure(n4) || s->g_arr.ensure(n4) || s->g_pos.ensure(n8) || s->g_nodes.ensure(8 * n4) ||
-      s->g_lt.ensure(n8) || s->g_start.ensure(n8) || s->g_tmp.ensure(size_t(n / 1024 + 4) * 8) || s->scal.ensure(64) ||
+      s->g_start.ensure(n8) || s->scal.ensure(64) ||
       s->a_cnt.ensure(n8) || s->a_ecnt.ensure(n8) || s->a_head.ensure(n4) || (in.valid && s->g_valid.ensure(size_t(n))) ||
       (in.topic && s->g_topic.ensure(n4)) || (in.partition && s->g_part.ensure(n4)) || (in.offset && s->g_off.ensure(n8)) ||
       (in.ts && s->g_ts.ensure(n8)))
@@ -1460,8 +1466,8 @@ static int group_batch(cep_session* s, const cep_batch* b, hipStream_t st, cep_b
   int32_t* nodes = s->g_nodes.as<int32_t>();
   G.node_key = nodes; G.node_chunk = nodes + n; G.node_cnt = nodes + 2 * n; G.node_next = nodes + 3 * n;
   G.node_prefix = nodes + 4 * n; G.node_leader = nodes + 5 * n; G.rec_node = nodes + 6 * n; G.rec_rank = nodes + 7 * n;
-  G.lt = s->g_lt.as<int64_t>(); G.start = s->g_start.as<int64_t>(); G.start_tot = s->g_top.as<int64_t>() + 1;
-  G.scan_tmp = s->g_tmp.as<int64_t>();
+  G.start = s->g_start.as<int64_t>();
+  G.cursor = s->g_top.as<unsigned long long>() + 1;
   G.key = in.key; G.g_key = s->g_key.as<int32_t>(); G.arr = s->g_arr.as<int32_t>(); G.pos = s->g_pos.as<int64_t>();
   G.base = s->base;
   G.valid = in.valid; G.g_valid = in.valid ? s->g_valid.as<uint8_t>() : nullptr;
@@ -1543,6 +1549,7 @@ int cep_push_batch(cep_session* s, const cep_batch* b, void* stream) {
   HIPCHECK(hipSetDevice(s->device));
   s->stream = st;
   s->n = b->n;
+  s->push_id++;
   s->pending = true;
   s->collected = false;
   s->e_rec.clear();
@@ -1665,6 +1672,79 @@ int cep_csr_check(const cep_matches* m, int64_t n_records, int32_t n_names) {
   return CEP_OK;
 }
 
+// A delivered batch (CEP_BATCH_DELIVER) from host buffer `slot`, stamped `want`: spin until the delivery
+// kernel has stamped it, then the host CSR.  latest: the last pushed batch (matches past the host buffer are
+// still in the device arrays)
+static int collect_delivered(cep_session* s, int slot, int64_t want, bool latest, cep_matches* o) {
+  {
+    const StencilProgram& SP = s->pat->prog.stencil;
+    const int k = SP.k;
+    int64_t* hdr;
+    int32_t* hkey;
+    int64_t* hpos;
+    dl_layout(s, slot, hdr, hkey, hpos);
+    // the delivery kernel's last workgroup stamps hdr[2] once every row is in host memory: spin on it (a
+    // stream wait sleeps and wakes microseconds late); a stamp that does not come -- a fault -- is left
+    // to the stream wait, which reports it
+    const volatile int64_t* stamp = hdr + 2;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*stamp != want) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+        HIPCHECK(hipStreamSynchronize(s->stream));
+        if (*stamp != want) return fail(CEP_E_HIP, "the delivery kernel did not complete");
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const int64_t nm = hdr[0];
+    const uint64_t hf = uint64_t(hdr[1]);
+    if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
+    if (hf & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
+    if (hf & 4) return fail(CEP_E_RUN_CAPACITY, "chain carry batch: more runs completing in one tile than its match space");
+    if (nm > s->out_cap) return fail(CEP_E_RUN_CAPACITY, "match output exceeded the session capacity");
+    const int64_t nh = std::min(nm, s->dl_cap);
+    if (nm > nh && !latest)                        // the rest was on the device, which a later push reused
+      return fail(CEP_E_UNSUPPORTED, "a batch with more matches than the host delivery buffer is collected only "
+                                     "before the next push");
+    std::vector<int64_t> rest_pos;
+    std::vector<int32_t> rest_key;
+    if (nm > nh) {                                 // past the host buffer: from the device arrays
+      rest_pos.resize(size_t(nm - nh) * k);
+      rest_key.resize(size_t(nm - nh));
+      HIPCHECK(hipMemcpy(rest_pos.data(), s->opos.as<int64_t>() + nh * k, rest_pos.size() * 8, hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(rest_key.data(), s->mkey.as<int32_t>() + nh, rest_key.size() * 4, hipMemcpyDeviceToHost));
+    }
+    s->match_record.resize(size_t(nm));
+    s->match_key.resize(size_t(nm));
+    s->ent_off.resize(size_t(nm) + 1);
+    s->ent_name.resize(size_t(nm) * k);
+    s->ent_record.resize(size_t(nm) * k);
+    int64_t ne = 0;
+    for (int64_t m = 0; m < nm; m++) {             // peek traversal order: final stage first
+      const int64_t* p = m < nh ? hpos + m * k : rest_pos.data() + (m - nh) * k;
+      s->match_key[size_t(m)] = m < nh ? hkey[m] : rest_key[size_t(m - nh)];
+      s->match_record[size_t(m)] = p[k - 1];
+      s->ent_off[size_t(m)] = ne;
+      for (int i = k - 1; i >= 0; i--) {
+        if (p[i] == -1) continue;                   // a skipped optional stage
+        s->ent_name[size_t(ne)] = SP.name[i];
+        s->ent_record[size_t(ne)] = p[i];
+        ne++;
+      }
+    }
+    s->ent_off[size_t(nm)] = ne;
+    s->ent_name.resize(size_t(ne));
+    s->ent_record.resize(size_t(ne));
+    o->n_matches = nm;
+    o->n_entries = ne;
+    o->path = s->last_path;
+    o->err = CEP_OK;
+    o->err_record = -1;
+  }
+  return CEP_OK;
+}
+
 int cep_collect(cep_session* s, cep_matches* o) {
   if (!s || !o) return fail(CEP_E_ARG, "null argument");
   RoctxRange range("cep_collect");
@@ -1707,67 +1787,8 @@ int cep_collect(cep_session* s, cep_matches* o) {
     if (rc) return rc;
     if (s->g_err) g_err = "the reference NFA raises an exception on this batch";
   } else if (s->delivered) {                       // CEP_BATCH_DELIVER: the device wrote the CSR's inputs
-    const StencilProgram& SP = s->pat->prog.stencil;
-    const int k = SP.k;
-    int64_t* hdr;
-    int32_t* hkey;
-    int64_t* hpos;
-    dl_layout(s, hdr, hkey, hpos);
-    // the delivery kernel's last workgroup stamps hdr[2] once every row is in host memory: spin on it (a
-    // stream wait sleeps and wakes microseconds late); a stamp that does not come -- a fault -- is left
-    // to the stream wait, which reports it
-    const volatile int64_t* stamp = hdr + 2;
-    const auto t0 = std::chrono::steady_clock::now();
-    while (*stamp != s->dl_stamp) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
-        HIPCHECK(hipStreamSynchronize(s->stream));
-        if (*stamp != s->dl_stamp) return fail(CEP_E_HIP, "the delivery kernel did not complete");
-        break;
-      }
-      __builtin_ia32_pause();
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    const int64_t nm = hdr[0];
-    const uint64_t hf = uint64_t(hdr[1]);
-    if (hf & 1) return fail(CEP_E_ARG, "carry sessions need key ids in [0, max_keys)");
-    if (hf & 2) return fail(CEP_E_ARG, "carry batch is not grouped by key: a key has two segments");
-    if (hf & 4) return fail(CEP_E_RUN_CAPACITY, "chain carry batch: more runs completing in one tile than its match space");
-    if (nm > s->out_cap) return fail(CEP_E_RUN_CAPACITY, "match output exceeded the session capacity");
-    const int64_t nh = std::min(nm, s->dl_cap);
-    std::vector<int64_t> rest_pos;
-    std::vector<int32_t> rest_key;
-    if (nm > nh) {                                 // past the host buffer: from the device arrays
-      rest_pos.resize(size_t(nm - nh) * k);
-      rest_key.resize(size_t(nm - nh));
-      HIPCHECK(hipMemcpy(rest_pos.data(), s->opos.as<int64_t>() + nh * k, rest_pos.size() * 8, hipMemcpyDeviceToHost));
-      HIPCHECK(hipMemcpy(rest_key.data(), s->mkey.as<int32_t>() + nh, rest_key.size() * 4, hipMemcpyDeviceToHost));
-    }
-    s->match_record.resize(size_t(nm));
-    s->match_key.resize(size_t(nm));
-    s->ent_off.resize(size_t(nm) + 1);
-    s->ent_name.resize(size_t(nm) * k);
-    s->ent_record.resize(size_t(nm) * k);
-    int64_t ne = 0;
-    for (int64_t m = 0; m < nm; m++) {             // peek traversal order: final stage first
-      const int64_t* p = m < nh ? hpos + m * k : rest_pos.data() + (m - nh) * k;
-      s->match_key[size_t(m)] = m < nh ? hkey[m] : rest_key[size_t(m - nh)];
-      s->match_record[size_t(m)] = p[k - 1];
-      s->ent_off[size_t(m)] = ne;
-      for (int i = k - 1; i >= 0; i--) {
-        if (p[i] == -1) continue;                   // a skipped optional stage
-        s->ent_name[size_t(ne)] = SP.name[i];
-        s->ent_record[size_t(ne)] = p[i];
-        ne++;
-      }
-    }
-    s->ent_off[size_t(nm)] = ne;
-    s->ent_name.resize(size_t(ne));
-    s->ent_record.resize(size_t(ne));
-    o->n_matches = nm;
-    o->n_entries = ne;
-    o->path = s->last_path;
-    o->err = CEP_OK;
-    o->err_record = -1;
+    int rc = collect_delivered(s, int(s->dl_stamp & 1), s->dl_stamp, true, o);
+    if (rc) return rc;
   } else {
     const StencilProgram& SP = s->pat->prog.stencil;
     const int k = SP.k;
@@ -1838,6 +1859,51 @@ int cep_collect(cep_session* s, cep_matches* o) {
   s->pending = false;
   s->collected = true;
   s->last = *o;
+  return CEP_OK;
+}
+
+int64_t cep_batch_id(const cep_session* s) { return s ? s->push_id : -1; }
+
+// the delivery buffer holding batch `id`, or -1
+static int delivered_slot(const cep_session* s, int64_t id) {
+  for (int j = 0; j < 2; j++)
+    if (s->dl[j] && s->dl_pid[j] == id) return j;
+  return -1;
+}
+
+int cep_batch_ready(cep_session* s, int64_t id) {
+  if (!s) return fail(CEP_E_ARG, "null argument");
+  if (id < 1 || id > s->push_id) return fail(CEP_E_ARG, "no such batch");
+  const int slot = delivered_slot(s, id);
+  if (slot >= 0) {                                 // delivered: its stamp is in host memory once complete
+    const int64_t want = s->dl_stamp - ((s->dl_stamp & 1) == slot ? 0 : 1);
+    return *reinterpret_cast<const volatile int64_t*>(static_cast<int64_t*>(s->dl[slot]) + 2) == want ? 1 : 0;
+  }
+  if (id < s->push_id) return 1;                   // (an earlier batch: the stream has moved past it, or will)
+  const hipError_t e = hipStreamQuery(s->stream);
+  if (e == hipErrorNotReady) return 0;
+  if (e != hipSuccess) return fail(CEP_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(e));
+  return 1;
+}
+
+int cep_collect_batch(cep_session* s, int64_t id, cep_matches* o) {
+  if (!s || !o) return fail(CEP_E_ARG, "null argument");
+  if (id == s->push_id) return cep_collect(s, o);
+  const int slot = delivered_slot(s, id);
+  if (slot < 0 || id != s->push_id - 1)
+    return fail(CEP_E_ARG, "only the last batch, or the delivered batch before it, can be collected");
+  RoctxRange range("cep_collect");
+  memset(o, 0, sizeof *o);
+  HIPCHECK(hipSetDevice(s->device));
+  const int64_t want = s->dl_stamp - ((s->dl_stamp & 1) == slot ? 0 : 1);
+  int rc = collect_delivered(s, slot, want, false, o);
+  if (rc) return rc;
+  o->match_record = s->match_record.data();
+  o->match_key = s->match_key.data();
+  o->ent_off = s->ent_off.data();
+  o->ent_name = s->ent_name.data();
+  o->ent_record = s->ent_record.data();
+  s->collected = false;                            // the host CSR now holds the older batch
   return CEP_OK;
 }
 

@@ -10,8 +10,8 @@
 //                   every (chunk, key) pair becomes a node pushed onto the key's list (an epoch-tagged head
 //                   per key id: nothing is cleared between batches)
 //     group_nodes   per node: the key's records in earlier chunks (its prefix), the key's total and its
-//                   leader (the node of the key's first chunk); the leaders' totals are scanned into the
-//                   groups' starts
+//                   leader (the node of the key's first chunk); each leader takes its key's group from a
+//                   cursor (one atomic per workgroup)
 //     group_gather  per record: grouped position = start(leader) + prefix + rank; every column moved there,
 //                   and its stream position written (base + arrival index)
 //   The paths take the grouped positions as NfaArgs.pos / RcIn.pos / StencilCarry.gpos, so carried state and
@@ -65,14 +65,23 @@ __global__ __launch_bounds__(64) void group_chunks(const int32_t* __restrict__ k
     tcnt[i] = 0;
     tmask[i] = 0;
   }
+  // the chunk's keys, all loads in flight at once (a batch read over the link in place costs a link
+  // round trip per dependent load: 16 of them took 55 us per 64 k-record flush)
+  int32_t kr[GR_CHUNK / 64];
+#pragma unroll
+  for (int round = 0; round < GR_CHUNK / 64; round++) {
+    const int64_t r = r0 + round * 64 + lane;
+    kr[round] = r < n ? key[r] : 0;
+  }
   __syncthreads();
+#pragma unroll
   for (int round = 0; round < GR_CHUNK / 64; round++) {
     const int64_t r = r0 + round * 64 + lane;
     if (r0 + round * 64 >= n) break;             // (uniform)
     const bool act = r < n;
     int h = 0;
     if (act) {
-      const int32_t k0 = key[r];
+      const int32_t k0 = kr[round];
       const int32_t k = k0 >= 0 && k0 < max_keys ? k0 : -1;
       h = int(gr_hash(k) & (GR_TAB - 1));
       for (;;) {
@@ -102,23 +111,37 @@ __global__ __launch_bounds__(64) void group_chunks(const int32_t* __restrict__ k
   for (int i = lane; i < GR_TAB; i += 64) d += __popcll(__ballot(tkey[i] != GR_EMPTY));
   if (lane == 0) s_base = d ? atomicAdd(node_top, d) : 0;
   __syncthreads();
+  // every head exchange of the chunk in flight before the first result is used (one list push per node;
+  // waited one by one they cost a memory round trip each: 32 per wave)
   int nd = s_base;
-  for (int i0 = 0; i0 < GR_TAB; i0 += 64) {
-    const int i = i0 + lane;
+  unsigned long long old[GR_TAB / 64];
+  int xs[GR_TAB / 64];
+#pragma unroll
+  for (int j = 0; j < GR_TAB / 64; j++) {
+    const int i = j * 64 + lane;
     const bool occ = tkey[i] != GR_EMPTY;
     const unsigned long long b = __ballot(occ);
+    xs[j] = -1;
+    old[j] = 0;
     if (occ) {
       const int x = nd + __popcll(b & ((1ull << lane) - 1ull));
       const int32_t k = tkey[i];
-      node_key[x] = k;
-      node_chunk[x] = int32_t(blockIdx.x);
-      node_cnt[x] = tcnt[i];
-      const unsigned long long old =
-          atomicExch(&head[k >= 0 ? k : max_keys], (static_cast<unsigned long long>(stamp) << 32) | uint32_t(x));
-      node_next[x] = uint32_t(old >> 32) == stamp ? int32_t(uint32_t(old)) : -1;
-      tcnt[i] = x;
+      xs[j] = x;
+      old[j] = atomicExch(&head[k >= 0 ? k : max_keys], (static_cast<unsigned long long>(stamp) << 32) | uint32_t(x));
     }
     nd += __popcll(b);
+  }
+#pragma unroll
+  for (int j = 0; j < GR_TAB / 64; j++) {
+    const int i = j * 64 + lane;
+    const int x = xs[j];
+    if (x >= 0) {
+      node_key[x] = tkey[i];
+      node_chunk[x] = int32_t(blockIdx.x);
+      node_cnt[x] = tcnt[i];
+      node_next[x] = uint32_t(old[j] >> 32) == stamp ? int32_t(uint32_t(old[j])) : -1;
+      tcnt[i] = x;
+    }
   }
   __syncthreads();
   for (int j = lane; j < GR_CHUNK; j += 64) {
@@ -129,40 +152,63 @@ __global__ __launch_bounds__(64) void group_chunks(const int32_t* __restrict__ k
   }
 }
 
-// per node: its key's records in earlier chunks, and the key's leader node (first chunk); a leader's lt is
-// the key's total (scanned into the groups' starts), every other node's 0
+// per node: its key's records in earlier chunks, and the key's leader node (first chunk); a leader takes
+// the key's group -- its total records -- from a cursor (any order of the groups will do: one atomic per
+// workgroup, lanes placed by a scan)
 __global__ __launch_bounds__(256) void group_nodes(int64_t cap, const int32_t* __restrict__ node_top, int32_t max_keys,
                                                    const unsigned long long* __restrict__ head,
                                                    const int32_t* __restrict__ node_key, const int32_t* __restrict__ node_chunk,
                                                    const int32_t* __restrict__ node_cnt, const int32_t* __restrict__ node_next,
                                                    int32_t* __restrict__ node_prefix, int32_t* __restrict__ node_leader,
-                                                   int64_t* __restrict__ lt) {
+                                                   int64_t* __restrict__ start, unsigned long long* __restrict__ cursor) {
   const int64_t x = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (x >= cap) return;
-  if (x >= *node_top) {
-    lt[x] = 0;
-    return;
+  const int lane = threadIdx.x & 63;
+  int64_t total = 0;
+  bool leader = false;
+  if (x < cap && x < *node_top) {
+    const int32_t k = node_key[x], c = node_chunk[x];
+    int32_t y = int32_t(uint32_t(head[k >= 0 ? k : max_keys]));   // (this batch's: x is on the list)
+    int64_t prefix = 0;
+    int32_t lead = int32_t(x), leadc = c;
+    while (y >= 0) {
+      const int32_t cc = node_chunk[y], cn = node_cnt[y];
+      total += cn;
+      if (cc < c) prefix += cn;
+      if (cc < leadc) { leadc = cc; lead = y; }
+      y = node_next[y];
+    }
+    node_prefix[x] = int32_t(prefix);
+    node_leader[x] = lead;
+    leader = lead == int32_t(x);
   }
-  const int32_t k = node_key[x], c = node_chunk[x];
-  int32_t y = int32_t(uint32_t(head[k >= 0 ? k : max_keys]));   // (this batch's: x is on the list)
-  int64_t prefix = 0, total = 0;
-  int32_t lead = int32_t(x), leadc = c;
-  while (y >= 0) {
-    const int32_t cc = node_chunk[y], cn = node_cnt[y];
-    total += cn;
-    if (cc < c) prefix += cn;
-    if (cc < leadc) { leadc = cc; lead = y; }
-    y = node_next[y];
+  __shared__ int64_t s_w[4];
+  __shared__ unsigned long long s_base;
+  const int wid = threadIdx.x >> 6;
+  int64_t v = leader ? total : 0, incl = v;      // the workgroup's leaders' groups: one cursor add
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
   }
-  node_prefix[x] = int32_t(prefix);
-  node_leader[x] = lead;
-  lt[x] = lead == int32_t(x) ? total : 0;
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t sum = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    s_base = sum ? atomicAdd(cursor, (unsigned long long)sum) : 0;
+  }
+  __syncthreads();
+  int64_t before = int64_t(s_base);
+  for (int w = 0; w < wid; w++) before += s_w[w];
+  if (leader) start[x] = before + incl - v;
 }
 
 // grouped record g = start(leader) + prefix + rank <- arrival record i; zeroes the reorder's per-record counts
 __global__ __launch_bounds__(256) void group_gather(GroupArgs G, int64_t n) {
   const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (i == 0) *G.node_top = 0;                    // (read by group_nodes only, which is done)
+  if (i == 0) {                                   // (read by group_nodes only, which is done)
+    *G.node_top = 0;
+    *G.cursor = 0;
+  }
   if (i >= n) return;
   const int32_t x = G.rec_node[i];
   const int64_t g = G.start[G.node_leader[x]] + G.node_prefix[x] + G.rec_rank[i];
@@ -239,16 +285,14 @@ __global__ __launch_bounds__(256) void stencil_arrival_count(const int32_t* __re
 
 // key ids -> the grouped batch (G.g_key, G.arr, G.pos, the columns); G.head: max_keys + 1 epoch-tagged list
 // heads (zeroed once), G.stamp: this call's number (>= 1, never repeated); scratch: n entries each of the
-// node and record arrays, G.node_top zeroed once (group_gather re-zeroes it)
+// node and record arrays, G.node_top and G.cursor zeroed once (group_gather re-zeroes them)
 hipError_t group_launch(const GroupArgs& G, int64_t n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const unsigned chunks = unsigned((n + GR_CHUNK - 1) / GR_CHUNK);
   hipLaunchKernelGGL(group_chunks, dim3(chunks), dim3(64), 0, st, G.key, n, G.max_keys, G.stamp, G.head, G.node_top,
                      G.node_key, G.node_chunk, G.node_cnt, G.node_next, G.rec_node, G.rec_rank);
   hipLaunchKernelGGL(group_nodes, dim3(blocks256(n)), dim3(256), 0, st, n, G.node_top, G.max_keys, G.head, G.node_key,
-                     G.node_chunk, G.node_cnt, G.node_next, G.node_prefix, G.node_leader, G.lt);
-  hipError_t e = exclusive_scan(G.lt, n, G.start, G.start_tot, G.scan_tmp, st);
-  if (e != hipSuccess) return e;
+                     G.node_chunk, G.node_cnt, G.node_next, G.node_prefix, G.node_leader, G.start, G.cursor);
   hipLaunchKernelGGL(group_gather, dim3(blocks256(n)), dim3(256), 0, st, G, n);
   return hipGetLastError();
 }

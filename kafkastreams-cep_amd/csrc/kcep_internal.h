@@ -198,7 +198,8 @@ struct GroupArgs {
   unsigned long long* head;       // max_keys + 1 epoch-tagged list heads
   int32_t* node_top;
   int32_t *node_key, *node_chunk, *node_cnt, *node_next, *node_prefix, *node_leader, *rec_node, *rec_rank;
-  int64_t *lt, *start, *start_tot, *scan_tmp;
+  int64_t* start;                 // per leader node: its key's first grouped position
+  unsigned long long* cursor;     // the groups placed so far (zeroed once)
 };
 hipError_t group_launch(const GroupArgs& G, int64_t n, hipStream_t st);
 hipError_t arrival_reorder(const int64_t* mrec, const int32_t* mkey, const int64_t* eoff, const int32_t* ename,

@@ -275,6 +275,122 @@ __global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __r
   deliver_done(ticket, unsigned(gridDim.x), hdr, stamp);
 }
 
+// Small arrival-order carry flushes (CEP_BATCH_ARRIVAL_ORDER, <= ARR_SMALL records, <= SMALL_FINISH
+// super-tiles): the rows, their order by the arrival of the completing record and the delivery in one
+// workgroup, one launch (was: the rows, a count, a three-kernel scan over the batch and the delivery).
+// Per arrival record a byte of LDS counts its matches (a strict fixed-length pattern completes at most
+// one run per record, a chain pattern at most K); match i of completing record a goes to
+// (matches of the records before a) + (its rank among a's matches, which are consecutive in the grouped
+// order: same key, same record).
+constexpr int ARR_SMALL = 65536;
+__global__ __launch_bounds__(1024) void stencil_finish_deliver_arrival(
+    const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt, int64_t nt, int k, int32_t* __restrict__ out,
+    int64_t out_cap, int sub, int64_t* __restrict__ total, unsigned long long* __restrict__ clear_flag, SlotFormat F,
+    const int32_t* __restrict__ key, StencilCarry C, int64_t n, int64_t host_cap, int64_t* __restrict__ hdr,
+    int32_t* __restrict__ hkey, int64_t* __restrict__ hpos, int32_t* __restrict__ dkey, int64_t* __restrict__ dpos,
+    unsigned* ticket, int64_t stamp) {
+  __shared__ int64_t s_pre[SMALL_FINISH + 1];
+  __shared__ int64_t s_w[16];
+  __shared__ uint32_t s_cnt[ARR_SMALL / 4];      // byte a & 3 of word a >> 2: matches completing at record a
+  __shared__ uint32_t s_tpre[1024];              // matches completing at records before thread t's 64
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t c0 = tid < nt ? cnt[tid] : 0;
+  int64_t incl = c0;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  for (int i = tid; i < ARR_SMALL / 4; i += 1024) s_cnt[i] = 0;
+  __syncthreads();
+  int64_t run = incl - c0;
+  for (int w = 0; w < wid; w++) run += s_w[w];
+  s_pre[tid] = run;
+  if (tid == 1023) s_pre[SMALL_FINISH] = run + c0;
+  __syncthreads();
+  const int64_t tot = s_pre[SMALL_FINISH];
+  if (tid == 0) {
+    *total = tot;
+    hdr[0] = tot;
+    hdr[1] = int64_t(*C.flags);                    // this batch's error flags (the count kernel is done)
+    if (clear_flag) *clear_flag = 0;
+  }
+  const bool fits = tot <= out_cap;
+  // pass A: every match's completing record, counted by its arrival index
+  for (int64_t t = wid; t < nt && fits; t += 16) {
+    const int64_t m = s_pre[t + 1] - s_pre[t];
+    for (int64_t q = lane; q < m; q += 64) {
+      const int32_t last = F.entry(slots, t, m, q, k - 1);
+      const int64_t a = C.gpos[last] - C.base;
+      atomicAdd(&s_cnt[a >> 2], 1u << (8 * (a & 3)));
+    }
+  }
+  __syncthreads();
+  {                                                // per thread 64 records: the byte sum, then a block scan
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t w = s_cnt[tid * 16 + j];
+      sum += (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    __syncthreads();                               // (s_w reused)
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t before = x - sum;
+    for (int w = 0; w < wid; w++) before += uint32_t(s_w[w]);
+    s_tpre[tid] = before;
+  }
+  __syncthreads();
+  // pass B: the rows (kept on the device for cep_checksum) and their delivery at the arrival rank
+  for (int64_t t = wid; t < nt && fits; t += 16) {
+    const int64_t m = s_pre[t + 1] - s_pre[t];
+    for (int64_t q = lane; q < m; q += 64) {
+      const int64_t i = s_pre[t] + q;
+      int32_t row[STENCIL_MAX_K], last = 0;
+#pragma unroll
+      for (int s2 = 0; s2 < STENCIL_MAX_K; s2++)
+        if (s2 < k) {
+          row[s2] = F.entry(slots, t, m, q, s2);
+          out[i * k + s2] = row[s2];
+          last = row[s2];
+        }
+      const int64_t a = C.gpos[last] - C.base;
+      int64_t j = s_tpre[a >> 6];
+      for (int64_t b = (a & ~int64_t(63)) >> 2; b < (a >> 2); b++) {   // whole words before a's, then a's bytes
+        const uint32_t w = s_cnt[b];
+        j += (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+      }
+      for (int64_t b = a & ~int64_t(3); b < a; b++) j += (s_cnt[b >> 2] >> (8 * (b & 3))) & 0xFF;
+      if (F.chain)                                 // (a strict fixed-length pattern: one match per record)
+        for (int64_t p = q - 1; p >= 0 && F.entry(slots, t, m, p, k - 1) == last; p--) j++;   // same record, earlier
+      const int32_t kk = key[last];
+      const bool kok = kk >= 0 && kk < C.max_keys;
+      const HaloHdr* h = kok ? C.hdr + kk : nullptr;
+      const int old = kok ? halo_old(*h, C.stamp) : 0;
+      const int64_t* hp = kok ? C.pos + (2 * int64_t(kk) + old) * C.km1 : nullptr;
+      const bool host = j < host_cap;
+      int64_t* pp = host ? hpos + j * k : dpos + j * k;
+#pragma unroll
+      for (int s2 = 0; s2 < STENCIL_MAX_K; s2++)
+        if (s2 < k) {
+          const int32_t r = row[s2];
+          pp[s2] = r >= 0 ? halo_gpos(C, r) : (r == -1 || !kok ? -1 : hp[h->cnt[old] - (-r - 1)]);
+        }
+      if (host) hkey[j] = kk;
+      else dkey[j] = kk;
+    }
+  }
+  (void)n;
+  deliver_done(ticket, 1u, hdr, stamp);
+}
+
 static hipError_t stencil_count(const StencilLaunch& L, hipStream_t st) {
   if (L.chain && L.k != 3 && L.k != 4) return hipErrorInvalidValue;   // an optional stage needs k >= 3; chain k <= 4
   switch (L.k) {
@@ -319,6 +435,12 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
   const bool plain = L.plain && !L.chain && L.k <= 7;
   const SlotFormat F{L.k, plain, L.chain, L.carry.hdr != nullptr, plain && !L.carry.hdr && ST_PLAIN_STAGE,
                      !plain && !L.carry.hdr && ST_KEYED_DENSE, nsuper, sub};
+  if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr && D.a_moff && L.n <= ARR_SMALL) {   // a small arrival-order flush
+    hipLaunchKernelGGL(stencil_finish_deliver_arrival, dim3(1), dim3(1024), 0, st, L.slots, L.tile_count, nsuper, L.k,
+                       L.out, L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, L.n, D.host_cap, D.hdr, D.hkey,
+                       D.hpos, D.dkey, D.dpos, D.ticket, D.stamp);
+    return hipGetLastError();
+  }
   if (nsuper <= SMALL_FINISH && D.hdr && L.carry.hdr && !D.a_moff) {   // a small carry flush: scan, rows and delivery at once
     hipLaunchKernelGGL(stencil_finish_deliver, dim3(unsigned(nsuper)), dim3(256), 0, st, L.slots, L.tile_count, nsuper,
                        L.k, L.out, L.out_cap, sub, L.total, L.clear_flag, F, L.key, L.carry, D.host_cap, D.hdr, D.hkey,

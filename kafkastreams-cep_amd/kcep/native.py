@@ -78,7 +78,7 @@ SYMBOLS = ["cep_compile", "cep_pattern_free", "cep_pattern_get_info", "cep_patte
            "cep_key_profile", "cep_key_hash", "cep_key_shard", "cep_shard_plan", "cep_partition", "cep_gather",
            "cep_match_count_to", "cep_state_evict", "cep_state_import_keys", "cep_state_positions",
            "cep_session_set_max_key_words", "cep_state_to_reference", "cep_pattern_check", "cep_batch_attempts",
-           "cep_csr_check"]
+           "cep_csr_check", "cep_batch_id", "cep_batch_ready", "cep_collect_batch"]
 
 _lib = None
 
@@ -129,6 +129,10 @@ def lib():
     L.cep_session_wave.argtypes = [P]
     L.cep_batch_attempts.argtypes = [P]
     L.cep_csr_check.argtypes = [C.POINTER(Matches), C.c_int64, C.c_int32]
+    L.cep_batch_id.argtypes = [P]
+    L.cep_batch_id.restype = C.c_int64
+    L.cep_batch_ready.argtypes = [P, C.c_int64]
+    L.cep_collect_batch.argtypes = [P, C.c_int64, C.POINTER(Matches)]
     L.cep_live_run_hwm.argtypes = [P, C.POINTER(C.c_int64)]
     L.cep_session_set_timing.argtypes = [P, C.c_int32]
     L.cep_batch_errors.argtypes = [P, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
@@ -282,13 +286,27 @@ class Session:
         self._keep = (key, cols, valid, topic, partition, offset, ts, colptrs, b)
         check(lib().cep_push_batch(self.h, C.byref(b), C.c_void_p(stream) if stream else None))
 
-    def collect(self, raise_on_error=True):
-        """Matches of the last batch as numpy arrays.  When the reference would have thrown
-        inside ``process()`` this raises ``CepError`` (code, record); with
-        ``raise_on_error=False`` the dict carries ``err``/``err_record`` instead, and the
-        matches emitted before ``err_record`` are the ones the reference forwarded."""
+    def batch_id(self) -> int:
+        """cep_batch_id: the number of the last pushed batch."""
+        return int(lib().cep_batch_id(self.h))
+
+    def batch_ready(self, batch_id: int) -> bool:
+        """cep_batch_ready: whether the batch's matches are complete (no wait)."""
+        rc = lib().cep_batch_ready(self.h, int(batch_id))
+        if rc not in (0, 1):                               # (CEP_E_ARG / CEP_E_HIP)
+            check(rc)
+        return rc == 1
+
+    def collect(self, raise_on_error=True, batch_id=None):
+        """Matches of the last batch (or, ``batch_id``: of the delivered batch before it, cep_collect_batch)
+        as numpy arrays.  When the reference would have thrown inside ``process()`` this raises
+        ``CepError`` (code, record); with ``raise_on_error=False`` the dict carries ``err``/``err_record``
+        instead, and the matches emitted before ``err_record`` are the ones the reference forwarded."""
         m = Matches()
-        check(lib().cep_collect(self.h, C.byref(m)))
+        if batch_id is None:
+            check(lib().cep_collect(self.h, C.byref(m)))
+        else:
+            check(lib().cep_collect_batch(self.h, int(batch_id), C.byref(m)))
         nm, ne = m.n_matches, m.n_entries
 
         def arr(p, n, dt):                                # one copy out of the library-owned CSR

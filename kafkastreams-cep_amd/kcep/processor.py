@@ -32,9 +32,10 @@ registers) plays the role of the reference's three stores.
   the task.
 * **Values** are decoded into the schema's typed columns by a
   ``kcep.ingest.ColumnDecoder``.
-* **Forward order.**  Each batch is stable-sorted by key for the device; the
-  matches are then put back into arrival order of their completing record
-  (stable, so one record's matches keep ``matchPattern``'s order).  The forwarded
+* **Forward order.**  Each batch goes to the device in arrival order
+  (``CEP_BATCH_ARRIVAL_ORDER``): the library groups it by key on the device and
+  returns the matches in arrival order of their completing record (one record's
+  matches in ``matchPattern``'s order), so the host sorts nothing.  The forwarded
   stream is therefore exactly the reference's, record for record -- only delayed
   to the flush.
 * **Errors.**  Where the reference throws out of ``process()`` (user-predicate
@@ -220,13 +221,12 @@ class GpuCEPProcessor:
 
     # ---- batching ----
     def _run(self, recs, idx):
-        """One cep_push_batch of the records ``recs[i] for i in idx`` (arrival indices, ascending),
-        grouped by key id.  Returns ``(matches, errors)``: per match (arrival index of the completing
-        record, key id, traversal entries as (name id, stream position)) in emission order, and per
-        failing key (arrival index, code)."""
+        """One cep_push_batch of the records ``recs[i] for i in idx`` (arrival indices, ascending), in
+        arrival order (the device groups them by key).  Returns ``(matches, errors)``: per match (arrival
+        index of the completing record, key id, traversal entries as (name id, stream position)) in
+        forward order, and per failing key (arrival index, code)."""
         n = len(idx)
-        kid = self._kid[idx]
-        perm = np.asarray(idx, np.int64)[np.argsort(kid, kind="stable")]   # arrival index of batch position
+        perm = np.asarray(idx, np.int64)                  # arrival index of batch position
         sorted_recs = [recs[i] for i in perm]
         cols = self.decoder.columns([r[1] for r in sorted_recs])
         topic = np.fromiter((r[2] for r in sorted_recs), np.int32, n)
@@ -237,8 +237,8 @@ class GpuCEPProcessor:
         for i, r in enumerate(sorted_recs):
             self._log[base + i] = r[6]
         try:
-            self.session.push(n, self._kid[perm], cols, topic=topic, partition=part, offset=off, ts=ts,
-                              flags=self._flags | N.BATCH_DELIVER)
+            self.session.push(n, np.ascontiguousarray(self._kid[perm]), cols, topic=topic, partition=part, offset=off,
+                              ts=ts, flags=self._flags | N.BATCH_DELIVER | N.BATCH_ARRIVAL_ORDER)
             out = self.session.collect(raise_on_error=False)
         except N.CepError as e:                           # no state was committed for this batch:
             self._failed = e                              # the task fails, as the reference's does
@@ -305,7 +305,8 @@ class GpuCEPProcessor:
                 raise self._failed
             matches += m2
             errors += e2
-        matches.sort(key=lambda m: m[0])                  # arrival order of the completing record (stable)
+        if cap:                                           # (each push's matches already come in arrival order)
+            matches.sort(key=lambda m: m[0])              # arrival order of the completing record (stable)
         limit = err_code = None
         if errors:                                        # the first failure in ARRIVAL order (cep_batch_errors)
             limit, err_code = min(errors)

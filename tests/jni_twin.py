@@ -28,6 +28,7 @@ NATIVES = ["cepCompile", "cepStageNames", "cepSessionOpen", "cepSessionPath", "c
 
 CEP_MODE_PROCESSOR, CEP_SESSION_CARRY, CEP_E_RUN_CAPACITY = 1, 1, 9
 CEP_PATH_STENCIL, CEP_PATH_CHAIN, CEP_PATH_RUNS, CEP_BATCH_OFFSETS_MONOTONE, CEP_BATCH_DELIVER = 1, 3, 4, 1, 2
+CEP_BATCH_ARRIVAL_ORDER = 4
 
 
 class JniLib:
@@ -54,7 +55,7 @@ class JniLib:
             "cepCompile": (C.c_int64, [P]),
             "cepStageNames": (P, [C.c_int64]),
             "cepSessionOpen": (C.c_int64, [C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_int64,
-                                           C.c_int64]),
+                                           C.c_int64, C.c_int64]),
             "cepSessionPath": (C.c_int32, [C.c_int64]),
             "cepPushBatch": (C.c_int32, [C.c_int64, C.c_int32, P, P, P, P, P, P, P, C.c_int32]),
             "cepCollect": (C.c_int64, [C.c_int64, P, P, P, P, P, P]),
@@ -112,8 +113,9 @@ class JniLib:
         o = self._cepStageNames(self.env, None, pattern)
         return [self.string(self.L.mock_obj_get(o, i)) for i in range(self.L.mock_len(o))]
 
-    def cepSessionOpen(self, pattern, device, mode, max_events, flags, max_keys, max_key_words) -> int:
-        return self._cepSessionOpen(self.env, None, pattern, device, mode, max_events, flags, max_keys, max_key_words)
+    def cepSessionOpen(self, pattern, device, mode, max_events, flags, max_keys, max_key_words, max_pool_bytes=0) -> int:
+        return self._cepSessionOpen(self.env, None, pattern, device, mode, max_events, flags, max_keys, max_key_words,
+                                    max_pool_bytes)
 
     def cepSessionPath(self, session) -> int:
         return self._cepSessionPath(self.env, None, session)
@@ -174,7 +176,8 @@ class JavaTwin:
     (key, [column values], topic, partition, offset, timestamp); the decoder is the identity on
     the per-column values with Java types ``types`` (1 int32, 2 int64, 3 double)."""
 
-    def __init__(self, jl: JniLib, ir: bytes, types, batch_size, max_keys, max_key_words=0, prune_at=None):
+    def __init__(self, jl: JniLib, ir: bytes, types, batch_size, max_keys, max_key_words=0, prune_at=None,
+                 max_pool_bytes=0):
         self.j = jl
         self.types = list(types)
         self.batch_size = batch_size
@@ -183,7 +186,7 @@ class JavaTwin:
         self.pattern = self._check(jl.cepCompile(ir))
         self.names = jl.cepStageNames(self.pattern)
         self.session = self._check(jl.cepSessionOpen(self.pattern, 0, CEP_MODE_PROCESSOR, batch_size,
-                                                     CEP_SESSION_CARRY, max_keys, max_key_words))
+                                                     CEP_SESSION_CARRY, max_keys, max_key_words, max_pool_bytes))
         self.path = jl.cepSessionPath(self.session)
         self.key_ids, self.id_keys, self.free_ids = {}, {}, []
         self.next_id = 0
@@ -222,7 +225,7 @@ class JavaTwin:
     def _run(self, recs, kid, idx, flags):
         j = self.j
         n = len(idx)
-        order = sorted(idx, key=lambda a: kid[a])           # stable: arrival order per key
+        order = list(idx)                                   # arrival order: the device groups by key
         key_id = np.array([kid[a] for a in order], np.int32)
         topic = np.array([self._topic(recs[a][2]) for a in order], np.int32)
         part = np.array([recs[a][3] for a in order], np.int32)
@@ -234,7 +237,7 @@ class JavaTwin:
         for jj, a in enumerate(order):
             self.log[base + jj] = recs[a]
         rc = j.cepPushBatch(self.session, n, key_id, topic, part, off, ts, np.array(self.types, np.int32), cols,
-                            flags | CEP_BATCH_DELIVER)
+                            flags | CEP_BATCH_DELIVER | CEP_BATCH_ARRIVAL_ORDER)
         self.pushes += 1
         if rc != 0:
             raise RuntimeError(f"cepPushBatch {rc}: {j.cepLastError()}")

@@ -185,3 +185,30 @@ def test_arrival_checksum_and_export_speak_arrival_positions():
             flags=N.BATCH_ARRIVAL_ORDER | N.BATCH_OFFSETS_MONOTONE)
     got2 = product_matches(s2, s2.collect())
     assert got1 + got2 == want and len(got2) > 0
+
+
+@pytest.mark.parametrize("name,mk", [("c2_strict", synth.c2_pattern), ("c5_optional", PL.c5_optional)])
+def test_pipelined_flushes_collect_the_batch_before(name, mk):
+    """cep_collect_batch: a stencil / chain carry session delivers each batch into one of two host buffers,
+    so batch i + 1 is pushed before batch i is collected; the joined output is the unpipelined one."""
+    key, val = stream(name, 9, 200, 20, 64 if name == "c5_optional" else 4)
+    ir = mk().to_ir(PL.I32)
+    want, _ = oracle_run(ir, key, [val], [1])
+    sess = N.Session(N.CompiledPattern(ir), 700, carry=True, max_keys=200)
+    bounds = list(range(0, len(key), 613)) + [len(key)]
+    got, prev = [], None
+    flags = N.BATCH_ARRIVAL_ORDER | N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        sess.push(b - a, np.ascontiguousarray(key[a:b]), [np.ascontiguousarray(val[a:b])], flags=flags)
+        if prev is not None:
+            got += product_matches(sess, sess.collect(batch_id=prev))
+        prev = sess.batch_id()
+    import time
+    t0 = time.time()
+    while not sess.batch_ready(prev) and time.time() - t0 < 10:
+        time.sleep(0.001)
+    assert sess.batch_ready(prev)
+    got += product_matches(sess, sess.collect(batch_id=prev))
+    assert got == want and len(want) > 0
+    with pytest.raises(N.CepError):                     # only the last batch and the one before it
+        sess.collect(batch_id=prev - 2)

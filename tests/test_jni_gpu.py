@@ -88,7 +88,7 @@ def test_unflagged_stencil_carry_batch_is_refused(jl):
     to its halo and refuses the batch -- what every round-2 Java flush of C2/C5 hit."""
     ir = synth.c2_pattern().to_ir(PL.I32)
     p = jl.cepCompile(ir)
-    s = jl.cepSessionOpen(p, 0, 1, 16, 1, 4, 0)
+    s = jl.cepSessionOpen(p, 0, 1, 16, 1, 4, 0, 0)
     assert s > 0 and jl.cepSessionPath(s) == 1
     z = np.zeros(4, np.int32)
     args = (s, 4, np.array([0, 0, 1, 1], np.int32), z, z, np.arange(4, dtype=np.int64), np.arange(4, dtype=np.int64),

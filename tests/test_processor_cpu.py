@@ -68,7 +68,10 @@ class StubSession:
     def stream_position(self):
         return self.pos
 
-    def push(self, n, key, cols, topic=None, partition=None, offset=None, ts=None, **kw):
+    def push(self, n, key, cols, topic=None, partition=None, offset=None, ts=None, flags=0, **kw):
+        # the processor hands its batches over in arrival order (CEP_BATCH_ARRIVAL_ORDER): the device groups
+        # them and answers in arrival order of the completing record, errors ascending -- as this stub does
+        assert flags & N.BATCH_ARRIVAL_ORDER
         self.pushes.append(dict(key=key.copy(), val=cols[0].copy(), offset=offset.copy(), topic=topic.copy()))
         rec, ents = [], []
         err, err_rec = 0, -1
@@ -108,7 +111,7 @@ def make(batch, stub):
     return p, got
 
 
-def test_processor_batches_grouped_and_forwarded_in_arrival_order():
+def test_processor_batches_in_arrival_order_and_forwarded_in_arrival_order():
     stub = StubSession(complete={7})
     p, got = make(6, stub)
     assert p.queryName == "my queryname"               # toLowerCase + literal replace of "\s+"
@@ -118,8 +121,8 @@ def test_processor_batches_grouped_and_forwarded_in_arrival_order():
         p.process(k, v, "events", 0, o, 100 + o)
     assert len(stub.pushes) == 1                        # nulls never reach the buffer: 6 records flushed
     b = stub.pushes[0]
-    assert list(b["key"]) == [0, 0, 1, 1, 2, 2]         # grouped by interned key, stable
-    assert list(b["offset"]) == [0, 6, 1, 4, 5, 7]
+    assert list(b["key"]) == [0, 1, 1, 2, 0, 2]         # interned keys, in arrival order (the device groups)
+    assert list(b["offset"]) == [0, 1, 4, 5, 6, 7]
     p.close()
     assert stub.closed
     # arrival order of the completing records: 0 (b), 4 (a), 5 (c), 6 (b)
@@ -141,16 +144,16 @@ def test_processor_error_truncates_and_fails():
 
 
 def test_processor_error_is_first_in_arrival_order():
-    """Two keys fail in one batch; the key-grouped batch puts the later-arriving failure first.
-    The processor must fail where the reference does: at the earliest arrival."""
+    """Two keys fail in one batch; the processor must fail where the reference does: at the earliest
+    arrival (the device reports the batch's exceptions in arrival order, CEP_BATCH_ARRIVAL_ORDER)."""
     stub = StubSession(complete={7}, err_value=9)
     p, got = make(100, stub)
     for k, v, o in [("a", 7, 0), ("b", 9, 1), ("a", 9, 2), ("a", 7, 3)]:
         p.process(k, v, "events", 0, o, o)
     with pytest.raises(N.CepError) as ei:
         p.flush()
-    assert stub.out["err_record"] == 1                  # grouped order: a0 a2 a3 b1 -> a2 reported first
-    assert ei.value.record == 1 and ei.value.code == 4  # but b1 arrived first
+    assert stub.out["err_record"] == 1
+    assert ei.value.record == 1 and ei.value.code == 4  # b1 arrived first
     assert got == [("a", [("$final", [0])])]
 
 

@@ -27,9 +27,9 @@ def test_builder_routes_topics_and_assigns_offsets():
     s1, s2 = stubs
     assert len(s1.pushes) == 1 and len(s2.pushes) == 1
     p1, p2 = s1.pushes[0], s2.pushes[0]
-    assert list(p1["key"]) == [0, 0, 1, 1]              # grouped by key: x, x, y, y
-    assert list(p1["offset"]) == [0, 1, 0, 1]           # offsets per (topic, partition)
-    assert list(p1["topic"]) == [0, 0, 1, 1]            # source topics interned first: t1=0, t2=1
+    assert list(p1["key"]) == [0, 1, 0, 1]              # arrival order (the device groups): x, y, x, y
+    assert list(p1["offset"]) == [0, 0, 1, 1]           # offsets per (topic, partition)
+    assert list(p1["topic"]) == [0, 1, 0, 1]            # source topics interned first: t1=0, t2=1
     assert list(p2["offset"]) == [0, 1] and list(p2["key"]) == [0, 0]
     assert got1 == ["x", "y"]                           # q1's forwards, in arrival order
     drv.close()

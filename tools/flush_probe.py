@@ -25,7 +25,12 @@ nb = int(sys.argv[2]) if len(sys.argv) > 2 else 200
 n = per * nb
 K = max(1000, n // 100)
 dev = torch.device("cuda", 0)
-key, val, _ = synth.c2_stream_torch(n, K, dev)
+key, val, order = synth.c2_stream_torch(n, K, dev)
+# the same records in arrival (generation) order: keys interleaved, for CEP_BATCH_ARRIVAL_ORDER
+akey, aval = torch.empty_like(key), torch.empty_like(val)
+akey[order] = key
+aval[order] = val
+ak, av = akey.cpu().pin_memory(), aval.cpu().pin_memory()
 ir = synth.c2_pattern().to_ir(Schema([("value", "i32")]))
 pat = N.CompiledPattern(ir)
 st = torch.cuda.current_stream(dev)
@@ -76,9 +81,15 @@ subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "
                 "-I", os.path.join(ROOT, "include"), "-L", os.path.dirname(N.LIB_PATH), "-l:libkcep.so",
                 "-Wl,-rpath," + os.path.dirname(N.LIB_PATH)], check=True)
 fl = C.CDLL(so)
-fl.flush_loop.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
-                          C.POINTER(C.c_double)]
-for label, kp, vp in (("pinned", pk.data_ptr(), pv.data_ptr()), ("pageable", hk.ctypes.data, hv.ctypes.data)):
+for f in (fl.flush_loop, fl.flush_loop_pipelined):
+    f.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                  C.POINTER(C.c_double)]
+A = N.BATCH_ARRIVAL_ORDER
+for label, kp, vp, xf, loop in (("pinned", pk.data_ptr(), pv.data_ptr(), 0, fl.flush_loop),
+                                ("pageable", hk.ctypes.data, hv.ctypes.data, 0, fl.flush_loop),
+                                ("pinned arrival", ak.data_ptr(), av.data_ptr(), A, fl.flush_loop),
+                                ("pinned arrival pipelined", ak.data_ptr(), av.data_ptr(), A, fl.flush_loop_pipelined),
+                                ("pinned grouped pipelined", pk.data_ptr(), pv.data_ptr(), 0, fl.flush_loop_pipelined)):
     s = N.Session(pat, per, mode=N.MODE_PROCESSOR, carry=True, max_keys=K)
     s.set_timing(False)
     best = None
@@ -86,12 +97,12 @@ for label, kp, vp in (("pinned", pk.data_ptr(), pv.data_ptr()), ("pageable", hk.
         s.state_clear()
         torch.cuda.synchronize()
         o = (C.c_double * 4)()
-        rc = fl.flush_loop(s.h, nb, per, kp, vp, N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER, st.cuda_stream, o)
+        rc = loop(s.h, nb, per, kp, vp, N.BATCH_OFFSETS_MONOTONE | N.BATCH_DELIVER | xf, st.cuda_stream, o)
         assert rc == 0, rc
         if best is None or o[0] < best[0]:
             best = list(o)
     dt, tp, tc, tot = best
-    print(f"C loop {label:9s} per={per} batches={nb}: {dt / nb:8.1f} us/batch  push {tp / nb:7.1f}  "
+    print(f"C loop {label:25s} per={per} batches={nb}: {dt / nb:8.1f} us/batch  push {tp / nb:7.1f}  "
           f"collect {tc / nb:7.1f}  {n / (dt * 1e-6):.3e} events/s  matches {int(tot)} (same: {int(tot) == want})",
           flush=True)
     s.close()
