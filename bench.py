@@ -419,7 +419,7 @@ def main(argv=None):
             # device (CEP_BATCH_ARRIVAL_ORDER) and hands the matches back in arrival order
             line["processor_batches"] += [
                 _arrival_batches(pat, n, K, key, cols, ts, stream, n_matches, csum, value / world, per=b, pipelined=p)
-                for b in args.processor_batch[:1] for p in (False, True)]
+                for b in args.processor_batch for p in (False, True)]
         if world == 1 and sess.path in (N.PATH_STENCIL, N.PATH_CHAIN, N.PATH_RUNS) and args.carry_batches > 1:
             line["carry_stream"] = _carry_stream(pat, n, K, key, cols, stream, args.carry_batches, n_matches, csum,
                                                  value / world)
