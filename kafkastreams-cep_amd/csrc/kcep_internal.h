@@ -147,6 +147,9 @@ struct StencilCarry {
                                      // bit 2: chain carry batch beyond a tile's match space
   const int64_t* gpos;               // stream position of each batch record (CEP_BATCH_ARRIVAL_ORDER: base + its
                                      // arrival index); null: base + record index
+  int32_t grouped;                   // the device grouped the batch (CEP_BATCH_ARRIVAL_ORDER): each key is one
+                                     // segment by construction, no claims (for an interleaved flush nearly every
+                                     // record starts a segment, and its returning atomic was waited for in turn)
 };
 KCEP_HD inline int64_t halo_gpos(const StencilCarry& C, int64_t r) { return C.gpos ? C.gpos[r] : C.base + r; }
 KCEP_HD inline int halo_old(const HaloHdr& h, int32_t stamp) {

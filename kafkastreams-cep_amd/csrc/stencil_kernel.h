@@ -509,6 +509,7 @@ __global__ __launch_bounds__(ST_THREADS) void stencil_kernel(
           okb = kb != ka && key_ok(C, kb);
           ra = halo_load(C, oka ? ka : 0);
           rb = halo_load(C, okb ? kb : 0);
+          if (C.grouped) starts = 0;
           while (starts) {                                 // claims, checked after the visits
             const int i = __ffs(starts) - 1;
             starts &= starts - 1;
@@ -1007,7 +1008,7 @@ __global__ __launch_bounds__(ST_THREADS, CARRY ? ST_CARRY_WAVES : ST_PLAIN_WAVES
         const int32_t ka = key_of(__ffs(todo) - 1), kb = key_of(31 - __clz(todo));
         const bool oka = key_ok(C, ka), okb = kb != ka && key_ok(C, kb);
         const HaloRaw ra = halo_load(C, oka ? ka : 0), rb = halo_load(C, okb ? kb : 0);
-        uint32_t st = starts;
+        uint32_t st = C.grouped ? 0u : starts;
         while (st) {                              // claims
           const int i = __ffs(st) - 1;
           st &= st - 1;
