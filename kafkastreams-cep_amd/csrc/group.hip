@@ -4,8 +4,8 @@
 // emits them (:148).  Neither the JVM nor the Python host sorts anything.
 //
 //   grouping: a stable grouping by key id without a sort, in three kernels and a scan (group_launch):
-//     group_chunks  one wave per chunk of 1024 consecutive records: an LDS hash table of the chunk's keys
-//                   gives every record its rank among the chunk's earlier records of its key (16 rounds of
+//     group_chunks  one wave per chunk of 256 / 1024 consecutive records: an LDS hash table of the chunk's keys
+//                   gives every record its rank among the chunk's earlier records of its key (rounds of
 //                   64 records; a round's lanes of one key found by an LDS bit mask, not by lane order), and
 //                   every (chunk, key) pair becomes a node pushed onto the key's list (an epoch-tagged head
 //                   per key id: nothing is cleared between batches)
@@ -36,8 +36,8 @@ __device__ __forceinline__ void copy_col(const void* src, void* dst, int type, i
   else static_cast<int64_t*>(dst)[to] = static_cast<const int64_t*>(src)[from];
 }
 
-constexpr int GR_CHUNK = 1024;                   // records per wave
-constexpr int GR_TAB = 2048;                     // LDS hash slots per wave
+// records per wave (a chunk): 1024, or 256 for batches up to 2^18 records (four times the waves: a 64 k-record
+// flush took 27 us with 64 of them); a key's node list is at most the batch's chunks long
 constexpr int32_t GR_EMPTY = -2;                 // (invalid key ids are all -1: one group, the batch fails later)
 
 __device__ __forceinline__ uint32_t gr_hash(int32_t k) {
@@ -46,12 +46,14 @@ __device__ __forceinline__ uint32_t gr_hash(int32_t k) {
   return h;
 }
 
+template <int GR_CHUNK>
 __global__ __launch_bounds__(64) void group_chunks(const int32_t* __restrict__ key, int64_t n, int32_t max_keys,
                                                    uint32_t stamp, unsigned long long* __restrict__ head,
                                                    int32_t* __restrict__ node_top, int32_t* __restrict__ node_key,
                                                    int32_t* __restrict__ node_chunk, int32_t* __restrict__ node_cnt,
                                                    int32_t* __restrict__ node_next, int32_t* __restrict__ rec_node,
                                                    int32_t* __restrict__ rec_rank) {
+  constexpr int GR_TAB = 2 * GR_CHUNK;           // LDS hash slots (at most half full)
   __shared__ int32_t tkey[GR_TAB];
   __shared__ int32_t tcnt[GR_TAB];               // the key's records so far; at the end: its node
   __shared__ unsigned long long tmask[GR_TAB];   // the round's lanes of the key
@@ -288,9 +290,14 @@ __global__ __launch_bounds__(256) void stencil_arrival_count(const int32_t* __re
 // node and record arrays, G.node_top and G.cursor zeroed once (group_gather re-zeroes them)
 hipError_t group_launch(const GroupArgs& G, int64_t n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const unsigned chunks = unsigned((n + GR_CHUNK - 1) / GR_CHUNK);
-  hipLaunchKernelGGL(group_chunks, dim3(chunks), dim3(64), 0, st, G.key, n, G.max_keys, G.stamp, G.head, G.node_top,
-                     G.node_key, G.node_chunk, G.node_cnt, G.node_next, G.rec_node, G.rec_rank);
+  if (n <= (int64_t(1) << 18)) {
+    hipLaunchKernelGGL(group_chunks<256>, dim3(unsigned((n + 255) / 256)), dim3(64), 0, st, G.key, n, G.max_keys, G.stamp,
+                       G.head, G.node_top, G.node_key, G.node_chunk, G.node_cnt, G.node_next, G.rec_node, G.rec_rank);
+  } else {
+    hipLaunchKernelGGL(group_chunks<1024>, dim3(unsigned((n + 1023) / 1024)), dim3(64), 0, st, G.key, n, G.max_keys,
+                       G.stamp, G.head, G.node_top, G.node_key, G.node_chunk, G.node_cnt, G.node_next, G.rec_node,
+                       G.rec_rank);
+  }
   hipLaunchKernelGGL(group_nodes, dim3(blocks256(n)), dim3(256), 0, st, n, G.node_top, G.max_keys, G.head, G.node_key,
                      G.node_chunk, G.node_cnt, G.node_next, G.node_prefix, G.node_leader, G.start, G.cursor);
   hipLaunchKernelGGL(group_gather, dim3(blocks256(n)), dim3(256), 0, st, G, n);
