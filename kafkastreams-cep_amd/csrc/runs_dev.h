@@ -161,6 +161,36 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int3
       continue;
     }
     const int32_t gs = alive ? r : i0;                          // a loadable record for idle lanes (JitTab)
+#ifdef KCEP_JIT
+    // Every stage's edge predicates at once, on the record and the run state as the sweep finds them.  A
+    // lane's state changes only when it consumes, after which it evaluates nothing more in the sweep, and a
+    // PROCEED stays on the same record: these are the values the stage loop would compute where the run
+    // goes, and in one basic block the compiler shares their subexpressions across stages (C3: the running
+    // average's divide once per record instead of once per visited stage).  Predicates have no side
+    // effects; a stage's first failing edge (later edges inactive, matchEdgesAndGet NFA.java:371-384)
+    // raises only where the run visits the stage.
+    uint32_t pre_m[NFA_MAX_STAGES];
+    int pre_e[NFA_MAX_STAGES];
+    KCEP_UNROLL
+    for (int s = nst - 1; s >= 1; s--) {
+      const auto& st = P.st[s];
+      uint32_t matched = 0;
+      int err = 0;
+      KCEP_UNROLL
+      for (int e = 0; e < st.nedges; e++) {
+        if (st.pred[e] < 0) { matched |= 1u << e; continue; }
+        RunEnv env{A, gs, rs, 0, false, 0, 0, cv};
+        int64_t v;
+        if (!T.eval(st.pred[e], env, true, v)) {
+          if (!err) err = env.err ? env.err : CEP_E_BAD_IR;
+        } else if (!err && v) {
+          matched |= 1u << e;
+        }
+      }
+      pre_m[s] = matched;
+      pre_e[s] = err;
+    }
+#endif
     KCEP_UNROLL
     for (int s = nst - 1; s >= 1; s--) {
       const bool here = alive && ps == s;
@@ -168,6 +198,10 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int3
       const auto& st = P.st[s];
       uint32_t matched = 0;
       bool ok = true;
+#ifdef KCEP_JIT
+      matched = pre_m[s];
+      if (here && pre_e[s]) { ok = false; res.err = pre_e[s]; }
+#else
       KCEP_UNROLL
       for (int e = 0; e < st.nedges; e++) {
         if (st.pred[e] < 0) { matched |= 1u << e; continue; }
@@ -180,6 +214,7 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int3
           matched |= 1u << e;
         }
       }
+#endif
       int take = -1, rec = -1;
       KCEP_UNROLL
       for (int e = 0; e < st.nedges; e++)
