@@ -191,6 +191,9 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int3
       pre_e[s] = err;
     }
 #endif
+    // the stage a lane consumed at in this sweep: it evaluates nothing more in the sweep, so on_consume
+    // runs once after the stage loop (one copy of its branches instead of one per unrolled stage)
+    int cstage = -1;
     KCEP_UNROLL
     for (int s = nst - 1; s >= 1; s--) {
       const bool here = alive && ps == s;
@@ -215,52 +218,55 @@ __device__ __forceinline__ void run_engine(const Tab& T, const RunsArgs& A, int3
         }
       }
 #endif
-      int take = -1, rec = -1;
+      // the last matching consuming edge's target and the last matching recursion edge's (-2: none),
+      // as selects: the stage's edges and ops are constants in a per-pattern kernel
+      int take = -1, tk_to = 0, rec_to = -2;
       KCEP_UNROLL
-      for (int e = 0; e < st.nedges; e++)
-        if ((matched >> e) & 1) {
-          const int op = st.op[e];
-          if (op == E_BEGIN || op == E_TAKE) take = e;
-          else if (op == E_PROCEED || op == E_SKIP_PROCEED) rec = e;
+      for (int e = 0; e < st.nedges; e++) {
+        const bool m = (matched >> e) & 1;
+        const int op = st.op[e];
+        if (op == E_BEGIN || op == E_TAKE) {
+          const int to = op == E_TAKE ? s : st.target[e];
+          take = m ? e : take;
+          tk_to = m ? to : tk_to;
+        } else if (op == E_PROCEED || op == E_SKIP_PROCEED) {
+          rec_to = m ? st.target[e] : rec_to;
         }
+      }
       const bool consume = here && ok && take >= 0;
-      KCEP_UNROLL
-      for (int f = 0; f < st.nfolds; f++) {                      // evaluateAggregates (:362-369)
-        if (!wave_any(consume && ok)) break;
-        const int sidx = st.fold_state[f];
-        int32_t ct = 0;
-        int64_t cvv = 0;
+      // evaluateAggregates (:362-369): a fold that raises stops the later ones; the state updates as selects
+      if (st.nfolds > 0 && wave_any(consume)) {
+        KCEP_UNROLL
+        for (int f = 0; f < st.nfolds; f++) {
+          const int sidx = st.fold_state[f];
+          int32_t ct = 0;
+          int64_t cvv = 0;
 #pragma unroll
-        for (int q = 0; q < RUNS_MAX_STATES; q++)
-          if (q == sidx) { ct = rs.tag[q]; cvv = rs.val[q]; }
-        RunEnv env{A, gs, rs, 0, true, ct, cvv, cv};
-        int64_t v;
-        const bool act = consume && ok;
-        if (!T.eval(st.fold_code[f], env, act, v)) {
-          if (act) { ok = false; res.err = env.err; }
-        } else if (act) {
+          for (int q = 0; q < RUNS_MAX_STATES; q++)
+            if (q == sidx) { ct = rs.tag[q]; cvv = rs.val[q]; }
+          RunEnv env{A, gs, rs, 0, true, ct, cvv, cv};
+          int64_t v = 0;
+          const bool act = consume && ok;
+          const bool good = T.eval(st.fold_code[f], env, act, v);
+          const bool put = act && good;
+          res.err = act && !good ? env.err : res.err;
+          ok = act && !good ? false : ok;
           const int32_t ft = st.fold_type[f];
 #pragma unroll
           for (int q = 0; q < RUNS_MAX_STATES; q++)
-            if (q == sidx) { rs.tag[q] = ft; rs.val[q] = v; }
+            if (q == sidx) { rs.tag[q] = put ? ft : rs.tag[q]; rs.val[q] = put ? v : rs.val[q]; }
         }
       }
-      if (here) {
-        if (!ok) {
-          res.fail_at = r;
-          ps = -2;                                                 // finished
-        } else if (take >= 0) {
-          on_consume(idx, r, s);
-          cur = st.op[take] == E_TAKE ? s : st.target[take];
-          ps = -1;
-          if (cur == 0) { res.end = r; ps = -2; }                // forwarding to $final: emitted
-        } else if (rec >= 0) {
-          ps = st.target[rec];
-        } else {
-          ps = -2;                                                 // no edge: the run is removed
-        }
-      }
+      // the lane's move, branch-free: failed -> finished; consumed -> the next record, or emitted when the
+      // edge forwards to $final; a recursion edge -> its target on the same record; no edge -> removed
+      const bool cons = here && ok && take >= 0;
+      res.fail_at = here && !ok ? r : res.fail_at;
+      res.end = cons && tk_to == 0 ? r : res.end;
+      cstage = cons ? s : cstage;
+      cur = cons ? tk_to : cur;
+      ps = !here ? ps : !ok ? -2 : take >= 0 ? (tk_to == 0 ? -2 : -1) : rec_to;
     }
+    if (cstage >= 0) on_consume(idx, r, cstage);
     if (alive) {
       if (ps == -1) {                                              // consumed: on to the next record
         r++;
