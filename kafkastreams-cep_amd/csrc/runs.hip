@@ -280,7 +280,17 @@ __global__ __launch_bounds__(256) void runs_expand(const DevProgram* __restrict_
 // contiguous entry range, each entry's stage from its run's packed segments.  Replaces runs_compact +
 // runs_order + the entry-offset scan + runs_expand (one pass over end_of and the segments instead of a
 // start-ordered list, a sorted copy, a length array and gathers at start positions).
+#ifndef RUNS_EMIT_PROBE
+#define RUNS_EMIT_PROBE 0                          // timing probes (A/B builds only): 1 no output, 2 headers only
+#endif
 constexpr int RUNS_EMIT_MAX = 2 * RUNS_CHUNK;      // window of starts: chunk + span < 2 chunks
+constexpr int EMIT_T = 2048;                       // entries per pass of the entry phase (8 per thread)
+static_assert(RUNS_EMIT_MAX <= 65536, "run indices are 16-bit in the entry phase");
+// SEG4: 4-word segment records (staged in LDS); POS: stream positions from pos[] (else base + record).
+// Template flags, not run-time branches: a branch that may load from global memory makes the compiler
+// wait for every outstanding memory operation -- this loop's own stores included -- before the merged
+// value is used, one store round trip per entry pass
+template <bool SEG4, bool POS>
 __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ P, const int32_t* __restrict__ key,
                                                  const int64_t* __restrict__ pos, int64_t base,
                                                  const uint16_t* __restrict__ segs, int segn,
@@ -296,10 +306,12 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   int32_t* const s_run = reinterpret_cast<int32_t*>(s_seg + WN);   // window offset of the start | end slot << 11
   int32_t* const s_at = s_run + WN;                // the runs' entry offsets in the chunk (WN + 1) ...
   int32_t* const s_fill = s_at;                    // ... and, before them, the end slots' fill cursors
-  int32_t* const s_cnt = s_at + WN + 1;            // end slot counts, then their prefix (chunk + 1)
+  // end slot counts, then their prefix (chunk + 1 <= WN words): in s_seg's space, which is written only
+  // after the runs are sorted (one 4 KB array less: 8 workgroups per CU instead of 7 at C3's span)
+  int32_t* const s_cnt = reinterpret_cast<int32_t*>(s_seg);
   __shared__ int32_t s_w[4];
   __shared__ int32_t s_name[16];
-  __shared__ unsigned long long s_mask[4];         // per wave: the run starts of its entry window
+  __shared__ __attribute__((aligned(16))) uint16_t s_of[EMIT_T];   // per entry of the pass: its run
   const int tid = threadIdx.x;
   const int64_t c = blockIdx.x, c0 = c * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
   if (tid < 16) s_name[tid] = tid < P->nstages ? P->st[tid].name : 0;
@@ -309,10 +321,17 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   for (int x = tid; x < E; x += 256) { s_cnt[x] = 0; s_fill[x] = 0; }
   __syncthreads();
   int32_t my[RUNS_EMIT_MAX / 256];                 // this thread's window entries: end slot, or -1
+  // the loads at clamped (always valid) addresses, all in flight together: a load under `x < L` was a
+  // branch each, waited on inside it -- eight memory round trips in a row
 #pragma unroll
   for (int q = 0; q < RUNS_EMIT_MAX / 256; q++) {
     const int x = tid + 256 * q;
-    const int64_t e = x < L ? int64_t(end_of[lo + x]) : -1;
+    my[q] = end_of[lo + (x < L ? x : L - 1)];
+  }
+#pragma unroll
+  for (int q = 0; q < RUNS_EMIT_MAX / 256; q++) {
+    const int x = tid + 256 * q;
+    const int64_t e = x < L ? int64_t(my[q]) : -1;
     my[q] = e >= c0 && e < c1 ? int32_t(e - c0) : -1;
   }
 #pragma unroll
@@ -386,58 +405,96 @@ __global__ __launch_bounds__(256) void runs_emit(const DevProgram* __restrict__ 
   }
   if (tid == 0) s_at[M] = NE;
   __syncthreads();
+  if (RUNS_EMIT_PROBE == 1) return;                // timing probes only (tools/variants.sh): no output
   // match headers, and every run's segments into LDS (all loads of the pass in flight together)
   const int64_t mb = pre[c], eb = pre[W + c];
-  for (int i = tid; i < M; i += 256) {
-    const int32_t r = s_run[i];
-    const int64_t e = c0 + (r >> 11);
-    if (segn == 4) s_seg[i] = *reinterpret_cast<const uint2*>(segs + (lo + (r & 2047)) * 4);
-    match_record[mb + i] = pos ? pos[e] : base + e;
-    match_key[mb + i] = key[e];
-    ent_off[mb + i] = eb + s_at[i];
+  if (M > 0) {                                     // (uniform) loads at clamped indices first, then the stores
+    uint2 sv[RUNS_EMIT_MAX / 256];
+    int32_t kv[RUNS_EMIT_MAX / 256];
+    int64_t pv[POS ? RUNS_EMIT_MAX / 256 : 1];
+#pragma unroll
+    for (int q = 0; q < RUNS_EMIT_MAX / 256; q++) {
+      const int i = tid + 256 * q;
+      const int32_t r = s_run[i < M ? i : M - 1];
+      const int64_t e = c0 + (r >> 11);
+      if (SEG4) sv[q] = *reinterpret_cast<const uint2*>(segs + (lo + (r & 2047)) * 4);
+      kv[q] = key[e];
+      if constexpr (POS) pv[q] = pos[e];
+    }
+#pragma unroll
+    for (int q = 0; q < RUNS_EMIT_MAX / 256; q++) {
+      const int i = tid + 256 * q;
+      if (i < M) {
+        const int64_t e = c0 + (s_run[i] >> 11);
+        if (SEG4) s_seg[i] = sv[q];
+        if constexpr (POS) match_record[mb + i] = pv[q];
+        else match_record[mb + i] = base + e;
+        match_key[mb + i] = kv[q];
+        ent_off[mb + i] = eb + s_at[i];
+      }
+    }
   }
   __syncthreads();
-  // the entries: each wave a quarter of the chunk's range, 64 consecutive entries per step (coalesced
-  // stores).  A lane finds its run from the window's run starts: the runs after the window's first one
-  // set their start's bit in a per-wave LDS mask, and a lane's run is the first one plus the starts at or
-  // before it (a popcount) -- one binary search per wave instead of one per entry.  (A binary search per
-  // entry: 222 us on C3; a per-run layout loop, one thread walking each of its runs' entries, diverged on
-  // the long runs: 714 us.)
-  const int wv = tid >> 6, lane = tid & 63;
-  const int per = ((NE + 3) / 4 + 63) & ~63;
-  const int x0 = wv * per, x1 = x0 + per < NE ? x0 + per : NE;
-  if (x0 < x1) {
-    int q0 = 0, b = M - 1;                         // the run holding entry x0
-    while (q0 < b) {
-      const int mid = (q0 + b + 1) >> 1;
-      if (s_at[mid] <= x0) q0 = mid; else b = mid - 1;
+  if (RUNS_EMIT_PROBE == 2) return;
+  // the entries, EMIT_T at a time: each run's index scattered at its first entry's offset in the window
+  // (and the run going on from the previous window at offset 0), an inclusive max-scan over the window
+  // gives every entry its run, then each thread writes entries tid, tid + 256, ... (coalesced stores, the
+  // window's LDS reads independent of each other).  (Was: per wave, 64 entries at a time, their runs from
+  // a bit mask of the run starts built by LDS atomics -- a chain of dependent LDS round trips and two wave
+  // barriers per 64 entries: 133 of runs_emit's 206 us on C3.  Before that: a binary search per entry,
+  // 222 us; one thread walking each of its runs' entries, 714 us.)
+  int carry = 0;                                   // the run holding the window's first entry (or 0)
+  for (int w0 = 0; w0 < NE; w0 += EMIT_T) {
+#pragma unroll
+    for (int q = 0; q < EMIT_T / 256 / 8; q++) reinterpret_cast<uint4*>(s_of)[q * 256 + tid] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (int i = tid; i < M; i += 256) {
+      const int p = s_at[i] - w0;
+      if (p >= 0 && p < EMIT_T) s_of[p] = uint16_t(i);
     }
-    for (int wb = x0; wb < x1; wb += 64) {
-      const int qi = q0 + 1 + lane;                // s_at[M] = NE: a start past every entry
-      const int d = qi <= M ? s_at[qi] - wb : 64;
-      if (lane == 0) s_mask[wv] = 0;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (d >= 0 && d < 64) atomicOr(&s_mask[wv], 1ull << d);
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const unsigned long long msk = s_mask[wv];
-      const int x = wb + lane;
-      if (x < x1) {
-        const int a = q0 + __popcll(msk & (lane == 63 ? ~0ull : (2ull << lane) - 1));
+    __syncthreads();
+    // inclusive max-scan, seeded with the run going on (its index is below every run starting in the
+    // window: runs are numbered by first entry): 8 consecutive per thread, the wave by shuffles, the
+    // waves by s_w
+    uint4 v8 = reinterpret_cast<const uint4*>(s_of)[tid];
+    uint32_t h[8] = {v8.x & 0xFFFFu, v8.x >> 16, v8.y & 0xFFFFu, v8.y >> 16,
+                     v8.z & 0xFFFFu, v8.z >> 16, v8.w & 0xFFFFu, v8.w >> 16};
+#pragma unroll
+    for (int q = 1; q < 8; q++) h[q] = h[q] > h[q - 1] ? h[q] : h[q - 1];
+    uint32_t m = h[7];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(m, d, 64);
+      if ((tid & 63) >= d) m = y > m ? y : m;
+    }
+    if ((tid & 63) == 63) s_w[tid >> 6] = int(m);
+    uint32_t ex = __shfl_up(m, 1, 64);
+    if ((tid & 63) == 0) ex = 0;
+    ex = ex > uint32_t(carry) ? ex : uint32_t(carry);
+    __syncthreads();
+    for (int w = 0; w < (tid >> 6); w++) ex = uint32_t(s_w[w]) > ex ? uint32_t(s_w[w]) : ex;
+#pragma unroll
+    for (int q = 0; q < 8; q++) h[q] = h[q] > ex ? h[q] : ex;
+    reinterpret_cast<uint4*>(s_of)[tid] = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16,
+                                                     h[6] | h[7] << 16);
+    __syncthreads();
+    carry = s_of[EMIT_T - 1];
+#pragma unroll 4
+    for (int q = 0; q < EMIT_T / 256; q++) {
+      const int x = w0 + q * 256 + tid;
+      if (x < NE) {
+        const int a = s_of[q * 256 + tid];
         const int32_t r = s_run[a];
         const int jo = r & 2047;                   // the start, from lo
         const int o = int(c0 - lo) + (r >> 11) - jo - (x - s_at[a]);   // the entry's record, from the start
-        const uint4 sg = segn == 4 ? make_uint4(s_seg[a].x, s_seg[a].y, 0xFFFFFFFFu, 0xFFFFFFFFu)
-                                   : seg_load(segs, segn, lo + jo);
+        const uint4 sg = SEG4 ? make_uint4(s_seg[a].x, s_seg[a].y, 0xFFFFFFFFu, 0xFFFFFFFFu)
+                              : seg_load(segs, segn, lo + jo);
         const int64_t rec = lo + jo + o;
         ent_name[eb + x] = s_name[seg_stage(sg, segn, o)];
-        ent_record[eb + x] = pos ? pos[rec] : base + rec;
+        ent_record[eb + x] = POS ? pos[rec] : base + rec;
       }
-      q0 += __popcll(msk);
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();             // (the mask is read before the next window resets it)
     }
+    __syncthreads();                               // (s_of is rewritten by the next window)
   }
 }
 
@@ -706,9 +763,11 @@ hipError_t runs_emit_launch(const RunsArgs& R, const int32_t* end_of, const int6
   const int64_t nw = (R.n + R.chunk - 1) / R.chunk, W = int64_t(runs_blocks(n_grid, R.chunk)) * (RT / 64);
   if (R.n <= 0) return hipSuccess;
   if (span < 0 || span >= R.chunk || R.chunk > RUNS_CHUNK || !R.segs) return hipErrorInvalidValue;
-  const size_t lds = size_t(R.chunk + span + 1) * 16 + size_t(R.chunk + 1) * 4 + 4;
-  hipLaunchKernelGGL(runs_emit, dim3(unsigned(nw)), dim3(256), lds, st, R.P, R.key, R.pos, R.base, R.segs, R.segn, end_of,
-                     R.n, R.chunk, span, pre, W, match_record, match_key, ent_off, ent_name, ent_record);
+  const size_t lds = size_t(R.chunk + span + 1) * 16 + 4;   // s_seg (and s_cnt) 8, s_run 4, s_at 4 per slot
+  auto k = R.segn == 4 ? (R.pos ? runs_emit<true, true> : runs_emit<true, false>)
+                       : (R.pos ? runs_emit<false, true> : runs_emit<false, false>);
+  hipLaunchKernelGGL(k, dim3(unsigned(nw)), dim3(256), lds, st, R.P, R.key, R.pos, R.base, R.segs, R.segn, end_of, R.n,
+                     R.chunk, span, pre, W, match_record, match_key, ent_off, ent_name, ent_record);
   return hipGetLastError();
 }
 

@@ -329,12 +329,23 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
               }
             }
           }
-          if (A.segs && res.end >= 0 && !old_end) {
-            if (seg_item != i) seg_n = 0;
-            for (int q = seg_n; q < RUNS_MAX_SEGS; q++) myseg[q] = 0xFFFF;   // terminator (and padding)
-            // one 8- or 16-byte store per completed run (dense by start record)
-            if (A.segn == 4) *reinterpret_cast<uint2*>(A.segs + i * 4) = *reinterpret_cast<const uint2*>(myseg);
-            else *reinterpret_cast<uint4*>(A.segs + i * 8) = *reinterpret_cast<const uint4*>(myseg);
+          // every item's slot is stored (a run that did not complete here: terminators only), so the
+          // chunk's segment words are written in full lines instead of one partial line per completed run
+          if (A.segs) {
+            // the run's segments, the ones past its last as the terminator (and padding) 0xFFFF, in
+            // registers (a fill loop over the lane's LDS words cost the wave a loop per finishing lane);
+            // one 8- or 16-byte store per item (dense by start record)
+            const int sn = res.end >= 0 && !old_end && seg_item == i ? seg_n : 0;
+            uint4 w = *reinterpret_cast<const uint4*>(myseg);
+            auto pad = [sn](uint32_t v, int q) {
+              return v | (q < sn ? 0u : 0xFFFFu) | (q + 1 < sn ? 0u : 0xFFFF0000u);
+            };
+            w.x = pad(w.x, 0);
+            w.y = pad(w.y, 2);
+            w.z = pad(w.z, 4);
+            w.w = pad(w.w, 6);
+            if (A.segn == 4) *reinterpret_cast<uint2*>(A.segs + i * 4) = make_uint2(w.x, w.y);
+            else *reinterpret_cast<uint4*>(A.segs + i * 8) = w;
           }
         },
         [&](int32_t i, int32_t r, int stage) {
