@@ -76,6 +76,46 @@ struct SlotFormat {
 // One thread per match: its slot word (and aux byte) loaded once, its k row entries stored (a wave's
 // stores of one stage k ints apart, the k stores together filling the wave's rows).  (Was one thread
 // per output word: a divide by k and the slot loads repeated k times per match.)
+// The plain kernel's dense slots (the headline path), K a template parameter: a thread's first
+// GATHER_B slot words are loaded at clamped addresses before any row is stored, so the loads are one
+// memory round trip, not one per match each behind the stores before it (a load under a branch or a
+// loop over a run-time k makes the compiler wait for every outstanding memory operation, stores
+// included); the rest, if a super-tile has more matches, one at a time
+constexpr int GATHER_B = 4;
+template <int K>
+__global__ __launch_bounds__(256) void stencil_gather_dense(const int32_t* __restrict__ slots,
+                                                            const int64_t* __restrict__ cnt,
+                                                            const int64_t* __restrict__ pre, int32_t* __restrict__ out,
+                                                            int64_t out_cap, int64_t nsuper, int sub) {
+  const int64_t t = blockIdx.x;                  // super-tile
+  const int64_t c = cnt[t], p = pre[t];
+  if (p + c > out_cap || c <= 0) return;
+  int32_t* const dst = out + p * K;
+  const int32_t* const dense = slots + t * ST_DENSE;
+  const int32_t* const over = slots + nsuper * ST_DENSE + t * int64_t(sub) * ST_TILE;
+  const int64_t cb = c < int64_t(GATHER_B) * blockDim.x ? c : int64_t(GATHER_B) * blockDim.x;
+  int32_t v[GATHER_B];
+#pragma unroll
+  for (int q = 0; q < GATHER_B; q++) {
+    const int64_t m = threadIdx.x + int64_t(q) * blockDim.x;
+    const int64_t mm = m < cb ? m : 0;
+    v[q] = (mm < ST_DENSE ? dense : over)[mm];
+  }
+#pragma unroll
+  for (int q = 0; q < GATHER_B; q++) {
+    const int64_t m = threadIdx.x + int64_t(q) * blockDim.x;
+    if (m < cb) {
+#pragma unroll
+      for (int s = 0; s < K; s++) dst[m * K + s] = v[q] + s;
+    }
+  }
+  for (int64_t m = cb + threadIdx.x; m < c; m += blockDim.x) {
+    const int32_t w = (m < ST_DENSE ? dense : over)[m];
+#pragma unroll
+    for (int s = 0; s < K; s++) dst[m * K + s] = w + s;
+  }
+}
+
 __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
                                                       const int64_t* __restrict__ pre, int32_t* __restrict__ out,
                                                       int64_t out_cap, int sub, SlotFormat F) {
@@ -460,8 +500,24 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
       if (e == hipSuccess && L.clear_flag) e = hipMemsetAsync(L.clear_flag, 0, 8, st);
       if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre,
-                       L.out, L.out_cap, sub, F);
+    if (F.dense) {
+      decltype(&stencil_gather_dense<1>) g = nullptr;
+      switch (L.k) {
+        case 1: g = stencil_gather_dense<1>; break;
+        case 2: g = stencil_gather_dense<2>; break;
+        case 3: g = stencil_gather_dense<3>; break;
+        case 4: g = stencil_gather_dense<4>; break;
+        case 5: g = stencil_gather_dense<5>; break;
+        case 6: g = stencil_gather_dense<6>; break;
+        case 7: g = stencil_gather_dense<7>; break;
+        default: return hipErrorInvalidValue;     // (the plain kernel: k <= 7)
+      }
+      hipLaunchKernelGGL(g, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre, L.out,
+                         L.out_cap, nsuper, sub);
+    } else {
+      hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre,
+                         L.out, L.out_cap, sub, F);
+    }
   }
   if (D.hdr) {
     hipError_t e = hipGetLastError();
