@@ -116,6 +116,63 @@ __global__ __launch_bounds__(256) void stencil_gather_dense(const int32_t* __res
   }
 }
 
+// Every other slot format (keyed / chain / carry), K a template parameter, the same batching: a
+// thread's first GATHER_B matches' slot words and aux bytes loaded before any row is stored.  The
+// format's branches are taken once per workgroup (uniform) around loads of one shape each: a value
+// loaded in either arm of a branch is merged after it, and that merge waits for every outstanding
+// memory operation
+template <int K, class Ld>
+__device__ __forceinline__ void gather_rows(int32_t* __restrict__ dst, int64_t c, const SlotFormat& F, Ld&& ld) {
+  const int64_t cb = c < int64_t(GATHER_B) * blockDim.x ? c : int64_t(GATHER_B) * blockDim.x;
+  int32_t v[GATHER_B];
+  uint32_t a[GATHER_B];
+#pragma unroll
+  for (int q = 0; q < GATHER_B; q++) {
+    const int64_t m = threadIdx.x + int64_t(q) * blockDim.x;
+    ld(m < cb ? m : 0, v[q], a[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < GATHER_B; q++) {
+    const int64_t m = threadIdx.x + int64_t(q) * blockDim.x;
+    if (m < cb) {
+#pragma unroll
+      for (int s = 0; s < K; s++) dst[m * K + s] = F.value(v[q], a[q], s);
+    }
+  }
+  for (int64_t m = cb + threadIdx.x; m < c; m += blockDim.x) {
+    int32_t w;
+    uint32_t b;
+    ld(m, w, b);
+#pragma unroll
+    for (int s = 0; s < K; s++) dst[m * K + s] = F.value(w, b, s);
+  }
+}
+template <int K>
+__global__ __launch_bounds__(256) void stencil_gather_k(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
+                                                        const int64_t* __restrict__ pre, int32_t* __restrict__ out,
+                                                        int64_t out_cap, SlotFormat F) {
+  const int64_t t = blockIdx.x;                  // super-tile
+  const int64_t c = cnt[t], p = pre[t];
+  if (p + c > out_cap || c <= 0) return;
+  int32_t* const dst = out + p * K;
+  if (F.kdense && c <= ST_DENSE_KEYED) {         // the keyed kernel's dense region (no carry)
+    const int32_t* const w0 = slots + t * ST_DENSE_KEYED;
+    const uint8_t* const a0 = reinterpret_cast<const uint8_t*>(slots + F.nsuper * ST_DENSE_KEYED) + t * ST_DENSE_KEYED;
+    gather_rows<K>(dst, c, F, [&](int64_t m, int32_t& v, uint32_t& a) { v = w0[m]; a = a0[m]; });
+    return;
+  }
+  const int32_t* const src = slots + (F.kdense ? F.nsuper * (ST_DENSE_KEYED + ST_DENSE_KEYED / 4) : 0) +
+                             t * int64_t(F.sub) * ST_TILE * K;
+  const uint8_t* const aux = reinterpret_cast<const uint8_t*>(src + int64_t(F.sub) * ST_TILE);
+  // the aux byte: keyed rows always (k > 1); plain rows only for a carry boundary match (v < 0) -- loaded
+  // whenever the format has it (K > 1: inside the slot) and used only then
+  const bool has_aux = K > 1 && (!F.plain || F.carry);
+  if (has_aux)
+    gather_rows<K>(dst, c, F, [&](int64_t m, int32_t& v, uint32_t& a) { v = src[m]; a = aux[m]; });
+  else
+    gather_rows<K>(dst, c, F, [&](int64_t m, int32_t& v, uint32_t& a) { v = src[m]; a = 0; });
+}
+
 __global__ __launch_bounds__(256) void stencil_gather(const int32_t* __restrict__ slots, const int64_t* __restrict__ cnt,
                                                       const int64_t* __restrict__ pre, int32_t* __restrict__ out,
                                                       int64_t out_cap, int sub, SlotFormat F) {
@@ -220,9 +277,11 @@ __global__ __launch_bounds__(1024) void stencil_finish_small(const int32_t* __re
     const int64_t pre = s_pre[t], m = s_pre[t + 1] - pre;
     if (pre + m > out_cap) continue;
     int32_t* dst = out + pre * k;
-    for (int64_t w = lane; w < m * k; w += 64) {
-      const int64_t q = w / k;
-      dst[w] = F.entry(slots, t, m, q, int(w - q * k));
+    for (int64_t q = lane; q < m; q += 64) {               // a match's slot word (and aux byte) loaded once
+      int32_t v;
+      uint32_t a;
+      F.load(slots, t, m, q, v, a);
+      for (int s2 = 0; s2 < k; s2++) dst[q * k + s2] = F.value(v, a, s2);
     }
   }
 }
@@ -286,11 +345,13 @@ __global__ __launch_bounds__(256) void stencil_finish_deliver(const int32_t* __r
   if (pre + m <= out_cap) {
     for (int64_t q = threadIdx.x; q < m; q += 256) {
       const int64_t i = pre + q;
-      int32_t row[STENCIL_MAX_K], last = 0;
+      int32_t row[STENCIL_MAX_K], last = 0, v;
+      uint32_t av;
+      F.load(slots, t, m, q, v, av);                 // (once per match, not once per stage)
 #pragma unroll
       for (int s = 0; s < STENCIL_MAX_K; s++)
         if (s < k) {
-          row[s] = F.entry(slots, t, m, q, s);
+          row[s] = F.value(v, av, s);
           out[i * k + s] = row[s];
           last = row[s];
         }
@@ -357,13 +418,29 @@ __global__ __launch_bounds__(1024) void stencil_finish_deliver_arrival(
     if (clear_flag) *clear_flag = 0;
   }
   const bool fits = tot <= out_cap;
-  // pass A: every match's completing record, counted by its arrival index
-  for (int64_t t = wid; t < nt && fits; t += 16) {
-    const int64_t m = s_pre[t + 1] - s_pre[t];
-    for (int64_t q = lane; q < m; q += 64) {
-      const int32_t last = F.entry(slots, t, m, q, k - 1);
-      const int64_t a = C.gpos[last] - C.base;
-      atomicAdd(&s_cnt[a >> 2], 1u << (8 * (a & 3)));
+  // pass A: every match's completing record, counted by its arrival index.  A thread's first FA_KEEP
+  // matches keep their slot word, aux byte, arrival index and key for pass B (loaded once, the key with
+  // the arrival index: pass B's chain of dependent loads is then the halo's alone)
+  constexpr int FA_KEEP = 2;
+  int32_t kv[FA_KEEP], kk_[FA_KEEP];
+  uint32_t ka[FA_KEEP];
+  int64_t karr[FA_KEEP];
+  {
+    int it = 0;
+    for (int64_t t = wid; t < nt && fits; t += 16) {
+      const int64_t m = s_pre[t + 1] - s_pre[t];
+      for (int64_t q = lane; q < m; q += 64, it++) {
+        int32_t v;
+        uint32_t a;
+        F.load(slots, t, m, q, v, a);
+        const int32_t last = F.value(v, a, k - 1);
+        const int64_t arr = C.gpos[last] - C.base;
+        const int32_t kk = key[last];
+        atomicAdd(&s_cnt[arr >> 2], 1u << (8 * (arr & 3)));
+#pragma unroll
+        for (int u = 0; u < FA_KEEP; u++)
+          if (u == it) { kv[u] = v; ka[u] = a; karr[u] = arr; kk_[u] = kk; }
+      }
     }
   }
   __syncthreads();
@@ -389,19 +466,30 @@ __global__ __launch_bounds__(1024) void stencil_finish_deliver_arrival(
   }
   __syncthreads();
   // pass B: the rows (kept on the device for cep_checksum) and their delivery at the arrival rank
+  int it = 0;
   for (int64_t t = wid; t < nt && fits; t += 16) {
     const int64_t m = s_pre[t + 1] - s_pre[t];
-    for (int64_t q = lane; q < m; q += 64) {
+    for (int64_t q = lane; q < m; q += 64, it++) {
       const int64_t i = s_pre[t] + q;
+      int32_t v = 0, kk = 0;
+      uint32_t av = 0;
+      int64_t a = 0;
+#pragma unroll
+      for (int u = 0; u < FA_KEEP; u++)
+        if (u == it) { v = kv[u]; av = ka[u]; a = karr[u]; kk = kk_[u]; }
+      if (it >= FA_KEEP) F.load(slots, t, m, q, v, av);
       int32_t row[STENCIL_MAX_K], last = 0;
 #pragma unroll
       for (int s2 = 0; s2 < STENCIL_MAX_K; s2++)
         if (s2 < k) {
-          row[s2] = F.entry(slots, t, m, q, s2);
+          row[s2] = F.value(v, av, s2);
           out[i * k + s2] = row[s2];
           last = row[s2];
         }
-      const int64_t a = C.gpos[last] - C.base;
+      if (it >= FA_KEEP) {
+        a = C.gpos[last] - C.base;
+        kk = key[last];
+      }
       int64_t j = s_tpre[a >> 6];
       for (int64_t b = (a & ~int64_t(63)) >> 2; b < (a >> 2); b++) {   // whole words before a's, then a's bytes
         const uint32_t w = s_cnt[b];
@@ -410,7 +498,6 @@ __global__ __launch_bounds__(1024) void stencil_finish_deliver_arrival(
       for (int64_t b = a & ~int64_t(3); b < a; b++) j += (s_cnt[b >> 2] >> (8 * (b & 3))) & 0xFF;
       if (F.chain)                                 // (a strict fixed-length pattern: one match per record)
         for (int64_t p = q - 1; p >= 0 && F.entry(slots, t, m, p, k - 1) == last; p--) j++;   // same record, earlier
-      const int32_t kk = key[last];
       const bool kok = kk >= 0 && kk < C.max_keys;
       const HaloHdr* h = kok ? C.hdr + kk : nullptr;
       const int old = kok ? halo_old(*h, C.stamp) : 0;
@@ -515,8 +602,25 @@ hipError_t stencil_launch(const StencilLaunch& L, hipEvent_t ev0, hipEvent_t ev1
       hipLaunchKernelGGL(g, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre, L.out,
                          L.out_cap, nsuper, sub);
     } else {
-      hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre,
-                         L.out, L.out_cap, sub, F);
+      decltype(&stencil_gather_k<1>) g = nullptr;
+      switch (L.k) {
+        case 1: g = stencil_gather_k<1>; break;
+        case 2: g = stencil_gather_k<2>; break;
+        case 3: g = stencil_gather_k<3>; break;
+        case 4: g = stencil_gather_k<4>; break;
+        case 5: g = stencil_gather_k<5>; break;
+        case 6: g = stencil_gather_k<6>; break;
+        case 7: g = stencil_gather_k<7>; break;
+        case 8: g = stencil_gather_k<8>; break;
+        default: break;
+      }
+      if (g) {
+        hipLaunchKernelGGL(g, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre, L.out,
+                           L.out_cap, F);
+      } else {
+        hipLaunchKernelGGL(stencil_gather, dim3(unsigned(nsuper)), dim3(128), 0, st, L.slots, L.tile_count, L.tile_pre,
+                           L.out, L.out_cap, sub, F);
+      }
     }
   }
   if (D.hdr) {
