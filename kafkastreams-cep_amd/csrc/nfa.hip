@@ -132,11 +132,16 @@ __global__ void scan_blocks(ScanPair S, int64_t* __restrict__ bsum) {
   const int64_t n = scan_len(S);
   const int64_t* __restrict__ in = S.in[blockIdx.y];
   const int64_t b0 = int64_t(blockIdx.x) * 1024;
-  int64_t acc = 0;
+  // loads at clamped indices, masked after (a load under `i < n` is a branch waited on inside it)
+  const int64_t last = n > 0 ? n - 1 : 0;
+  int64_t v[4], acc = 0;
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     const int64_t i = b0 + threadIdx.x * 4 + k;
-    if (i < n) acc += in[i];
+    v[k] = in[i < n ? i : last];
   }
+#pragma unroll
+  for (int k = 0; k < 4; k++) acc += b0 + threadIdx.x * 4 + k < n ? v[k] : 0;
   s[threadIdx.x] = acc;
   __syncthreads();
   for (int d = 128; d > 0; d >>= 1) {
@@ -174,9 +179,12 @@ __device__ __forceinline__ void scan_sums_reg_body(int64_t* __restrict__ bsum, i
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t per = (nb + 1023) / 1024, a = tid * per;
   int64_t v[SCAN_REG], sum = 0;
+  const int64_t lastb = nb > 0 ? nb - 1 : 0;
+#pragma unroll
+  for (int i = 0; i < SCAN_REG; i++) v[i] = bsum[i < per && a + i < nb ? a + i : lastb];   // (clamped, masked below)
 #pragma unroll
   for (int i = 0; i < SCAN_REG; i++) {
-    v[i] = i < per && a + i < nb ? bsum[a + i] : 0;
+    if (!(i < per && a + i < nb)) v[i] = 0;
     sum += v[i];
   }
   int64_t incl = sum;
@@ -209,9 +217,14 @@ __global__ void scan_final(ScanPair S, const int64_t* __restrict__ bsum) {
   const int64_t b0 = int64_t(blockIdx.x) * 1024;
   if (b0 >= n) return;                             // (whole block: the barriers below stay uniform)
   int64_t v[4], acc = 0;
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     const int64_t i = b0 + threadIdx.x * 4 + k;
-    v[k] = i < n ? in[i] : 0;
+    v[k] = in[i < n ? i : n - 1];                  // (clamped, masked below; n > b0 >= 0 here)
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (b0 + threadIdx.x * 4 + k >= n) v[k] = 0;
     acc += v[k];
   }
   int64_t tot = 0;
