@@ -329,13 +329,14 @@ __device__ __forceinline__ void runs_sim_body(const Tab& T, const RunsArgs& A, i
               }
             }
           }
-          // every item's slot is stored (a run that did not complete here: terminators only), so the
-          // chunk's segment words are written in full lines instead of one partial line per completed run
-          if (A.segs) {
+          // (storing every item's slot, terminators for runs that did not complete, so that the segment
+          // words go out in full lines: C3 runs_sim WRITE 178 -> 229 MB -- the completed runs' partial lines
+          // cost less than the dense array)
+          if (A.segs && res.end >= 0 && !old_end) {
             // the run's segments, the ones past its last as the terminator (and padding) 0xFFFF, in
             // registers (a fill loop over the lane's LDS words cost the wave a loop per finishing lane);
-            // one 8- or 16-byte store per item (dense by start record)
-            const int sn = res.end >= 0 && !old_end && seg_item == i ? seg_n : 0;
+            // one 8- or 16-byte store per completed run (by start record)
+            const int sn = seg_item == i ? seg_n : 0;
             uint4 w = *reinterpret_cast<const uint4*>(myseg);
             auto pad = [sn](uint32_t v, int q) {
               return v | (q < sn ? 0u : 0xFFFFu) | (q + 1 < sn ? 0u : 0xFFFF0000u);
