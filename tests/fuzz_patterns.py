@@ -1,0 +1,106 @@
+"""Seeded random patterns and streams for the parity fuzz tests (tests/test_fuzz_gpu.py,
+tests/test_fuzz_cpu.py).
+
+A pattern is 1-5 stages built through the reference's builder surface (QueryBuilder.java:25-60,
+StageBuilder / PatternBuilder): each stage picks a contiguity (strict / skip-till-next /
+skip-till-any, Selected.java), a cardinality (one, optional, oneOrMore, zeroOrMore, times(n),
+StagesFactory.java), a predicate over the record's value (comparisons, modulo tests, and/or/not), and
+sometimes a fold into a state the next stage reads (the stock demo's shape, Patterns.java:11-25) or
+a window (within).  The same seed always gives the same pattern and stream."""
+import numpy as np
+
+from kcep import QueryBuilder, Selected, TimeUnit, Event, States, Curr, Long
+
+VMAX = 6                     # values 0..VMAX-1: small, so that predicates hit often
+
+
+def _pred(rng):
+    v = Event.value()
+    kind = rng.integers(0, 6)
+    c = int(rng.integers(0, VMAX))
+    if kind == 0:
+        return v == c
+    if kind == 1:
+        return v < max(1, c)
+    if kind == 2:
+        return v > min(VMAX - 2, c)
+    if kind == 3:
+        return (v % 2) == int(rng.integers(0, 2))
+    if kind == 4:
+        d = int(rng.integers(0, VMAX))
+        return (v == c) | (v == d)
+    return ~(v == c) & (v < VMAX - 1)
+
+
+def random_pattern(seed):
+    """(builder pattern, description) for `seed`."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 6))
+    cls = seed % 3                   # the stream's key length class (random_stream)
+    n_any = n_rep = 0
+    desc = []
+    fold_state = None
+    b = None
+    for s in range(n):
+        name = f"s{s}"
+        strat = int(rng.choice([0, 1, 2], p=[0.35, 0.4, 0.25])) if s > 0 else 0
+        card = int(rng.choice([0, 1, 2, 3, 4], p=[0.5, 0.12, 0.15, 0.1, 0.13])) if s > 0 else int(
+            rng.choice([0, 2, 4], p=[0.7, 0.15, 0.15]))
+        if s == n - 1 and rng.random() < 0.9:
+            card = 0                 # mostly valid: a final stage may be neither optional nor repeated
+                                     # (StagesFactory.java InvalidPatternException); the rest checks the error
+        # Skipping strategies over open-ended repeats enumerate subsets of a key's records (as the
+        # reference does, exponentially): so that every seed runs in seconds (the device evaluates
+        # every key, the task stops at the first exception), skip-till-any repeats and skip-till-any
+        # after a repeat only on the short keys, at most two skip-till-any stages and no open-ended
+        # repeat on the long keys (checked by the per-key oracle over seeds 0-299: <= 3.2 k matches a key)
+        if strat == 2 and card in (2, 3) and cls > 0 and s < n - 1:
+            card = 0
+        if strat == 2 and (n_any >= 2 and cls == 2 or n_rep >= 1 and cls > 0):
+            strat = 1
+        if card in (2, 3) and cls == 2:
+            card = 4 if s < n - 1 else 0
+        n_any += strat == 2
+        n_rep += card in (2, 3)
+        sel = [Selected.withStrictContiguity, Selected.withSkipTilNextMatch, Selected.withSkipTilAnyMatch][strat]()
+        st = (QueryBuilder().select(name, sel) if b is None else b.then().select(name, sel))
+        if card == 1:
+            st = st.optional()
+        elif card == 2:
+            st = st.oneOrMore()
+        elif card == 3:
+            st = st.zeroOrMore()
+        elif card == 4:
+            st = st.times(int(rng.integers(2, 4)))
+        if fold_state is not None and rng.random() < 0.6:
+            p = Event.value() >= States.getOrElse(fold_state, Long(0)).asLong() % VMAX
+            desc.append(f"{name}:{strat}/{card}/state")
+        else:
+            p = _pred(rng)
+            desc.append(f"{name}:{strat}/{card}")
+        b = st.where(p)
+        if rng.random() < 0.2:
+            b = b.or_(Event.value() == int(rng.integers(0, VMAX)))
+        fold_state = None
+        if s < n - 1 and rng.random() < 0.2:
+            fold_state = f"f{s}"
+            b = b.fold(fold_state, Curr.long() + Event.value())
+    window = None
+    if rng.random() < 0.25:
+        window = int(rng.integers(3, 20))
+        b = b.within(window, TimeUnit.MILLISECONDS)
+        desc.append(f"within {window} ms")
+    return b.build(), " ".join(desc), window
+
+
+def random_stream(seed, n_keys=None, per_key=None):
+    """Key-grouped (key, value, timestamp) arrays for `seed`: Poisson record counts per key (short,
+    medium or long keys by seed), values 0..VMAX-1, timestamps strictly increasing by 1-3 ms."""
+    rng = np.random.default_rng(seed + 7919)
+    if per_key is None:
+        n_keys, per_key = [(300, 4), (120, 12), (40, 30)][seed % 3]
+    lens = rng.poisson(per_key, n_keys) + 1
+    key = np.repeat(np.arange(n_keys, dtype=np.int32), lens)
+    val = rng.integers(0, VMAX, len(key)).astype(np.int32)
+    ts = np.cumsum(rng.integers(1, 4, len(key))).astype(np.int64)
+    return key, val, ts

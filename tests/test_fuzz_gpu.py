@@ -1,0 +1,77 @@
+"""Random-pattern parity fuzz (tests/fuzz_patterns.py): each seed builds a pattern through the
+reference's builder surface and a key-grouped stream with timestamps, runs it through libkcep.so on
+cuda:0 -- once on the path the product picks for it (stencil / chain / runs / general, JIT'd as in
+production) and once on the general path forced (interpreted; wave or lane engine by seed) -- and
+compares both bit-exactly with oracle/cep_oracle.c: every match (emitting record, key, full buffer
+traversal), and the reference's own exception (code and failing record, NFA.java:148-155) where the
+pattern raises one, with the matches of the records before it."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from kcep import native as N
+import fuzz_patterns as F
+import patterns_lib as PL
+
+pytestmark = pytest.mark.gpu
+
+# 40 seeds in the default suite (~2 min, mostly JIT builds); KCEP_FUZZ_SEEDS=a:b for a campaign
+_a, _b = map(int, os.environ.get("KCEP_FUZZ_SEEDS", "0:40").split(":"))
+SEEDS = range(_a, _b)
+
+
+def _oracle(ir, mode, key, val, ts):
+    p = O.OraclePattern(ir)
+    r = O.OracleRun(p, mode)
+    err = None
+    try:
+        r.process(O.BatchArrays(key, [val], [1], ts=ts))
+    except O.OracleError as e:
+        err = (e.code, e.record)
+    return [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)], err
+
+
+def _device(ir, gmode, key, val, ts, **opts):
+    cp = N.CompiledPattern(ir)
+    s = N.Session(cp, len(key), mode=gmode, **opts)
+    s.push(len(key), key, [val], ts=ts)
+    out = s.collect(raise_on_error=False)
+    got, err = [], None
+    if out is not None:
+        for m in range(len(out["match_record"])):
+            a, b = out["ent_off"][m], out["ent_off"][m + 1]
+            got.append((int(out["match_record"][m]), int(out["match_key"][m]),
+                        [(cp.names[out["ent_name"][i]], int(out["ent_record"][i])) for i in range(a, b)]))
+        if out["err"]:
+            err = (int(out["err"]), int(out["err_record"]))
+    return got, err, s.path
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_pattern_parity(seed):
+    pat, desc, _ = F.random_pattern(seed)
+    ir = pat.to_ir(PL.I32)
+    try:
+        O.OraclePattern(ir)
+    except O.OracleError as e:          # an invalid pattern: the product refuses it the same way
+        with pytest.raises(N.CepError) as ei:
+            N.CompiledPattern(ir)
+        assert ei.value.code == e.code
+        return
+    key, val, ts = F.random_stream(seed)
+    rng = np.random.default_rng(seed)
+    omode = O.MODE_PROCESSOR if rng.random() < 0.5 else O.MODE_NFA_PER_KEY
+    gmode = N.MODE_PROCESSOR if omode == O.MODE_PROCESSOR else N.MODE_NFA
+    want, oerr = _oracle(ir, omode, key, val, ts)
+    lane = bool(rng.random() < 0.5)
+    for opts in (dict(), dict(force_path=N.PATH_GENERAL, interpret=True, lane_nfa=lane)):
+        got, gerr, path = _device(ir, gmode, key, val, ts, **opts)
+        w = want
+        if oerr is not None:             # the task stops at its first exception: earlier records' matches
+            got = [m for m in got if m[0] < oerr[1]]
+            w = [m for m in want if m[0] < oerr[1]]
+        ctx = (seed, desc, omode, path, opts)
+        assert gerr == oerr, ctx
+        assert got == w, ctx
