@@ -4,7 +4,10 @@ cuda:0 -- once on the path the product picks for it (stencil / chain / runs / ge
 production) and once on the general path forced (interpreted; wave or lane engine by seed) -- and
 compares both bit-exactly with oracle/cep_oracle.c: every match (emitting record, key, full buffer
 traversal), and the reference's own exception (code and failing record, NFA.java:148-155) where the
-pattern raises one, with the matches of the records before it."""
+pattern raises one, with the matches of the records before it.  The carry variant interleaves the
+keys (arrival order, as a topic partition delivers them), cuts the stream into 2-6 batches and runs
+them through one carry session (CEP_SESSION_CARRY: each key's state kept on the device between
+batches, CEPProcessor.java:111-124) against the oracle's single pass over the same records."""
 import os
 
 import numpy as np
@@ -17,8 +20,8 @@ import patterns_lib as PL
 
 pytestmark = pytest.mark.gpu
 
-# 40 seeds in the default suite (~2 min, mostly JIT builds); KCEP_FUZZ_SEEDS=a:b for a campaign
-_a, _b = map(int, os.environ.get("KCEP_FUZZ_SEEDS", "0:40").split(":"))
+# 24 seeds each in the default suite (~1 min each, mostly JIT builds); KCEP_FUZZ_SEEDS=a:b for a campaign
+_a, _b = map(int, os.environ.get("KCEP_FUZZ_SEEDS", "0:24").split(":"))
 SEEDS = range(_a, _b)
 
 
@@ -75,3 +78,52 @@ def test_random_pattern_parity(seed):
         ctx = (seed, desc, omode, path, opts)
         assert gerr == oerr, ctx
         assert got == w, ctx
+
+
+def _carry_stream(seed):
+    """The seed's records in interleaved arrival order, timestamps rising in that order, cut into
+    2-6 batches; every batch grouped by key (stable), as the host driver hands it to the device."""
+    key, val, _ = F.random_stream(seed)
+    rng = np.random.default_rng(seed + 104729)
+    perm = rng.permutation(len(key))
+    key, val = key[perm], val[perm]
+    ts = np.cumsum(rng.integers(1, 4, len(key))).astype(np.int64)
+    nb = int(rng.integers(2, 7))
+    bounds = [0] + sorted(rng.choice(np.arange(1, len(key)), nb - 1, replace=False).tolist()) + [len(key)]
+    order = np.concatenate([a + np.argsort(key[a:b], kind="stable") for a, b in zip(bounds[:-1], bounds[1:])])
+    return key[order], val[order], ts[order], bounds
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_pattern_carry_parity(seed):
+    pat, desc, _ = F.random_pattern(seed)
+    ir = pat.to_ir(PL.I32)
+    try:
+        O.OraclePattern(ir)
+    except O.OracleError:
+        pytest.skip("invalid pattern (test_random_pattern_parity checks the refusal)")
+    key, val, ts, bounds = _carry_stream(seed)
+    rng = np.random.default_rng(seed + 1)
+    omode = O.MODE_PROCESSOR if rng.random() < 0.5 else O.MODE_NFA_PER_KEY
+    gmode = N.MODE_PROCESSOR if omode == O.MODE_PROCESSOR else N.MODE_NFA
+    want, oerr = _oracle(ir, omode, key, val, ts)
+    cp = N.CompiledPattern(ir)
+    s = N.Session(cp, max(b - a for a, b in zip(bounds[:-1], bounds[1:])), mode=gmode, carry=True,
+                  max_keys=int(key.max()) + 1, lane_nfa=bool(rng.random() < 0.5))
+    got, gerr = [], None
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        s.push(b - a, np.ascontiguousarray(key[a:b]), [np.ascontiguousarray(val[a:b])], ts=np.ascontiguousarray(ts[a:b]))
+        out = s.collect(raise_on_error=False)
+        for m in range(len(out["match_record"])):
+            x, y = out["ent_off"][m], out["ent_off"][m + 1]
+            got.append((int(out["match_record"][m]), int(out["match_key"][m]),
+                        [(cp.names[out["ent_name"][i]], int(out["ent_record"][i])) for i in range(x, y)]))
+        if out["err"]:
+            gerr = (int(out["err"]), int(out["err_record"]))
+            break
+    ctx = (seed, desc, omode, s.path, len(bounds) - 1)
+    if oerr is not None:
+        got = [m for m in got if m[0] < oerr[1]]
+        want = [m for m in want if m[0] < oerr[1]]
+    assert gerr == oerr, ctx
+    assert got == want, ctx
