@@ -9,9 +9,24 @@ sometimes a fold into a state the next stage reads (the stock demo's shape, Patt
 a window (within).  The same seed always gives the same pattern and stream."""
 import numpy as np
 
-from kcep import QueryBuilder, Selected, TimeUnit, Event, States, Curr, Long
+from kcep import QueryBuilder, Selected, TimeUnit, Event, States, Curr, Long, Schema
 
 VMAX = 6                     # values 0..VMAX-1: small, so that predicates hit often
+# the rich variant: three typed columns and two topics (Selected.withTopic, Selected.java:19-67)
+RICH = Schema([("value", "i32"), ("px", "i64"), ("r", "f64")], topics=["A", "B"])
+
+
+def _pred_rich(rng):
+    kind = rng.integers(0, 5)
+    if kind == 0:
+        return Event.field("px") > int(rng.integers(0, 6)) * 1000
+    if kind == 1:
+        return Event.field("r") < float(rng.choice([0.25, 0.5, 0.75]))
+    if kind == 2:
+        return (Event.field("px") % 3) == (Event.value() % 3)
+    if kind == 3:
+        return (Event.field("r") * 4 > Event.value()) | (Event.field("px") < 500)
+    return _pred(rng)
 
 
 def _pred(rng):
@@ -32,8 +47,9 @@ def _pred(rng):
     return ~(v == c) & (v < VMAX - 1)
 
 
-def random_pattern(seed):
-    """(builder pattern, description) for `seed`."""
+def random_pattern(seed, rich=False):
+    """(builder pattern, description, window) for `seed`; `rich`: predicates over the RICH schema's
+    columns and stages reading one topic."""
     rng = np.random.default_rng(seed)
     n = int(rng.integers(1, 6))
     cls = seed % 3                   # the stream's key length class (random_stream)
@@ -63,6 +79,8 @@ def random_pattern(seed):
         n_any += strat == 2
         n_rep += card in (2, 3)
         sel = [Selected.withStrictContiguity, Selected.withSkipTilNextMatch, Selected.withSkipTilAnyMatch][strat]()
+        if rich and rng.random() < 0.25:
+            sel = sel.withTopic(str(rng.choice(["A", "B"])))
         st = (QueryBuilder().select(name, sel) if b is None else b.then().select(name, sel))
         if card == 1:
             st = st.optional()
@@ -76,7 +94,7 @@ def random_pattern(seed):
             p = Event.value() >= States.getOrElse(fold_state, Long(0)).asLong() % VMAX
             desc.append(f"{name}:{strat}/{card}/state")
         else:
-            p = _pred(rng)
+            p = _pred_rich(rng) if rich else _pred(rng)
             desc.append(f"{name}:{strat}/{card}")
         b = st.where(p)
         if rng.random() < 0.2:
@@ -104,3 +122,27 @@ def random_stream(seed, n_keys=None, per_key=None):
     val = rng.integers(0, VMAX, len(key)).astype(np.int32)
     ts = np.cumsum(rng.integers(1, 4, len(key))).astype(np.int64)
     return key, val, ts
+
+
+def rich_columns(seed, key, val, ts, processor):
+    """Columns and record metadata of the rich variant for a key-grouped `key`: px (i64), r (f64),
+    topic 0/1, ~5 % null records, and in processor mode ~5 % re-deliveries, which the processor's
+    high-water mark drops when it has seen the offset (CEPProcessor.java:152-160).  A re-delivery is
+    the record 3 positions back delivered again (same key, offset and contents: an offset names one
+    record of a partition; buffer nodes are keyed by it, Matched.java:31-35).  Returns
+    (val, ts, px, r, topic, valid, offset)."""
+    rng = np.random.default_rng(seed + 15485863)
+    n = len(key)
+    val, ts = val.copy(), ts.copy()
+    px = rng.integers(0, 6000, n).astype(np.int64)
+    r = rng.random(n)
+    topic = rng.integers(0, 2, n).astype(np.int32)
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    offset = np.arange(n, dtype=np.int64)
+    if processor:
+        dup = rng.random(n) < 0.05
+        for i in np.nonzero(dup)[0]:
+            if i >= 3 and key[i - 3] == key[i]:
+                for a in (val, ts, px, r, topic, valid, offset):
+                    a[i] = a[i - 3]
+    return val, ts, px, r, topic, valid, offset

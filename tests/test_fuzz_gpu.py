@@ -25,21 +25,21 @@ _a, _b = map(int, os.environ.get("KCEP_FUZZ_SEEDS", "0:24").split(":"))
 SEEDS = range(_a, _b)
 
 
-def _oracle(ir, mode, key, val, ts):
+def _oracle(ir, mode, key, val, ts, cols=None, coltypes=(1,), **kw):
     p = O.OraclePattern(ir)
     r = O.OracleRun(p, mode)
     err = None
     try:
-        r.process(O.BatchArrays(key, [val], [1], ts=ts))
+        r.process(O.BatchArrays(key, cols or [val], list(coltypes), ts=ts, **kw))
     except O.OracleError as e:
         err = (e.code, e.record)
     return [(m.record, m.key, [(p.names[nm], ev) for nm, ev in m.traversal]) for m in r.matches(with_groups=False)], err
 
 
-def _device(ir, gmode, key, val, ts, **opts):
+def _device(ir, gmode, key, val, ts, cols=None, meta=None, **opts):
     cp = N.CompiledPattern(ir)
     s = N.Session(cp, len(key), mode=gmode, **opts)
-    s.push(len(key), key, [val], ts=ts)
+    s.push(len(key), key, cols or [val], ts=ts, **(meta or {}))
     out = s.collect(raise_on_error=False)
     got, err = [], None
     if out is not None:
@@ -127,3 +127,33 @@ def test_random_pattern_carry_parity(seed):
         want = [m for m in want if m[0] < oerr[1]]
     assert gerr == oerr, ctx
     assert got == want, ctx
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_rich_parity(seed):
+    """The rich variant: i32/i64/f64 columns, stages reading one topic, null records and (processor
+    mode) re-delivered records, on the product's path and the forced general path."""
+    pat, desc, _ = F.random_pattern(seed, rich=True)
+    ir = pat.to_ir(F.RICH)
+    try:
+        O.OraclePattern(ir)
+    except O.OracleError:
+        pytest.skip("invalid pattern (test_random_pattern_parity checks the refusal)")
+    key, val, ts = F.random_stream(seed)
+    rng = np.random.default_rng(seed + 2)
+    omode = O.MODE_PROCESSOR if rng.random() < 0.5 else O.MODE_NFA_PER_KEY
+    gmode = N.MODE_PROCESSOR if omode == O.MODE_PROCESSOR else N.MODE_NFA
+    val, ts, px, r, topic, valid, offset = F.rich_columns(seed, key, val, ts, omode == O.MODE_PROCESSOR)
+    cols = [val, px, r]
+    meta = dict(topic=topic, valid=valid, offset=offset)
+    want, oerr = _oracle(ir, omode, key, val, ts, cols=cols, coltypes=(1, 2, 3), **meta)
+    lane = bool(rng.random() < 0.5)
+    for opts in (dict(), dict(force_path=N.PATH_GENERAL, interpret=True, lane_nfa=lane)):
+        got, gerr, path = _device(ir, gmode, key, val, ts, cols=cols, meta=meta, **opts)
+        w = want
+        if oerr is not None:
+            got = [m for m in got if m[0] < oerr[1]]
+            w = [m for m in want if m[0] < oerr[1]]
+        ctx = (seed, desc, omode, path, opts)
+        assert gerr == oerr, ctx
+        assert got == w, ctx
