@@ -157,3 +157,45 @@ def test_random_rich_parity(seed):
         ctx = (seed, desc, omode, path, opts)
         assert gerr == oerr, ctx
         assert got == w, ctx
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_pattern_arrival_parity(seed):
+    """Processor flushes in arrival order (CEP_BATCH_ARRIVAL_ORDER, csrc/group.hip): the interleaved
+    stream cut into 1-6 batches handed over ungrouped; the device groups each batch by key and returns
+    the matches in the reference's forward order (CEPProcessor.java:134-150), element by element."""
+    pat, desc, _ = F.random_pattern(seed)
+    ir = pat.to_ir(PL.I32)
+    try:
+        O.OraclePattern(ir)
+    except O.OracleError:
+        pytest.skip("invalid pattern (test_random_pattern_parity checks the refusal)")
+    key, val, _ = F.random_stream(seed)
+    rng = np.random.default_rng(seed + 3)
+    perm = rng.permutation(len(key))
+    key, val = np.ascontiguousarray(key[perm]), np.ascontiguousarray(val[perm])
+    ts = np.cumsum(rng.integers(1, 4, len(key))).astype(np.int64)
+    off = np.arange(len(key), dtype=np.int64)
+    nb = int(rng.integers(1, 7))
+    bounds = [0] + sorted(rng.choice(np.arange(1, len(key)), nb - 1, replace=False).tolist()) + [len(key)]
+    want, oerr = _oracle(ir, O.MODE_PROCESSOR, key, val, ts, offset=off)
+    cp = N.CompiledPattern(ir)
+    s = N.Session(cp, len(key), carry=True, max_keys=int(key.max()) + 1, lane_nfa=bool(rng.random() < 0.5))
+    got, gerr = [], None
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        s.push(b - a, key[a:b].copy(), [val[a:b].copy()], flags=N.BATCH_ARRIVAL_ORDER | N.BATCH_OFFSETS_MONOTONE,
+               ts=ts[a:b].copy(), offset=off[a:b].copy())
+        out = s.collect(raise_on_error=False)
+        for m in range(len(out["match_record"])):
+            x, y = out["ent_off"][m], out["ent_off"][m + 1]
+            got.append((int(out["match_record"][m]), int(out["match_key"][m]),
+                        [(cp.names[out["ent_name"][i]], int(out["ent_record"][i])) for i in range(x, y)]))
+        if out["err"]:
+            gerr = (int(out["err"]), int(out["err_record"]))
+            break
+    ctx = (seed, desc, s.path, nb)
+    if oerr is not None:
+        got = [m for m in got if m[0] < oerr[1]]
+        want = [m for m in want if m[0] < oerr[1]]
+    assert gerr == oerr, ctx
+    assert got == want, ctx
