@@ -29,9 +29,11 @@ def _pred_rich(rng):
     return _pred(rng)
 
 
-def _pred(rng):
+def _pred(rng, lowerable=False):
+    """A value predicate; `lowerable`: comparisons and their and/or/not only (the stencil lowering,
+    compile.cpp, takes no arithmetic)."""
     v = Event.value()
-    kind = rng.integers(0, 6)
+    kind = rng.choice([0, 1, 2, 4, 5]) if lowerable else rng.integers(0, 6)
     c = int(rng.integers(0, VMAX))
     if kind == 0:
         return v == c
@@ -146,3 +148,41 @@ def rich_columns(seed, key, val, ts, processor):
                 for a in (val, ts, px, r, topic, valid, offset):
                     a[i] = a[i - 3]
     return val, ts, px, r, topic, valid, offset
+
+
+def random_strict_pattern(seed):
+    """A pattern of the stencil / chain paths' class (compile.cpp analyse_stencil): 1-8 strict
+    stages on value predicates (ranges, sets, complements, and/or), optional middle stages in
+    patterns of <= 4 stages (the chain path), sometimes a window.  Returns (pattern, desc, window)."""
+    rng = np.random.default_rng(seed + 31337)
+    n = int(rng.choice(np.arange(1, 9), p=[.1, .2, .2, .2, .1, .08, .06, .06]))
+    chain = n <= 4 and rng.random() < 0.5
+    b, desc = None, []
+    for s in range(n):
+        st = QueryBuilder().select(f"s{s}") if b is None else b.then().select(f"s{s}")
+        opt = chain and 0 < s < n - 1 and rng.random() < 0.6
+        if opt:
+            st = st.optional()
+        b = st.where(_pred(rng, lowerable=True))
+        if rng.random() < 0.15:
+            b = b.or_(Event.value() == int(rng.integers(0, VMAX)))
+        desc.append(f"s{s}{'?' if opt else ''}")
+    window = None
+    if rng.random() < 0.2:
+        window = int(rng.integers(3, 20))
+        b = b.within(window, TimeUnit.MILLISECONDS)
+        desc.append(f"within {window} ms")
+    return b.build(), " ".join(desc), window
+
+
+def pattern_for(seed, variant):
+    return random_strict_pattern(seed) if variant == "strict" else random_pattern(seed)
+
+
+def stream_for(seed, variant):
+    """The strict variant's streams span several 4096-record stencil tiles (12-30 k records), so
+    that tile, super-tile and batch boundaries fall inside keys' runs."""
+    if variant == "strict":
+        n_keys, per_key = [(3000, 4), (2000, 12), (500, 60)][seed % 3]
+        return random_stream(seed, n_keys, per_key)
+    return random_stream(seed)

@@ -52,9 +52,10 @@ def _device(ir, gmode, key, val, ts, cols=None, meta=None, **opts):
     return got, err, s.path
 
 
+@pytest.mark.parametrize("variant", ["mixed", "strict"])
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_pattern_parity(seed):
-    pat, desc, _ = F.random_pattern(seed)
+def test_random_pattern_parity(seed, variant):
+    pat, desc, _ = F.pattern_for(seed, variant)
     ir = pat.to_ir(PL.I32)
     try:
         O.OraclePattern(ir)
@@ -63,7 +64,7 @@ def test_random_pattern_parity(seed):
             N.CompiledPattern(ir)
         assert ei.value.code == e.code
         return
-    key, val, ts = F.random_stream(seed)
+    key, val, ts = F.stream_for(seed, variant)
     rng = np.random.default_rng(seed)
     omode = O.MODE_PROCESSOR if rng.random() < 0.5 else O.MODE_NFA_PER_KEY
     gmode = N.MODE_PROCESSOR if omode == O.MODE_PROCESSOR else N.MODE_NFA
@@ -80,10 +81,10 @@ def test_random_pattern_parity(seed):
         assert got == w, ctx
 
 
-def _carry_stream(seed):
+def _carry_stream(seed, variant):
     """The seed's records in interleaved arrival order, timestamps rising in that order, cut into
     2-6 batches; every batch grouped by key (stable), as the host driver hands it to the device."""
-    key, val, _ = F.random_stream(seed)
+    key, val, _ = F.stream_for(seed, variant)
     rng = np.random.default_rng(seed + 104729)
     perm = rng.permutation(len(key))
     key, val = key[perm], val[perm]
@@ -94,15 +95,16 @@ def _carry_stream(seed):
     return key[order], val[order], ts[order], bounds
 
 
+@pytest.mark.parametrize("variant", ["mixed", "strict"])
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_pattern_carry_parity(seed):
-    pat, desc, _ = F.random_pattern(seed)
+def test_random_pattern_carry_parity(seed, variant):
+    pat, desc, _ = F.pattern_for(seed, variant)
     ir = pat.to_ir(PL.I32)
     try:
         O.OraclePattern(ir)
     except O.OracleError:
         pytest.skip("invalid pattern (test_random_pattern_parity checks the refusal)")
-    key, val, ts, bounds = _carry_stream(seed)
+    key, val, ts, bounds = _carry_stream(seed, variant)
     rng = np.random.default_rng(seed + 1)
     omode = O.MODE_PROCESSOR if rng.random() < 0.5 else O.MODE_NFA_PER_KEY
     gmode = N.MODE_PROCESSOR if omode == O.MODE_PROCESSOR else N.MODE_NFA
@@ -159,18 +161,19 @@ def test_random_rich_parity(seed):
         assert got == w, ctx
 
 
+@pytest.mark.parametrize("variant", ["mixed", "strict"])
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_pattern_arrival_parity(seed):
+def test_random_pattern_arrival_parity(seed, variant):
     """Processor flushes in arrival order (CEP_BATCH_ARRIVAL_ORDER, csrc/group.hip): the interleaved
     stream cut into 1-6 batches handed over ungrouped; the device groups each batch by key and returns
     the matches in the reference's forward order (CEPProcessor.java:134-150), element by element."""
-    pat, desc, _ = F.random_pattern(seed)
+    pat, desc, _ = F.pattern_for(seed, variant)
     ir = pat.to_ir(PL.I32)
     try:
         O.OraclePattern(ir)
     except O.OracleError:
         pytest.skip("invalid pattern (test_random_pattern_parity checks the refusal)")
-    key, val, _ = F.random_stream(seed)
+    key, val, _ = F.stream_for(seed, variant)
     rng = np.random.default_rng(seed + 3)
     perm = rng.permutation(len(key))
     key, val = np.ascontiguousarray(key[perm]), np.ascontiguousarray(val[perm])
