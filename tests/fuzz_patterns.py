@@ -9,7 +9,7 @@ sometimes a fold into a state the next stage reads (the stock demo's shape, Patt
 a window (within).  The same seed always gives the same pattern and stream."""
 import numpy as np
 
-from kcep import QueryBuilder, Selected, TimeUnit, Event, States, Curr, Long, Schema
+from kcep import QueryBuilder, Selected, TimeUnit, Event, States, Curr, Long, Int, Schema
 
 VMAX = 6                     # values 0..VMAX-1: small, so that predicates hit often
 # the rich variant: three typed columns and two topics (Selected.withTopic, Selected.java:19-67)
@@ -175,14 +175,68 @@ def random_strict_pattern(seed):
     return b.build(), " ".join(desc), window
 
 
+def random_runs_pattern(seed):
+    """A pattern of the runs path's class (compile.cpp analyse_runs): 2-6 strict stages, the first
+    plain; later ones plain, optional, times(n) or oneOrMore, a oneOrMore stage's successor reading
+    the complement of its predicate (provably exclusive, so no run branches); folds into states
+    (sums, counts, last values) that later predicates compare against, C3's shape
+    (NFATest.java:66-87).  Returns (pattern, desc, window)."""
+    rng = np.random.default_rng(seed + 271828)
+    n = int(rng.integers(2, 7))
+    b, desc, prev, folded = None, [], None, []
+    for s in range(n):
+        st = QueryBuilder().select(f"s{s}") if b is None else b.then().select(f"s{s}")
+        card = 0 if s == 0 or s == n - 1 else int(rng.choice([0, 1, 2, 3], p=[0.35, 0.15, 0.35, 0.15]))
+        if card == 1:
+            st = st.optional()
+        elif card == 2:
+            st = st.oneOrMore()
+        elif card == 3:
+            st = st.times(int(rng.integers(2, 4)))
+        if prev is not None:                     # successor of a oneOrMore stage
+            p = ~prev if rng.random() < 0.5 else (~prev & (Event.value() < VMAX - 1))
+        elif card == 2:
+            p = Event.value() >= int(rng.integers(1, VMAX)) if rng.random() < 0.6 else Event.value() == int(rng.integers(0, VMAX))
+        elif folded and rng.random() < 0.5:
+            nm = str(rng.choice(folded))
+            if rng.random() < 0.5:
+                p = Event.value() * 2 >= States.getOrElse(nm, Long(0)).asLong() % (2 * VMAX)
+            else:
+                p = (States.getInt("sum") / States.getInt("count")).asDouble() < Event.value() if (
+                    "sum" in folded and "count" in folded) else Event.value() != States.getOrElse(nm, Long(-1)).asLong()
+        else:
+            p = _pred(rng)
+        prev = p if card == 2 else None
+        b = st.where(p)
+        desc.append(f"s{s}{['', '?', '+', '{n}'][card]}")
+        if s < n - 1 and rng.random() < 0.35:
+            kind = int(rng.integers(0, 3))
+            if kind == 0:
+                b = b.fold("sum", (Curr.int() + Event.value()) if "sum" in folded else Event.value())
+                b = b.fold("count", (Curr.int() + 1) if "count" in folded else Int(1))
+                folded += [x for x in ("sum", "count") if x not in folded]
+            elif kind == 1:
+                b = b.fold("last", Event.value().asLong())
+                folded += [] if "last" in folded else ["last"]
+            else:
+                b = b.fold("tot", Curr.long() + Event.value()) if "tot" in folded else b.fold("tot", Event.value().asLong())
+                folded += [] if "tot" in folded else ["tot"]
+    window = None
+    if rng.random() < 0.3:
+        window = int(rng.integers(5, 40))
+        b = b.within(window, TimeUnit.MILLISECONDS)
+        desc.append(f"within {window} ms")
+    return b.build(), " ".join(desc), window
+
+
 def pattern_for(seed, variant):
-    return random_strict_pattern(seed) if variant == "strict" else random_pattern(seed)
+    return {"strict": random_strict_pattern, "runs": random_runs_pattern}.get(variant, random_pattern)(seed)
 
 
 def stream_for(seed, variant):
     """The strict variant's streams span several 4096-record stencil tiles (12-30 k records), so
     that tile, super-tile and batch boundaries fall inside keys' runs."""
-    if variant == "strict":
+    if variant in ("strict", "runs"):
         n_keys, per_key = [(3000, 4), (2000, 12), (500, 60)][seed % 3]
         return random_stream(seed, n_keys, per_key)
     return random_stream(seed)

@@ -52,7 +52,7 @@ def _device(ir, gmode, key, val, ts, cols=None, meta=None, **opts):
     return got, err, s.path
 
 
-@pytest.mark.parametrize("variant", ["mixed", "strict"])
+@pytest.mark.parametrize("variant", ["mixed", "strict", "runs"])
 @pytest.mark.parametrize("seed", SEEDS)
 def test_random_pattern_parity(seed, variant):
     pat, desc, _ = F.pattern_for(seed, variant)
@@ -95,7 +95,7 @@ def _carry_stream(seed, variant):
     return key[order], val[order], ts[order], bounds
 
 
-@pytest.mark.parametrize("variant", ["mixed", "strict"])
+@pytest.mark.parametrize("variant", ["mixed", "strict", "runs"])
 @pytest.mark.parametrize("seed", SEEDS)
 def test_random_pattern_carry_parity(seed, variant):
     pat, desc, _ = F.pattern_for(seed, variant)
@@ -161,7 +161,7 @@ def test_random_rich_parity(seed):
         assert got == w, ctx
 
 
-@pytest.mark.parametrize("variant", ["mixed", "strict"])
+@pytest.mark.parametrize("variant", ["mixed", "strict", "runs"])
 @pytest.mark.parametrize("seed", SEEDS)
 def test_random_pattern_arrival_parity(seed, variant):
     """Processor flushes in arrival order (CEP_BATCH_ARRIVAL_ORDER, csrc/group.hip): the interleaved
