@@ -7,7 +7,8 @@ traversal), and the reference's own exception (code and failing record, NFA.java
 pattern raises one, with the matches of the records before it.  The carry variant interleaves the
 keys (arrival order, as a topic partition delivers them), cuts the stream into 2-6 batches and runs
 them through one carry session (CEP_SESSION_CARRY: each key's state kept on the device between
-batches, CEPProcessor.java:111-124) against the oracle's single pass over the same records."""
+batches, CEPProcessor.java:111-124), checkpointed at a random batch boundary into a fresh session
+(state export / import), against the oracle's single pass over the same records."""
 import os
 
 import numpy as np
@@ -113,7 +114,14 @@ def test_random_pattern_carry_parity(seed, variant):
     s = N.Session(cp, max(b - a for a, b in zip(bounds[:-1], bounds[1:])), mode=gmode, carry=True,
                   max_keys=int(key.max()) + 1, lane_nfa=bool(rng.random() < 0.5))
     got, gerr = [], None
-    for a, b in zip(bounds[:-1], bounds[1:]):
+    ckpt = int(rng.integers(1, len(bounds) - 1))        # checkpoint: restore into a fresh session here
+    for j, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+        if j == ckpt:                                    # cep_state_export / cep_state_import
+            blob = s.state_export()
+            s = N.Session(cp, max(b - a for a, b in zip(bounds[:-1], bounds[1:])), mode=gmode, carry=True,
+                          max_keys=int(key.max()) + 1, lane_nfa=bool(rng.random() < 0.5))
+            s.state_import(blob)
+            assert s.stream_position() == a
         s.push(b - a, np.ascontiguousarray(key[a:b]), [np.ascontiguousarray(val[a:b])], ts=np.ascontiguousarray(ts[a:b]))
         out = s.collect(raise_on_error=False)
         for m in range(len(out["match_record"])):
