@@ -289,3 +289,75 @@ def test_random_pattern_evict_to_reference(seed, variant):
                  [(cp.names[out["ent_name"][i]], pos_rec[int(out["ent_record"][i])]) for i in range(x, y)]))
     bad = [k for k in set(got) | set(want) if got.get(k) != want.get(k)]   # (a short message: no list diff)
     assert not bad, (seed, desc, ek, cut, bad[:5], [(len(got.get(k, [])), len(want.get(k, []))) for k in bad[:5]])
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_rich_carry_parity(seed):
+    """The rich variant as a processor sees a topic partition: interleaved keys, ~5 % null records,
+    ~5 % re-deliveries of an earlier record of the same key (same offset and contents, possibly in a
+    later batch: the high-water mark carried across batches drops them, CEPProcessor.java:152-160),
+    stages reading one topic, i64/f64 predicates; 2-6 carry batches, each grouped by key, against the
+    oracle's single pass."""
+    pat, desc, _ = F.random_pattern(seed, rich=True)
+    ir = pat.to_ir(F.RICH)
+    try:
+        O.OraclePattern(ir)
+    except O.OracleError:
+        pytest.skip("invalid pattern")
+    key, val, _ = F.random_stream(seed)
+    rng = np.random.default_rng(seed + 6)
+    perm = rng.permutation(len(key))
+    key, val = key[perm], val[perm]
+    n = len(key)
+    ts = np.cumsum(rng.integers(1, 4, n)).astype(np.int64)
+    px = rng.integers(0, 6000, n).astype(np.int64)
+    r = rng.random(n)
+    topic = rng.integers(0, 2, n).astype(np.int32)
+    valid = (rng.random(n) > 0.05).astype(np.uint8)
+    off = np.arange(n, dtype=np.int64)
+    last = {}
+    for i in range(n):                                   # re-delivery: an earlier record of the key again
+        k = int(key[i])
+        if k in last and rng.random() < 0.05:
+            j = int(rng.choice(last[k][-4:]))
+            for a in (val, ts, px, r, topic, valid, off):
+                a[i] = a[j]
+        last.setdefault(k, []).append(i)
+    nb = int(rng.integers(2, 7))
+    bounds = [0] + sorted(rng.choice(np.arange(1, n), nb - 1, replace=False).tolist()) + [n]
+    order = np.concatenate([a + np.argsort(key[a:b], kind="stable") for a, b in zip(bounds[:-1], bounds[1:])])
+    key, val, ts, px, r, topic, valid, off = (x[order] for x in (key, val, ts, px, r, topic, valid, off))
+    cols = [val, px, r]
+    want, oerr = _oracle(ir, O.MODE_PROCESSOR, key, val, ts, cols=cols, coltypes=(1, 2, 3), topic=topic,
+                         valid=valid, offset=off)
+    cp = N.CompiledPattern(ir)
+    mk = lambda **o: N.Session(cp, max(b - a for a, b in zip(bounds[:-1], bounds[1:])), mode=N.MODE_PROCESSOR,
+                               carry=True, max_keys=int(key.max()) + 1, lane_nfa=bool(seed & 1), **o)
+    s = mk()
+    if s.path != N.PATH_GENERAL:
+        # the stencil / chain / runs carry sessions carry halos or tails, not per-record processor
+        # state: they refuse batches with null records or re-delivered offsets (CEP_E_UNSUPPORTED),
+        # and such a stream runs on the general path
+        a, b = bounds[0], bounds[1]
+        with pytest.raises(N.CepError, match="Unsupported"):
+            s.push(b - a, key[a:b].copy(), [c[a:b].copy() for c in cols], ts=ts[a:b].copy(), topic=topic[a:b].copy(),
+                   valid=valid[a:b].copy(), offset=off[a:b].copy())
+        s = mk(force_path=N.PATH_GENERAL)
+    got, gerr = [], None
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        sl = lambda x: np.ascontiguousarray(x[a:b])
+        s.push(b - a, sl(key), [sl(c) for c in cols], ts=sl(ts), topic=sl(topic), valid=sl(valid), offset=sl(off))
+        out = s.collect(raise_on_error=False)
+        for m in range(len(out["match_record"])):
+            x, y = out["ent_off"][m], out["ent_off"][m + 1]
+            got.append((int(out["match_record"][m]), int(out["match_key"][m]),
+                        [(cp.names[out["ent_name"][i]], int(out["ent_record"][i])) for i in range(x, y)]))
+        if out["err"]:
+            gerr = (int(out["err"]), int(out["err_record"]))
+            break
+    ctx = (seed, desc, s.path, nb)
+    if oerr is not None:
+        got = [m for m in got if m[0] < oerr[1]]
+        want = [m for m in want if m[0] < oerr[1]]
+    assert gerr == oerr, ctx
+    assert got == want, ctx
