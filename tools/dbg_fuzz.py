@@ -1,6 +1,7 @@
 """Debug one fuzz seed (tests/fuzz_patterns.py) on the GPU: the keys given, one engine option set;
 prints the oracle's and the device's error and match counts.  Usage:
-python tools/dbg_fuzz.py SEED KEYS(a:b) OPT(jit_wave|interp_lane|interp_wave|jit_lane) [MODE 1|2]"""
+python tools/dbg_fuzz.py SEED KEYS(a:b) OPT(jit_wave|interp_lane|interp_wave|jit_lane) [VARIANT mixed|strict|runs]
+[MODE 1|2]"""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "kafkastreams-cep_amd"), os.path.join(ROOT, "oracle")]
@@ -10,15 +11,16 @@ from kcep import native as N
 import fuzz_patterns as F, patterns_lib as PL
 
 seed = int(sys.argv[1]); ka, kb = map(int, sys.argv[2].split(":")); opt = sys.argv[3]
-pat, desc, _ = F.random_pattern(seed)
+variant = sys.argv[4] if len(sys.argv) > 4 else "mixed"
+pat, desc, _ = F.pattern_for(seed, variant)
 ir = pat.to_ir(PL.I32)
-key, val, ts = F.random_stream(seed)
+key, val, ts = F.stream_for(seed, variant)
 m = (key >= ka) & (key < kb)
 key, val, ts = np.ascontiguousarray(key[m]), np.ascontiguousarray(val[m]), np.ascontiguousarray(ts[m])
 rng = np.random.default_rng(seed)
 omode = O.MODE_PROCESSOR if rng.random() < 0.5 else O.MODE_NFA_PER_KEY
-if len(sys.argv) > 4:
-    omode = int(sys.argv[4])
+if len(sys.argv) > 5:
+    omode = int(sys.argv[5])
 gmode = N.MODE_PROCESSOR if omode == O.MODE_PROCESSOR else N.MODE_NFA
 p = O.OraclePattern(ir); r = O.OracleRun(p, omode); oerr = None
 try:
