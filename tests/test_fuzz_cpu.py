@@ -1,6 +1,8 @@
 """Random patterns (tests/fuzz_patterns.py): the product's pattern compiler (libkcep.so, host code)
 accepts exactly the patterns the oracle accepts, with the same error class for the rest
-(StagesFactory.java InvalidPatternException), and the generator is deterministic."""
+(StagesFactory.java InvalidPatternException), the generator is deterministic, and the default GPU
+suite's seeds stay small per key."""
+import numpy as np
 import pytest
 
 import oracle as O
@@ -38,3 +40,29 @@ def test_compile_validity_matches_oracle():
         assert oerr == gerr, (seed, desc, oerr, gerr)
         seen["ok" if oerr is None else "invalid"] += 1
     assert seen["ok"] > 200 and seen["invalid"] > 5, seen
+
+
+@pytest.mark.parametrize("variant", ["mixed", "strict", "runs"])
+def test_default_seeds_stay_bounded(variant):
+    """The default GPU suite's seeds (test_fuzz_gpu.py, 0-11) run in seconds: the device evaluates
+    every key even where the reference task would stop at an earlier key's exception, so each key on
+    its own must stay small (the generator keeps skipping strategies off open-ended repeats on long
+    keys; one unbounded seed once took the device past its test timeout)."""
+    for seed in range(12):
+        pat, desc, _ = F.pattern_for(seed, variant)
+        ir = pat.to_ir(PL.I32)
+        try:
+            p = O.OraclePattern(ir)
+        except O.OracleError:
+            continue
+        key, val, ts = F.stream_for(seed, variant)
+        worst = 0
+        for k in np.unique(key):
+            m = key == k
+            r = O.OracleRun(p, O.MODE_NFA_PER_KEY)
+            try:
+                r.process(O.BatchArrays(key[m], [val[m]], [1], ts=ts[m]))
+            except O.OracleError:
+                pass
+            worst = max(worst, len(r.matches(with_groups=False)))
+        assert worst < 5000, (seed, desc, worst)
